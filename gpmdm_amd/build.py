@@ -1,0 +1,68 @@
+"""Build libgpmdm_hip.so in-tree (hipcc, gfx950 only).
+
+    python -m gpmdm_amd.build          # or __graft_entry__.build()
+
+Each translation unit is compiled with ``hipcc --offload-arch=gfx950 -O3`` and linked
+into ``gpmdm_amd/libgpmdm_hip.so``; objects go to ``gpmdm_amd/_build/``.  Rebuilds only
+what changed (source or header newer than the object).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+OBJ = PKG / "_build"
+LIB = PKG / "libgpmdm_hip.so"
+SOURCES = ["gp_tile.hip", "pf_kernels.hip", "capi.hip"]
+HEADERS = [CSRC / "common.h", CSRC / "pf_kernels.h", ROOT / "include" / "gpmdm_hip.h"]
+ARCH = "gfx950"
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (ROCm is required to build libgpmdm_hip.so)")
+
+
+def _flags():
+    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+            "-Wno-unused-function", "-munsafe-fp-atomics", f"-I{ROOT / 'include'}"]
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    OBJ.mkdir(exist_ok=True)
+    cc = hipcc()
+    newest_hdr = max(h.stat().st_mtime for h in HEADERS)
+    jobs = []
+    for src in SOURCES:
+        s = CSRC / src
+        o = OBJ / (src + ".o")
+        if force or not o.exists() or o.stat().st_mtime < max(s.stat().st_mtime, newest_hdr):
+            jobs.append([cc, *_flags(), "-c", str(s), "-o", str(o)])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        return r
+
+    with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        list(ex.map(run, jobs))
+    objs = [str(OBJ / (s + ".o")) for s in SOURCES]
+    if force or jobs or not LIB.exists():
+        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *objs])
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,845 @@
+// C ABI of libgpmdm_hip.so (include/gpmdm_hip.h): model and particle-filter handles,
+// device memory layout, and the per-frame launch sequence.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gpmdm_hip.h"
+#include "common.h"
+#include "pf_kernels.h"
+
+using namespace gpmdm;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(GPMDM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));         \
+  } while (0)
+
+#define CHECK(cond, msg)                                                                   \
+  do {                                                                                     \
+    if (!(cond)) return fail(GPMDM_E_INVALID, msg);                                        \
+  } while (0)
+
+#define TRY(expr)                                                                          \
+  do {                                                                                     \
+    int rc_ = (expr);                                                                      \
+    if (rc_ != GPMDM_OK) return rc_;                                                       \
+  } while (0)
+
+template <typename T>
+int dalloc(T** p, size_t n) {
+  *p = nullptr;
+  if (n == 0) n = 1;
+  hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+  if (e != hipSuccess) return fail(GPMDM_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  return GPMDM_OK;
+}
+
+template <typename T>
+void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
+
+bool supported_d(int d) { return (d >= 1 && d <= 16) || d == 24 || d == 32; }
+
+// One GP's device image: scaled inputs, raw inputs, and B = [R | M] zero padded.
+struct GpImage {
+  int n_rows = 0, n_m = 0, n_j = 0, k_pad = 0;
+  long long ld = 0;
+  double* Xs = nullptr;   // n_rows x d, inputs / lengthscales
+  double* Xl = nullptr;   // n_rows x d, raw inputs (dynamics)
+  double* B = nullptr;
+
+  void release() {
+    dfree(Xs);
+    dfree(Xl);
+    dfree(B);
+  }
+  SegDesc seg() const {
+    SegDesc s{};
+    s.Xs = Xs;
+    s.Xl = Xl;
+    s.B = B;
+    s.ld = ld;
+    s.n_rows = n_rows;
+    s.n_m = n_m;
+    s.n_j = n_j;
+    return s;
+  }
+  int n_parts() const { return 2 * (int)cdiv(n_rows, kNT); }
+};
+
+// Build B = [triu(R) | M] in row chunks and upload it; inputs scaled by the lengthscales.
+int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const double* ls,
+                bool keep_raw, const double* R, const double* M) {
+  g.n_rows = n_rows;
+  g.n_m = n_m;
+  g.ld = cdiv(n_rows + n_m, kNT) * kNT;
+  g.n_j = (int)(g.ld / kNT);
+  g.k_pad = (int)(cdiv(n_rows, kBK) * kBK);
+  std::vector<double> xs((size_t)n_rows * d);
+  for (long long i = 0; i < n_rows; ++i)
+    for (int j = 0; j < d; ++j) xs[i * d + j] = X[i * d + j] / ls[j];
+  TRY(dalloc(&g.Xs, xs.size()));
+  HIPCHK(hipMemcpy(g.Xs, xs.data(), xs.size() * sizeof(double), hipMemcpyHostToDevice));
+  if (keep_raw) {
+    TRY(dalloc(&g.Xl, (size_t)n_rows * d));
+    HIPCHK(hipMemcpy(g.Xl, X, (size_t)n_rows * d * sizeof(double), hipMemcpyHostToDevice));
+  }
+  TRY(dalloc(&g.B, (size_t)g.k_pad * g.ld));
+  HIPCHK(hipMemset(g.B, 0, (size_t)g.k_pad * g.ld * sizeof(double)));
+  const long long chunk = 512;
+  std::vector<double> buf((size_t)chunk * g.ld);
+  for (long long r0 = 0; r0 < n_rows; r0 += chunk) {
+    const long long nr = std::min(chunk, (long long)n_rows - r0);
+    std::fill(buf.begin(), buf.begin() + nr * g.ld, 0.0);
+    for (long long r = 0; r < nr; ++r) {
+      const long long i = r0 + r;
+      double* row = buf.data() + r * g.ld;
+      for (long long j = i; j < n_rows; ++j) row[j] = R[i * n_rows + j];   // upper triangle only
+      for (int j = 0; j < n_m; ++j) row[n_rows + j] = M[i * n_m + j];
+    }
+    HIPCHK(hipMemcpy(g.B + r0 * g.ld, buf.data(), (size_t)nr * g.ld * sizeof(double), hipMemcpyHostToDevice));
+  }
+  return GPMDM_OK;
+}
+
+}  // namespace
+
+// =====================================================================================
+struct gpmdm_model {
+  int device = 0;
+  long long N = 0;
+  int D = 0, d = 0, C = 0;
+  std::vector<double> X;              // host copy, N x d
+  std::vector<double> y_ls, x_ls, x_lin_c2, x_il2, y_il2;
+  GpImage obs;
+  std::vector<GpImage> dyn;
+  double* y_il2_dev = nullptr;
+  // predictive-map scratch
+  int* tab = nullptr;                 // 5 ints: begin, end, out_base, tile_start[2]
+  double* qscratch = nullptr;
+  size_t qcap = 0;
+
+  ~gpmdm_model() {
+    obs.release();
+    for (auto& g : dyn) g.release();
+    dfree(y_il2_dev);
+    dfree(tab);
+    dfree(qscratch);
+  }
+  int ensure_q(size_t n) {
+    if (n <= qcap) return GPMDM_OK;
+    dfree(qscratch);
+    TRY(dalloc(&qscratch, n));
+    qcap = n;
+    return GPMDM_OK;
+  }
+};
+
+struct gpmdm_pf {
+  gpmdm_model* m = nullptr;
+  long long P = 0, lo = 0, hi = 0, nloc = 0;
+  int n_ranks = 1, rank = 0, rng_mode = 0, resample_mode = 0, nb = 0;
+  unsigned seed_lo = 0, seed_hi = 0, frame = 0;
+  bool initialised = false, switched = false, propagated = false;
+  // device state
+  double *T = nullptr, *X = nullptr, *X_prop = nullptr, *ll = nullptr;
+  int *cls = nullptr, *cls_new = nullptr, *perm = nullptr, *ridx = nullptr;
+  int *blockcounts = nullptr, *blockoff = nullptr, *small = nullptr;   // small: class tables
+  int *obs_tab = nullptr;
+  double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *muobs = nullptr;
+  int nparts_dyn_max = 0;
+  double *z = nullptr, *E = nullptr, *normals = nullptr, *U = nullptr;
+  unsigned long long* gmax = nullptr;
+  double *e = nullptr, *local = nullptr, *blocksum = nullptr, *blockoffw = nullptr, *total = nullptr,
+         *cum = nullptr, *partials = nullptr, *readout = nullptr;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> pool;
+  struct Rec { int stage; hipEvent_t a, b; };
+  std::vector<Rec> recs;
+
+  int* class_start() const { return small; }
+  int* counts() const { return small + 40; }
+  int* seg_begin() const { return small + 80; }
+  int* seg_end() const { return small + 120; }
+  int* seg_out() const { return small + 160; }
+  int* seg_tiles() const { return small + 200; }
+
+  ~gpmdm_pf() {
+    double* ds[] = {T, X, X_prop, ll, qdyn, mudyn, qobs, muobs, z, E, normals, U,
+                    e, local, blocksum, blockoffw, total, cum, partials, readout};
+    for (double* p : ds) dfree(p);
+    int* is[] = {cls, cls_new, perm, ridx, blockcounts, blockoff, small, obs_tab};
+    for (int* p : is) dfree(p);
+    dfree(gmax);
+    for (auto& r : recs) { pool.push_back(r.a); pool.push_back(r.b); }
+    for (auto ev : pool) (void)hipEventDestroy(ev);
+  }
+
+  hipEvent_t ev() {
+    if (!pool.empty()) { hipEvent_t x = pool.back(); pool.pop_back(); return x; }
+    hipEvent_t x = nullptr;
+    (void)hipEventCreate(&x);
+    return x;
+  }
+  void mark_begin(hipStream_t s, hipEvent_t& a) {
+    a = nullptr;
+    if (timing) { a = ev(); (void)hipEventRecord(a, s); }
+  }
+  void mark_end(hipStream_t s, int stage, hipEvent_t a) {
+    if (!timing || !a) return;
+    hipEvent_t b = ev();
+    (void)hipEventRecord(b, s);
+    recs.push_back({stage, a, b});
+  }
+};
+
+// =====================================================================================
+extern "C" {
+
+const char* gpmdm_last_error(void) { return g_err.c_str(); }
+const char* gpmdm_version(void) { return "gpmdm_hip 0.1.0 (gfx950, fp64 MFMA)"; }
+
+int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* out) {
+  CHECK(desc && out, "null argument");
+  *out = nullptr;
+  CHECK(desc->N > 0 && desc->D > 0 && desc->C > 0, "N, D and C must be positive");
+  CHECK(supported_d(desc->d), "latent dimension d must be 1..16, 24 or 32");
+  CHECK(desc->C <= kMaxClasses, "at most 32 classes");
+  CHECK(desc->N < (1ll << 30), "N too large");
+  CHECK(desc->X && desc->obs_R && desc->obs_beta && desc->y_lengthscales && desc->y_inv_lambda2 &&
+            desc->Nc && desc->Xin && desc->dyn_R && desc->dyn_alpha && desc->x_lengthscales &&
+            desc->x_lin_coeff2 && desc->x_inv_lambda2,
+        "null array in model descriptor");
+  HIPCHK(hipSetDevice(device));
+  auto* m = new gpmdm_model();
+  m->device = device;
+  m->N = desc->N;
+  m->D = desc->D;
+  m->d = desc->d;
+  m->C = desc->C;
+  const int d = m->d;
+  m->X.assign(desc->X, desc->X + desc->N * d);
+  m->y_ls.assign(desc->y_lengthscales, desc->y_lengthscales + d);
+  m->y_il2.assign(desc->y_inv_lambda2, desc->y_inv_lambda2 + m->D);
+  m->x_ls.assign(desc->x_lengthscales, desc->x_lengthscales + d);
+  m->x_lin_c2.assign(desc->x_lin_coeff2, desc->x_lin_coeff2 + d + 1);
+  m->x_il2.assign(desc->x_inv_lambda2, desc->x_inv_lambda2 + d);
+  int rc = build_image(m->obs, (int)m->N, d, m->D, desc->X, desc->y_lengthscales, false,
+                       desc->obs_R, desc->obs_beta);
+  if (rc) { delete m; return rc; }
+  m->dyn.resize(m->C);
+  for (int c = 0; c < m->C; ++c) {
+    if (desc->Nc[c] <= 0 || !desc->Xin[c] || !desc->dyn_R[c] || !desc->dyn_alpha[c]) {
+      delete m;
+      return fail(GPMDM_E_INVALID, "class " + std::to_string(c) + " has no dynamics rows");
+    }
+    rc = build_image(m->dyn[c], (int)desc->Nc[c], d, d, desc->Xin[c], desc->x_lengthscales, true,
+                     desc->dyn_R[c], desc->dyn_alpha[c]);
+    if (rc) { delete m; return rc; }
+  }
+  rc = dalloc(&m->y_il2_dev, m->D);
+  if (rc) { delete m; return rc; }
+  if (hipMemcpy(m->y_il2_dev, m->y_il2.data(), m->D * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+    delete m;
+    return fail(GPMDM_E_HIP, "upload y_inv_lambda2");
+  }
+  rc = dalloc(&m->tab, 8);
+  if (rc) { delete m; return rc; }
+  *out = m;
+  return GPMDM_OK;
+}
+
+int gpmdm_model_destroy(gpmdm_model_t m) {
+  delete m;
+  return GPMDM_OK;
+}
+
+// ------------------------------------------------------------------------------------
+static void fill_tile_common(TileParams& tp, const gpmdm_model* m, bool dyn) {
+  const int d = m->d;
+  for (int j = 0; j < d; ++j) tp.ls[j] = dyn ? m->x_ls[j] : m->y_ls[j];
+  if (dyn)
+    for (int j = 0; j <= d; ++j) tp.lin_c2[j] = m->x_lin_c2[j];
+}
+
+int gpmdm_predict_obs(gpmdm_model_t m, const double* Xs, int64_t n, double* mu, double* var, void* stream) {
+  CHECK(m, "null model");
+  CHECK(n >= 0 && n < (1ll << 31), "bad n");
+  if (n == 0) return GPMDM_OK;
+  CHECK(Xs && mu && var, "null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(m->device));
+  const int nparts = m->obs.n_parts();
+  TRY(m->ensure_q((size_t)nparts * n));
+  const int tab[5] = {0, (int)n, 0, 0, (int)cdiv(n, kPT)};
+  HIPCHK(hipMemcpyAsync(m->tab, tab, sizeof(tab), hipMemcpyHostToDevice, s));
+  TileParams tp{};
+  tp.seg[0] = m->obs.seg();
+  tp.n_seg = 1;
+  tp.tiles_ub = (int)cdiv(n, kPT);
+  tp.n_j_max = m->obs.n_j;
+  tp.seg_pos_begin = m->tab + 0;
+  tp.seg_pos_end = m->tab + 1;
+  tp.seg_out_base = m->tab + 2;
+  tp.seg_tile_start = m->tab + 3;
+  tp.perm = nullptr;
+  tp.X = Xs;
+  fill_tile_common(tp, m, false);
+  tp.qpart = m->qscratch;
+  tp.ld_q = n;
+  tp.mu = mu;
+  tp.ld_mu = m->D;
+  launch_gp_tile(tp, m->d, false, s);
+  ObsFinishArgs fa{};
+  fa.n_out = n;
+  fa.n_parts = nparts;
+  fa.D = m->D;
+  fa.qpart = m->qscratch;
+  fa.ld_q = n;
+  fa.mu = mu;
+  fa.ld_mu = m->D;
+  fa.il2 = m->y_il2_dev;
+  fa.var_out = var;
+  launch_obs_finish(fa, s);
+  HIPCHK(hipGetLastError());
+  return GPMDM_OK;
+}
+
+int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, double* mu, double* var, void* stream) {
+  CHECK(m, "null model");
+  CHECK(c >= 0 && c < m->C, "class index out of range");
+  CHECK(n >= 0 && n < (1ll << 31), "bad n");
+  if (n == 0) return GPMDM_OK;
+  CHECK(Xs && mu && var, "null buffer");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(m->device));
+  const GpImage& g = m->dyn[c];
+  const int nparts = g.n_parts();
+  TRY(m->ensure_q((size_t)nparts * n));
+  const int tab[5] = {0, (int)n, 0, 0, (int)cdiv(n, kPT)};
+  HIPCHK(hipMemcpyAsync(m->tab, tab, sizeof(tab), hipMemcpyHostToDevice, s));
+  TileParams tp{};
+  tp.seg[0] = g.seg();
+  tp.n_seg = 1;
+  tp.tiles_ub = (int)cdiv(n, kPT);
+  tp.n_j_max = g.n_j;
+  tp.seg_pos_begin = m->tab + 0;
+  tp.seg_pos_end = m->tab + 1;
+  tp.seg_out_base = m->tab + 2;
+  tp.seg_tile_start = m->tab + 3;
+  tp.X = Xs;
+  fill_tile_common(tp, m, true);
+  tp.qpart = m->qscratch;
+  tp.ld_q = n;
+  tp.mu = mu;
+  tp.ld_mu = m->d;
+  launch_gp_tile(tp, m->d, true, s);
+  DynFinishArgs fa{};
+  fa.n_out = n;
+  fa.n_seg = 1;
+  fa.d = m->d;
+  fa.n_parts[0] = nparts;
+  fa.qpart = m->qscratch;
+  fa.ld_q = n;
+  fa.mu = mu;
+  fa.ld_mu = m->d;
+  fa.X = Xs;
+  for (int j = 0; j <= m->d; ++j) fa.lin_c2[j] = m->x_lin_c2[j];
+  for (int j = 0; j < m->d; ++j) fa.il2[j] = m->x_il2[j];
+  fa.var_out = var;
+  launch_dyn_finish(fa, s);
+  HIPCHK(hipGetLastError());
+  return GPMDM_OK;
+}
+
+// ------------------------------------------------------------------------------------
+int gpmdm_pf_create(gpmdm_model_t m, const double* T, int64_t P, int rng_mode, uint64_t seed,
+                    int resample_mode, int n_ranks, int rank, gpmdm_pf_t* out) {
+  CHECK(m && T && out, "null argument");
+  *out = nullptr;
+  CHECK(P >= 1 && P < (1ll << 31) - 256, "num_particles out of range");
+  CHECK(rng_mode == GPMDM_RNG_REPLAY || rng_mode == GPMDM_RNG_PHILOX, "bad rng mode");
+  CHECK(resample_mode == GPMDM_RESAMPLE_MULTINOMIAL || resample_mode == GPMDM_RESAMPLE_SYSTEMATIC,
+        "bad resample mode");
+  CHECK(n_ranks >= 1 && rank >= 0 && rank < n_ranks, "bad rank");
+  HIPCHK(hipSetDevice(m->device));
+  auto* pf = new gpmdm_pf();
+  pf->m = m;
+  pf->P = P;
+  pf->n_ranks = n_ranks;
+  pf->rank = rank;
+  pf->lo = P * rank / n_ranks;
+  pf->hi = P * (rank + 1) / n_ranks;
+  pf->nloc = pf->hi - pf->lo;
+  pf->rng_mode = rng_mode;
+  pf->resample_mode = resample_mode;
+  pf->seed_lo = (unsigned)(seed & 0xffffffffu);
+  pf->seed_hi = (unsigned)(seed >> 32);
+  pf->nb = (int)cdiv(P, 256);
+  const int C = m->C, d = m->d, D = m->D;
+  int maxparts = 0;
+  for (auto& g : m->dyn) maxparts = std::max(maxparts, g.n_parts());
+  pf->nparts_dyn_max = maxparts;
+  const long long nl = std::max(pf->nloc, 1ll);
+  int rc = 0;
+#define ALLOC(ptr, n) do { rc = dalloc(&pf->ptr, (size_t)(n)); if (rc) { delete pf; return rc; } } while (0)
+  ALLOC(T, C * C);
+  ALLOC(X, P * d);
+  ALLOC(X_prop, P * d);
+  ALLOC(ll, P);
+  ALLOC(cls, P);
+  ALLOC(cls_new, P);
+  ALLOC(perm, P);
+  ALLOC(ridx, P);
+  ALLOC(blockcounts, (long long)pf->nb * C);
+  ALLOC(blockoff, (long long)pf->nb * C);
+  ALLOC(small, 256);
+  ALLOC(obs_tab, 8);
+  ALLOC(qdyn, (long long)maxparts * nl);
+  ALLOC(mudyn, nl * d);
+  ALLOC(qobs, (long long)m->obs.n_parts() * nl);
+  ALLOC(muobs, nl * D);
+  ALLOC(z, D);
+  if (rng_mode == GPMDM_RNG_REPLAY) {
+    ALLOC(E, P * C);
+    ALLOC(normals, P * d);
+    ALLOC(U, P);
+  }
+  ALLOC(gmax, 1);
+  ALLOC(e, P);
+  ALLOC(local, P);
+  ALLOC(blocksum, pf->nb);
+  ALLOC(blockoffw, pf->nb);
+  ALLOC(total, 1);
+  ALLOC(cum, P);
+  ALLOC(partials, (long long)pf->nb * (C + 1 + d));
+  ALLOC(readout, C + d + 1);
+#undef ALLOC
+  const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, kPT)};
+  if (hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(pf->T, T, sizeof(double) * C * C, hipMemcpyHostToDevice) != hipSuccess) {
+    delete pf;
+    return fail(GPMDM_E_HIP, "upload of particle-filter tables failed");
+  }
+  *out = pf;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_destroy(gpmdm_pf_t pf) {
+  delete pf;
+  return GPMDM_OK;
+}
+
+static ResampleArgs resample_args(gpmdm_pf* pf) {
+  const gpmdm_model* m = pf->m;
+  ResampleArgs ra{};
+  ra.P = pf->P;
+  ra.nb = pf->nb;
+  ra.C = m->C;
+  ra.d = m->d;
+  ra.systematic = pf->resample_mode == GPMDM_RESAMPLE_SYSTEMATIC;
+  ra.frame = pf->frame;
+  ra.seed_lo = pf->seed_lo;
+  ra.seed_hi = pf->seed_hi;
+  ra.cum = pf->cum;
+  ra.ll = pf->ll;
+  ra.e = pf->e;
+  ra.total = pf->total;
+  ra.gmax = pf->gmax;
+  ra.cls_src = pf->cls_new;
+  ra.X_src = pf->X_prop;
+  ra.cls_dst = pf->cls;
+  ra.X_dst = pf->X;
+  ra.ridx = pf->ridx;
+  ra.partials = pf->partials;
+  ra.readout = pf->readout;
+  return ra;
+}
+
+static NormArgs norm_args(gpmdm_pf* pf) {
+  NormArgs na{};
+  na.P = pf->P;
+  na.nb = pf->nb;
+  na.ll = pf->ll;
+  na.gmax = pf->gmax;
+  na.e = pf->e;
+  na.local = pf->local;
+  na.blocksum = pf->blocksum;
+  na.blockoff = pf->blockoffw;
+  na.total = pf->total;
+  na.cum = pf->cum;
+  return na;
+}
+
+int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
+  CHECK(pf && states && classes, "null argument");
+  gpmdm_model* m = pf->m;
+  HIPCHK(hipSetDevice(m->device));
+  const long long P = pf->P;
+  std::vector<int> c32(P);
+  for (long long i = 0; i < P; ++i) {
+    CHECK(classes[i] >= 0 && classes[i] < m->C, "class id out of range");
+    c32[i] = (int)classes[i];
+  }
+  HIPCHK(hipMemcpy(pf->X, states, sizeof(double) * P * m->d, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(pf->cls, c32.data(), sizeof(int) * P, hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(pf->ll, 0, sizeof(double) * P));
+  const unsigned long long neg = 0x000fffffffffffffull;   // ord_enc(-inf)
+  HIPCHK(hipMemcpy(pf->gmax, &neg, sizeof(neg), hipMemcpyHostToDevice));
+  // read-outs of the initial state: ll = log_w = 0, w = 1/P (gpmdm_pf.py:102-104)
+  launch_normalise(norm_args(pf), nullptr);
+  ResampleArgs ra = resample_args(pf);
+  ra.identity = 1;
+  ra.cls_src = pf->cls;
+  ra.X_src = pf->X;
+  launch_resample(ra, nullptr);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  pf->initialised = true;
+  pf->switched = pf->propagated = false;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void* stream) {
+  CHECK(pf, "null handle");
+  if (!pf->initialised) return fail(GPMDM_E_STATE, "particle filter not initialised");
+  gpmdm_model* m = pf->m;
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(m->device));
+  const int C = m->C;
+  if (pf->rng_mode == GPMDM_RNG_REPLAY) {
+    CHECK(E, "replay mode needs the Exp(1) switch draws");
+    HIPCHK(hipMemcpyAsync(pf->E, E, sizeof(double) * pf->P * C, hipMemcpyHostToDevice, s));
+  }
+  hipEvent_t t0;
+  pf->mark_begin(s, t0);
+  SwitchArgs sa{};
+  sa.P = pf->P;
+  sa.C = C;
+  sa.frame = pf->frame;
+  sa.seed_lo = pf->seed_lo;
+  sa.seed_hi = pf->seed_hi;
+  sa.cls = pf->cls;
+  sa.cls_new = pf->cls_new;
+  sa.T = pf->T;
+  sa.E = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->E : nullptr;
+  sa.blockcounts = pf->blockcounts;
+  sa.gmax_reset = pf->gmax;
+  launch_switch(sa, s);
+  ScanArgs sc{};
+  sc.nb = pf->nb;
+  sc.C = C;
+  sc.lo = pf->lo;
+  sc.hi = pf->hi;
+  sc.blockcounts = pf->blockcounts;
+  sc.cls_new = pf->cls_new;
+  sc.blockoff = pf->blockoff;
+  sc.class_start = pf->class_start();
+  sc.counts = pf->counts();
+  sc.seg_pos_begin = pf->seg_begin();
+  sc.seg_pos_end = pf->seg_end();
+  sc.seg_out_base = pf->seg_out();
+  sc.seg_tile_start = pf->seg_tiles();
+  launch_scan_counts(sc, s);
+  GroupArgs ga{};
+  ga.P = pf->P;
+  ga.C = C;
+  ga.cls_new = pf->cls_new;
+  ga.class_start = pf->class_start();
+  ga.blockoff = pf->blockoff;
+  ga.perm = pf->perm;
+  launch_group(ga, s);
+  pf->mark_end(s, GPMDM_STAGE_SWITCH, t0);
+  HIPCHK(hipGetLastError());
+  if (class_counts) {
+    int tmp[kMaxClasses];
+    HIPCHK(hipMemcpyAsync(tmp, pf->counts(), sizeof(int) * C, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int c = 0; c < C; ++c) class_counts[c] = tmp[c];
+  }
+  pf->switched = true;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, void* stream) {
+  CHECK(pf && zh, "null argument");
+  if (!pf->switched) return fail(GPMDM_E_STATE, "propagate called before switch");
+  gpmdm_model* m = pf->m;
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(m->device));
+  const int C = m->C, d = m->d, D = m->D;
+  HIPCHK(hipMemcpyAsync(pf->z, zh, sizeof(double) * D, hipMemcpyHostToDevice, s));
+  if (pf->rng_mode == GPMDM_RNG_REPLAY) {
+    CHECK(normals, "replay mode needs the dynamics normals");
+    HIPCHK(hipMemcpyAsync(pf->normals, normals, sizeof(double) * pf->P * d, hipMemcpyHostToDevice, s));
+  }
+  const long long nl = pf->nloc;
+  if (nl > 0) {
+    // ---- dynamics GP per class (segments of at most kMaxSeg classes per launch) ----
+    hipEvent_t t0;
+    pf->mark_begin(s, t0);
+    for (int c0 = 0; c0 < C; c0 += kMaxSeg) {
+      const int ns = std::min(kMaxSeg, C - c0);
+      TileParams tp{};
+      int njm = 0;
+      for (int k = 0; k < ns; ++k) {
+        tp.seg[k] = m->dyn[c0 + k].seg();
+        njm = std::max(njm, m->dyn[c0 + k].n_j);
+      }
+      tp.n_seg = ns;
+      tp.tiles_ub = (int)(cdiv(nl, kPT) + ns);
+      tp.n_j_max = njm;
+      tp.seg_pos_begin = pf->seg_begin() + c0;
+      tp.seg_pos_end = pf->seg_end() + c0;
+      tp.seg_out_base = pf->seg_out() + c0;
+      tp.seg_tile_start = pf->seg_tiles() + c0;
+      tp.perm = pf->perm;
+      tp.X = pf->X;
+      fill_tile_common(tp, m, true);
+      tp.qpart = pf->qdyn;
+      tp.ld_q = nl;
+      tp.mu = pf->mudyn;
+      tp.ld_mu = d;
+      launch_gp_tile(tp, d, true, s);
+    }
+    pf->mark_end(s, GPMDM_STAGE_DYN_GEMM, t0);
+    pf->mark_begin(s, t0);
+    DynFinishArgs fa{};
+    fa.n_out = nl;
+    fa.n_seg = C;
+    fa.d = d;
+    fa.frame = pf->frame;
+    fa.seed_lo = pf->seed_lo;
+    fa.seed_hi = pf->seed_hi;
+    fa.seg_out_base = pf->seg_out();
+    fa.seg_pos_begin = pf->seg_begin();
+    fa.perm = pf->perm;
+    for (int c = 0; c < C; ++c) fa.n_parts[c] = m->dyn[c].n_parts();
+    fa.qpart = pf->qdyn;
+    fa.ld_q = nl;
+    fa.mu = pf->mudyn;
+    fa.ld_mu = d;
+    fa.X = pf->X;
+    for (int j = 0; j <= d; ++j) fa.lin_c2[j] = m->x_lin_c2[j];
+    for (int j = 0; j < d; ++j) fa.il2[j] = m->x_il2[j];
+    fa.normals = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->normals : nullptr;
+    fa.X_out = pf->X_prop;
+    launch_dyn_finish(fa, s);
+    pf->mark_end(s, GPMDM_STAGE_DYN_FINISH, t0);
+
+    // ---- observation GP + likelihood over particles [lo, hi) ----
+    pf->mark_begin(s, t0);
+    TileParams tp{};
+    tp.seg[0] = m->obs.seg();
+    tp.n_seg = 1;
+    tp.tiles_ub = (int)cdiv(nl, kPT);
+    tp.n_j_max = m->obs.n_j;
+    tp.seg_pos_begin = pf->obs_tab + 0;
+    tp.seg_pos_end = pf->obs_tab + 1;
+    tp.seg_out_base = pf->obs_tab + 2;
+    tp.seg_tile_start = pf->obs_tab + 3;
+    tp.perm = nullptr;
+    tp.X = pf->X_prop;
+    fill_tile_common(tp, m, false);
+    tp.qpart = pf->qobs;
+    tp.ld_q = nl;
+    tp.mu = pf->muobs;
+    tp.ld_mu = D;
+    launch_gp_tile(tp, d, false, s);
+    pf->mark_end(s, GPMDM_STAGE_OBS_GEMM, t0);
+    pf->mark_begin(s, t0);
+    ObsFinishArgs oa{};
+    oa.n_out = nl;
+    oa.n_parts = m->obs.n_parts();
+    oa.D = D;
+    oa.qpart = pf->qobs;
+    oa.ld_q = nl;
+    oa.mu = pf->muobs;
+    oa.ld_mu = D;
+    oa.z = pf->z;
+    oa.il2 = m->y_il2_dev;
+    oa.ll_const = (double)((float)(0.5 * D) * (float)1.8378770351409912);
+    oa.ll = pf->ll;
+    oa.ll_offset = pf->lo;
+    launch_obs_finish(oa, s);
+    pf->mark_end(s, GPMDM_STAGE_OBS_FINISH, t0);
+  }
+  HIPCHK(hipGetLastError());
+  pf->propagated = true;
+  pf->switched = false;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_exchange_width(gpmdm_pf_t pf, int64_t* width, int64_t* lo, int64_t* hi) {
+  CHECK(pf, "null handle");
+  if (width) *width = pf->m->d + 2;
+  if (lo) *lo = pf->lo;
+  if (hi) *hi = pf->hi;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_pack(gpmdm_pf_t pf, double* send, void* stream) {
+  CHECK(pf && send, "null argument");
+  HIPCHK(hipSetDevice(pf->m->device));
+  PackArgs a{};
+  a.n = pf->nloc;
+  a.lo = pf->lo;
+  a.d = pf->m->d;
+  a.buf = send;
+  a.ll = pf->ll;
+  a.cls = pf->cls_new;
+  a.X = pf->X_prop;
+  launch_pack(a, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_unpack(gpmdm_pf_t pf, const double* recv, void* stream) {
+  CHECK(pf && recv, "null argument");
+  HIPCHK(hipSetDevice(pf->m->device));
+  PackArgs a{};
+  a.n = pf->P;
+  a.lo = 0;
+  a.d = pf->m->d;
+  a.buf = const_cast<double*>(recv);
+  a.ll = pf->ll;
+  a.cls = pf->cls_new;
+  a.X = pf->X_prop;
+  launch_unpack(a, (hipStream_t)stream);
+  HIPCHK(hipGetLastError());
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
+  CHECK(pf, "null handle");
+  if (!pf->propagated) return fail(GPMDM_E_STATE, "resample called before propagate");
+  gpmdm_model* m = pf->m;
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(m->device));
+  const bool sys = pf->resample_mode == GPMDM_RESAMPLE_SYSTEMATIC;
+  if (pf->rng_mode == GPMDM_RNG_REPLAY) {
+    CHECK(uniforms, "replay mode needs the resampling uniforms");
+    HIPCHK(hipMemcpyAsync(pf->U, uniforms, sizeof(double) * (sys ? 1 : pf->P), hipMemcpyHostToDevice, s));
+  }
+  hipEvent_t t0;
+  pf->mark_begin(s, t0);
+  launch_normalise(norm_args(pf), s);
+  ResampleArgs ra = resample_args(pf);
+  ra.U = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->U : nullptr;
+  launch_resample(ra, s);
+  pf->mark_end(s, GPMDM_STAGE_RESAMPLE, t0);
+  HIPCHK(hipGetLastError());
+  pf->frame += 1;
+  pf->propagated = false;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_step(gpmdm_pf_t pf, const double* zh, const double* E, const double* normals,
+                  const double* uniforms, void* stream) {
+  CHECK(pf, "null handle");
+  CHECK(pf->n_ranks == 1, "gpmdm_pf_step is single-rank; use switch/propagate/pack/unpack/resample");
+  TRY(gpmdm_pf_switch(pf, E, nullptr, stream));
+  TRY(gpmdm_pf_propagate(pf, zh, normals, stream));
+  TRY(gpmdm_pf_resample(pf, uniforms, stream));
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_read(gpmdm_pf_t pf, double* post, double* mean, double* lik, void* stream) {
+  CHECK(pf, "null handle");
+  if (!pf->initialised) return fail(GPMDM_E_STATE, "particle filter not initialised");
+  const gpmdm_model* m = pf->m;
+  HIPCHK(hipSetDevice(m->device));
+  hipStream_t s = (hipStream_t)stream;
+  double buf[kMaxReadout + 1];
+  HIPCHK(hipMemcpyAsync(buf, pf->readout, sizeof(double) * (m->C + m->d + 1), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (post) std::memcpy(post, buf, sizeof(double) * m->C);
+  if (mean) std::memcpy(mean, buf + m->C, sizeof(double) * m->d);
+  if (lik) *lik = buf[m->C + m->d];
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_export(gpmdm_pf_t pf, double* states, int64_t* classes, double* ll, double* log_w,
+                    double* w, int64_t* ridx, void* stream) {
+  CHECK(pf, "null handle");
+  const gpmdm_model* m = pf->m;
+  HIPCHK(hipSetDevice(m->device));
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipStreamSynchronize(s));
+  const long long P = pf->P;
+  if (states) HIPCHK(hipMemcpy(states, pf->X, sizeof(double) * P * m->d, hipMemcpyDeviceToHost));
+  std::vector<int> tmp(P);
+  if (classes) {
+    HIPCHK(hipMemcpy(tmp.data(), pf->cls, sizeof(int) * P, hipMemcpyDeviceToHost));
+    for (long long i = 0; i < P; ++i) classes[i] = tmp[i];
+  }
+  if (ridx) {
+    HIPCHK(hipMemcpy(tmp.data(), pf->ridx, sizeof(int) * P, hipMemcpyDeviceToHost));
+    for (long long i = 0; i < P; ++i) ridx[i] = tmp[i];
+  }
+  std::vector<double> l(P);
+  HIPCHK(hipMemcpy(l.data(), pf->ll, sizeof(double) * P, hipMemcpyDeviceToHost));
+  if (ll) std::memcpy(ll, l.data(), sizeof(double) * P);
+  unsigned long long gm = 0;
+  double S = 0;
+  HIPCHK(hipMemcpy(&gm, pf->gmax, sizeof(gm), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(&S, pf->total, sizeof(S), hipMemcpyDeviceToHost));
+  const unsigned long long v = (gm >> 63) ? (gm & 0x7fffffffffffffffull) : ~gm;
+  double M;
+  std::memcpy(&M, &v, sizeof(M));
+  if (log_w)
+    for (long long i = 0; i < P; ++i) log_w[i] = l[i] - M;
+  if (w) {
+    HIPCHK(hipMemcpy(w, pf->e, sizeof(double) * P, hipMemcpyDeviceToHost));
+    for (long long i = 0; i < P; ++i) w[i] /= S;
+  }
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_enable_timing(gpmdm_pf_t pf, int enable) {
+  CHECK(pf, "null handle");
+  pf->timing = enable != 0;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_stage_times(gpmdm_pf_t pf, double* ms, int64_t* launches) {
+  CHECK(pf, "null handle");
+  HIPCHK(hipSetDevice(pf->m->device));
+  double acc[GPMDM_N_STAGES] = {0};
+  int64_t n[GPMDM_N_STAGES] = {0};
+  for (auto& r : pf->recs) {
+    HIPCHK(hipEventSynchronize(r.b));
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, r.a, r.b));
+    acc[r.stage] += t;
+    n[r.stage] += 1;
+    pf->pool.push_back(r.a);
+    pf->pool.push_back(r.b);
+  }
+  pf->recs.clear();
+  if (ms) std::memcpy(ms, acc, sizeof(acc));
+  if (launches) std::memcpy(launches, n, sizeof(n));
+  return GPMDM_OK;
+}
+
+}  // extern "C"

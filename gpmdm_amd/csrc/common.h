@@ -1,0 +1,106 @@
+// Shared device helpers and launch declarations for libgpmdm_hip (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gpmdm {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------
+// Fused GP tile "GEMM" geometry (see gp_tile.hip and DESIGN.md §3).
+//   one workgroup = 4 waves = a PT x NT tile of V = K* . B, where K* (particles x training
+//   rows) is generated on the fly and B = [R | M] is the extended weight matrix.
+// ---------------------------------------------------------------------------------
+constexpr int kPT = 128;          // particles per tile (MFMA M)
+constexpr int kNT = 128;          // columns of B per tile (MFMA N)
+constexpr int kBK = 16;           // training rows per K-step (4 x K=4 MFMA sub-steps)
+constexpr int kLDA = kPT + 16;    // LDS row strides (doubles): +128 B shifts rows by 32 banks
+constexpr int kLDB = kNT + 16;
+constexpr int kMaxSeg = 8;        // segments (classes) per launch
+constexpr int kMaxD = 32;         // latent dimension limit
+
+struct SegDesc {                  // one GP: the observation GP, or the class-c dynamics GP
+  const double* Xs;               // n_rows x d : training inputs / lengthscales
+  const double* Xl;               // n_rows x d : raw training inputs (linear kernel; dyn only)
+  const double* B;                // k_pad x ld : [R | M], zero padded (k_pad = ceil(n_rows/BK)*BK)
+  long long ld;                   // columns of B (multiple of kNT)
+  int n_rows;                     // training rows = R columns
+  int n_m;                        // mean columns (D or d)
+  int n_j;                        // column blocks = ld / kNT
+  int pad_;
+};
+
+struct TileParams {
+  SegDesc seg[kMaxSeg];
+  int n_seg;
+  int tiles_ub;                   // grid = n_j_max * tiles_ub workgroups
+  int n_j_max;
+  int pad_;
+  const int* seg_pos_begin;       // [n_seg]   first position (device)
+  const int* seg_pos_end;         // [n_seg]
+  const int* seg_out_base;        // [n_seg]   output row of the first position
+  const int* seg_tile_start;      // [n_seg+1] prefix of tiles
+  const int* perm;                // position -> particle row (nullptr: identity)
+  const double* X;                // particle rows, n x d
+  double ls[kMaxD];               // RBF lengthscales
+  double lin_c2[kMaxD + 1];       // linear-kernel c^2, bias last (dyn only)
+  double* qpart;                  // [2*J + wn][ld_q]: partial sums of (R^T k)^2
+  long long ld_q;
+  double* mu;                     // [out][ld_mu] mean columns
+  long long ld_mu;
+};
+
+void launch_gp_tile(const TileParams& p, int d, bool dyn, hipStream_t stream);
+
+// ---------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11), counter = (index, frame, stream, sub).
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const unsigned hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+    const unsigned hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+    c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+    k.x += 0x9E3779B9u;
+    k.y += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// 53-bit uniforms from two 32-bit words.
+__device__ __forceinline__ double u01_co(unsigned hi, unsigned lo) {   // [0, 1)
+  const unsigned long long x = (((unsigned long long)hi << 32) | lo) >> 11;
+  return (double)x * 0x1.0p-53;
+}
+__device__ __forceinline__ double u01_oo(unsigned hi, unsigned lo) {   // (0, 1)
+  const unsigned long long x = (((unsigned long long)hi << 32) | lo) >> 11;
+  return ((double)x + 0.5) * 0x1.0p-53;
+}
+
+enum RngStream : unsigned { kStreamSwitch = 0, kStreamDyn = 1, kStreamResample = 2, kStreamSystematic = 3 };
+
+// Order-preserving uint64 image of a double (atomicMax on doubles).
+__device__ __forceinline__ unsigned long long ord_enc(double x) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double ord_dec(unsigned long long u) {
+  const unsigned long long v = (u >> 63) ? (u & 0x7fffffffffffffffull) : ~u;
+  return __longlong_as_double((long long)v);
+}
+
+// Wave (64-lane) reductions.
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+  return v;
+}
+
+}  // namespace gpmdm

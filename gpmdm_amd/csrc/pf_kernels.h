@@ -1,0 +1,132 @@
+// Argument blocks and launchers of the particle-filter kernels (pf_kernels.hip).
+#pragma once
+
+#include "common.h"
+
+namespace gpmdm {
+
+constexpr int kMaxClasses = 32;
+constexpr int kMaxReadout = kMaxClasses + 1 + kMaxD;
+
+struct SwitchArgs {
+  long long P;
+  int C;
+  unsigned frame, seed_lo, seed_hi;
+  const int* cls;                 // P   current classes
+  int* cls_new;                   // P   switched classes
+  const double* T;                // C x C Markov matrix (device)
+  const double* E;                // P x C Exp(1) draws (replay) or nullptr (philox)
+  int* blockcounts;               // nb x C
+  unsigned long long* gmax_reset; // reset of the normaliser's running max (or nullptr)
+};
+
+struct ScanArgs {
+  int nb, C;
+  long long lo, hi;               // this rank's particle slice
+  const int* blockcounts;
+  const int* cls_new;
+  int* blockoff;                  // nb x C
+  int* class_start;               // C + 1
+  int* counts;                    // C
+  int* seg_pos_begin;             // C
+  int* seg_pos_end;               // C
+  int* seg_out_base;              // C
+  int* seg_tile_start;            // C + 1
+};
+
+struct GroupArgs {
+  long long P;
+  int C;
+  const int* cls_new;
+  const int* class_start;
+  const int* blockoff;
+  int* perm;                      // grouped position -> particle
+};
+
+struct DynFinishArgs {
+  long long n_out;                // rows produced by the tile kernel
+  int n_seg, d;
+  unsigned frame, seed_lo, seed_hi;
+  const int* seg_out_base;        // nullptr: single segment
+  const int* seg_pos_begin;
+  const int* perm;                // nullptr: identity
+  int n_parts[kMaxClasses];       // q partials per segment
+  const double* qpart;
+  long long ld_q;
+  const double* mu;
+  long long ld_mu;
+  const double* X;                // input rows (pre-dynamics states)
+  double lin_c2[kMaxD + 1];
+  double il2[kMaxD];              // exp(x_log_lambdas)^-2
+  const double* normals;          // grouped-position-major draws (replay) or nullptr
+  double* X_out;                  // PF: propagated states (P x d, particle index)
+  double* var_out;                // predictive map: n x d variances (PF: nullptr)
+};
+
+struct ObsFinishArgs {
+  long long n_out;
+  int n_parts, D;
+  const double* qpart;
+  long long ld_q;
+  const double* mu;
+  long long ld_mu;
+  const double* z;                // D (device)
+  const double* il2;              // D  exp(y_log_lambdas)^-2 (device)
+  double ll_const;                // 0.5 * D * ln(2 pi) in float32 (gpmdm_pf.py:5, 191)
+  double* ll;                     // PF output (ll[ll_offset + o]) or nullptr
+  long long ll_offset;
+  double* var_out;                // predictive map output n x D, or nullptr
+};
+
+struct NormArgs {
+  long long P;
+  int nb;
+  const double* ll;
+  unsigned long long* gmax;
+  double* e;                      // exp(ll - max)
+  double* local;                  // block-local inclusive scan of e
+  double* blocksum;
+  double* blockoff;
+  double* total;                  // sum of e
+  double* cum;                    // normalised CDF
+};
+
+struct ResampleArgs {
+  long long P;
+  int nb, C, d, systematic, identity;
+  unsigned frame, seed_lo, seed_hi;
+  const double* U;                // uniforms (replay) or nullptr
+  const double* cum;
+  const double* ll;
+  const double* e;
+  const double* total;
+  const unsigned long long* gmax;
+  const int* cls_src;
+  const double* X_src;
+  int* cls_dst;
+  double* X_dst;
+  int* ridx;
+  double* partials;               // nb x (C + 1 + d)
+  double* readout;                // C posterior, d mean, 1 likelihood sum
+};
+
+struct PackArgs {
+  long long n, lo;
+  int d;
+  double* buf;
+  double* ll;
+  int* cls;
+  double* X;
+};
+
+void launch_switch(const SwitchArgs& a, hipStream_t s);
+void launch_scan_counts(const ScanArgs& a, hipStream_t s);
+void launch_group(const GroupArgs& a, hipStream_t s);
+void launch_dyn_finish(const DynFinishArgs& a, hipStream_t s);
+void launch_obs_finish(const ObsFinishArgs& a, hipStream_t s);
+void launch_normalise(const NormArgs& a, hipStream_t s);
+void launch_resample(const ResampleArgs& a, hipStream_t s);
+void launch_pack(const PackArgs& a, hipStream_t s);
+void launch_unpack(const PackArgs& a, hipStream_t s);
+
+}  // namespace gpmdm

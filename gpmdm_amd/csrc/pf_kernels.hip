@@ -1,0 +1,457 @@
+// Particle-filter kernels around the fused GP tiles (gfx950).
+//
+//   k_switch        _propogate_markov_switching   gpmdm_pf.py:137-151
+//   k_scan_counts   class counts, per-block offsets, this rank's class segments
+//   k_group         stable class grouping (the order of gpmdm_pf.py:158-161)
+//   k_dyn_finish    variance + sample mu + sqrt(var) eps   gpmdm.py:1062-1067, gpmdm_pf.py:167-168
+//   k_obs_finish    variance + Gaussian log-likelihood      gpmdm.py:958-961, gpmdm_pf.py:188-192
+//   k_norm_*        log_w = ll - max, w = exp / sum          gpmdm_pf.py:200-204
+//   k_cdf/k_resample  torch.multinomial(w, P, True) inverse CDF + gathers  gpmdm_pf.py:206-213
+//                   and the read-out partial sums            gpmdm_pf.py:224-262, 302-312
+//   k_readout       read-out totals
+// All arithmetic is fp64; every reduction has a fixed order (bitwise run-to-run repeatable).
+#include "common.h"
+#include "pf_kernels.h"
+
+namespace gpmdm {
+
+constexpr int kB = 256;   // threads per block of the O(P) kernels
+
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kB) void k_switch(SwitchArgs a) {
+  __shared__ int hist[kMaxClasses];
+  const int tid = threadIdx.x;
+  if (tid < a.C) hist[tid] = 0;
+  if (blockIdx.x == 0 && tid == 0 && a.gmax_reset) *a.gmax_reset = ord_enc(-INFINITY);
+  __syncthreads();
+  const long long p = (long long)blockIdx.x * kB + tid;
+  if (p < a.P) {
+    const int c0 = a.cls[p];
+    int best = 0;
+    double bestv = -INFINITY;
+    for (int j = 0; j < a.C; j += 2) {
+      double e0, e1 = 1.0;
+      if (a.E) {
+        e0 = a.E[p * a.C + j];
+        if (j + 1 < a.C) e1 = a.E[p * a.C + j + 1];
+      } else {
+        const uint4 r = philox4x32_10(make_uint4((unsigned)p, a.frame, kStreamSwitch, (unsigned)(j >> 1)),
+                                      make_uint2(a.seed_lo, a.seed_hi));
+        e0 = -log(u01_oo(r.x, r.y));
+        e1 = -log(u01_oo(r.z, r.w));
+      }
+      // torch.multinomial(p, 1) == argmax(p / E), first maximum (gpmdm_pf.py:150)
+      const double v0 = a.T[c0 * a.C + j] / e0;
+      if (v0 > bestv) { bestv = v0; best = j; }
+      if (j + 1 < a.C) {
+        const double v1 = a.T[c0 * a.C + j + 1] / e1;
+        if (v1 > bestv) { bestv = v1; best = j + 1; }
+      }
+    }
+    a.cls_new[p] = best;
+    atomicAdd(&hist[best], 1);
+  }
+  __syncthreads();
+  if (tid < a.C) a.blockcounts[(long long)blockIdx.x * a.C + tid] = hist[tid];
+}
+
+// ---------------------------------------------------------------------------------
+// One workgroup: exclusive scans of the per-block class counts, class starts, and the
+// segments (grouped position ranges) of this rank's particle slice [lo, hi).
+__global__ __launch_bounds__(1024) void k_scan_counts(ScanArgs a) {
+  __shared__ int part[1024];
+  __shared__ int tot[kMaxClasses];
+  __shared__ int lo_cnt[kMaxClasses], hi_cnt[kMaxClasses];
+  const int tid = threadIdx.x;
+  const int nb = a.nb;
+  const int chunk = (nb + 1023) / 1024;
+  for (int c = 0; c < a.C; ++c) {
+    int s = 0;
+    for (int i = 0; i < chunk; ++i) {
+      const int b = tid * chunk + i;
+      if (b < nb) s += a.blockcounts[(long long)b * a.C + c];
+    }
+    part[tid] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {        // Hillis-Steele inclusive scan
+      const int v = tid >= off ? part[tid - off] : 0;
+      __syncthreads();
+      part[tid] += v;
+      __syncthreads();
+    }
+    int run = tid ? part[tid - 1] : 0;
+    for (int i = 0; i < chunk; ++i) {
+      const int b = tid * chunk + i;
+      if (b < nb) {
+        a.blockoff[(long long)b * a.C + c] = run;
+        run += a.blockcounts[(long long)b * a.C + c];
+      }
+    }
+    if (tid == 1023) tot[c] = part[1023];
+    __syncthreads();
+  }
+  // counts of each class among particles [0, lo) and [0, hi)
+  if (tid < a.C) { lo_cnt[tid] = 0; hi_cnt[tid] = 0; }
+  __syncthreads();
+  for (int which = 0; which < 2; ++which) {
+    const long long bound = which ? a.hi : a.lo;
+    const long long bb = bound / kB;
+    const long long start = bb * kB;
+    if (tid < kB && start + tid < bound) atomicAdd(which ? &hi_cnt[a.cls_new[start + tid]] : &lo_cnt[a.cls_new[start + tid]], 1);
+    __syncthreads();
+    if (tid < a.C) {
+      const int base = bb < nb ? a.blockoff[bb * a.C + tid] : tot[tid];
+      if (which) hi_cnt[tid] += base; else lo_cnt[tid] += base;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    int cs = 0, ob = 0, ts = 0;
+    for (int c = 0; c < a.C; ++c) {
+      a.class_start[c] = cs;
+      a.counts[c] = tot[c];
+      const int b0 = cs + lo_cnt[c], e0 = cs + hi_cnt[c];
+      a.seg_pos_begin[c] = b0;
+      a.seg_pos_end[c] = e0;
+      a.seg_out_base[c] = ob;
+      a.seg_tile_start[c] = ts;
+      ob += e0 - b0;
+      ts += (e0 - b0 + kPT - 1) / kPT;
+      cs += tot[c];
+    }
+    a.class_start[a.C] = cs;
+    a.seg_tile_start[a.C] = ts;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kB) void k_group(GroupArgs a) {
+  __shared__ int wcount[kB / 64][kMaxClasses];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long p = (long long)blockIdx.x * kB + tid;
+  const int c = p < a.P ? a.cls_new[p] : -1;
+  int rank = 0;
+  for (int k = 0; k < a.C; ++k) {
+    const unsigned long long m = __ballot(c == k);
+    if (c == k) rank = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wcount[w][k] = __popcll(m);
+  }
+  __syncthreads();
+  if (c >= 0) {
+    int off = a.class_start[c] + a.blockoff[(long long)blockIdx.x * a.C + c];
+    for (int v = 0; v < w; ++v) off += wcount[v][c];
+    a.perm[off + rank] = (int)p;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// out index o -> class segment
+__device__ __forceinline__ int seg_of(const int* seg_out_base, int n_seg, int total, int o) {
+  int c = 0;
+  for (int s = 1; s < n_seg; ++s)
+    if (o >= seg_out_base[s]) c = s;
+  (void)total;
+  return c;
+}
+
+__global__ __launch_bounds__(kB) void k_dyn_finish(DynFinishArgs a) {
+  const long long o = (long long)blockIdx.x * kB + threadIdx.x;
+  if (o >= a.n_out) return;
+  const int c = a.seg_out_base ? seg_of(a.seg_out_base, a.n_seg, (int)a.n_out, (int)o) : 0;
+  const long long pos = (a.seg_pos_begin ? a.seg_pos_begin[c] : 0) + (o - (a.seg_out_base ? a.seg_out_base[c] : 0));
+  const long long p = a.perm ? a.perm[pos] : pos;
+  double q = 0.0;
+  const int np = a.n_parts[c];
+  for (int k = 0; k < np; ++k) q += a.qpart[(long long)k * a.ld_q + o];
+  // k(x*, x*) of the dynamics kernel without noise: 1 + [x,1] diag(c^2) [x,1]^T (gpmdm.py:1100)
+  const int d = a.d;
+  double kd = 0.0;
+  for (int j = 0; j < d; ++j) {
+    const double x = a.X[p * d + j];
+    kd = fma(a.lin_c2[j] * x, x, kd);
+  }
+  kd = 1.0 + (kd + a.lin_c2[d]);
+  const double vc = kd - q;
+  if (a.var_out) {                      // predictive map (map_x_dynamics_for_class)
+    for (int j = 0; j < d; ++j) a.var_out[o * d + j] = vc * a.il2[j];
+    return;
+  }
+  // torch.normal(mean, std) = eps * std + mean (gpmdm_pf.py:167-168)
+  for (int j = 0; j < d; j += 2) {
+    double e0, e1 = 0.0;
+    if (a.normals) {
+      e0 = a.normals[pos * d + j];
+      if (j + 1 < d) e1 = a.normals[pos * d + j + 1];
+    } else {
+      const uint4 r = philox4x32_10(make_uint4((unsigned)p, a.frame, kStreamDyn, (unsigned)(j >> 1)),
+                                    make_uint2(a.seed_lo, a.seed_hi));
+      const double u1 = u01_oo(r.x, r.y), u2 = u01_co(r.z, r.w);
+      const double rr = sqrt(-2.0 * log(u1));
+      double sn, cs;
+      sincos(6.283185307179586476925 * u2, &sn, &cs);
+      e0 = rr * cs;
+      e1 = rr * sn;
+    }
+    a.X_out[p * d + j] = e0 * sqrt(vc * a.il2[j]) + a.mu[o * a.ld_mu + j];
+    if (j + 1 < d) a.X_out[p * d + j + 1] = e1 * sqrt(vc * a.il2[j + 1]) + a.mu[o * a.ld_mu + j + 1];
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// One wave per particle: the D-term log-likelihood sum is spread over 64 lanes.
+__global__ __launch_bounds__(kB) void k_obs_finish(ObsFinishArgs a) {
+  const int lane = threadIdx.x & 63;
+  const long long o = (long long)blockIdx.x * (kB / 64) + (threadIdx.x >> 6);
+  __shared__ double smax[kB / 64];
+  double llv = -INFINITY;
+  if (o < a.n_out) {
+    double q = 0.0;
+    for (int k = lane; k < a.n_parts; k += 64) q += a.qpart[(long long)k * a.ld_q + o];
+    q = wave_sum(q);
+    const double vc = 1.0 - q;                         // k(x*,x*) = 1 (gpmdm.py:991)
+    const double* mu = a.mu + o * a.ld_mu;
+    if (a.var_out) {
+      for (int j = lane; j < a.D; j += 64) a.var_out[o * a.D + j] = vc * a.il2[j];
+    } else {
+      // ll = -1/2 sum[(z-mu)^2/var + log var] + sum(-log sqrt var) - D/2 ln(2pi)_f32
+      double s1 = 0.0, s2 = 0.0;
+      for (int j = lane; j < a.D; j += 64) {
+        const double var = vc * a.il2[j];
+        const double t = a.z[j] - mu[j];
+        s1 += t * t / var + log(var);
+        s2 += -log(sqrt(var));
+      }
+      s1 = wave_sum(s1);
+      s2 = wave_sum(s2);
+      llv = -0.5 * s1 + s2 - a.ll_const;
+      if (lane == 0) a.ll[a.ll_offset + o] = llv;
+    }
+  }
+  (void)smax;
+}
+
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kB) void k_norm_max(NormArgs a) {
+  __shared__ double s[kB / 64];
+  const long long p = (long long)blockIdx.x * kB + threadIdx.x;
+  double v = p < a.P ? a.ll[p] : -INFINITY;
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = s[0];
+    for (int i = 1; i < kB / 64; ++i) m = fmax(m, s[i]);
+    atomicMax(a.gmax, ord_enc(m));
+  }
+}
+
+// e = exp(ll - max); block-local inclusive scan of e; block sums.
+__global__ __launch_bounds__(kB) void k_norm_exp_scan(NormArgs a) {
+  __shared__ double wsum[kB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long p = (long long)blockIdx.x * kB + tid;
+  const double M = ord_dec(*a.gmax);
+  const double e = p < a.P ? exp(a.ll[p] - M) : 0.0;
+  if (p < a.P) a.e[p] = e;
+  double x = e;                               // wave inclusive scan
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const double y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  double base = 0.0;
+  for (int v = 0; v < w; ++v) base += wsum[v];
+  x += base;
+  if (p < a.P) a.local[p] = x;
+  if (tid == kB - 1) a.blocksum[blockIdx.x] = x;
+}
+
+// One workgroup: exclusive scan of block sums, total S.
+__global__ __launch_bounds__(1024) void k_norm_total(NormArgs a) {
+  __shared__ double part[1024];
+  const int tid = threadIdx.x;
+  const int nb = a.nb;
+  const int chunk = (nb + 1023) / 1024;
+  double s = 0.0;
+  for (int i = 0; i < chunk; ++i) {
+    const int b = tid * chunk + i;
+    if (b < nb) s += a.blocksum[b];
+  }
+  part[tid] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const double v = tid >= off ? part[tid - off] : 0.0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  double run = tid ? part[tid - 1] : 0.0;
+  for (int i = 0; i < chunk; ++i) {
+    const int b = tid * chunk + i;
+    if (b < nb) {
+      a.blockoff[b] = run;
+      run += a.blocksum[b];
+    }
+  }
+  if (tid == 1023) *a.total = part[1023];
+}
+
+__global__ __launch_bounds__(kB) void k_cdf(NormArgs a) {
+  const long long p = (long long)blockIdx.x * kB + threadIdx.x;
+  if (p >= a.P) return;
+  const double S = *a.total;
+  // torch: cumsum(w) / sum, last bucket forced to 1
+  a.cum[p] = p == a.P - 1 ? 1.0 : (a.blockoff[blockIdx.x] + a.local[p]) / S;
+}
+
+// One thread per output slot s: inverse-CDF search, gather, read-out partials.
+// identity=1 computes the read-outs of the current state without resampling (after init).
+__global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
+  __shared__ double red[kB / 64][kMaxReadout];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long s = (long long)blockIdx.x * kB + tid;
+  const int C = a.C, d = a.d;
+  const int nq = C + 1 + d;
+  const bool act = s < a.P;
+  long long idx = 0;
+  int cnew = -1;
+  double e2 = 0.0, wv = 0.0;
+  if (act) {
+    if (a.identity) {
+      idx = s;
+    } else {
+      double u;
+      if (a.systematic) {
+        double u0;
+        if (a.U) {
+          u0 = a.U[0];
+        } else {
+          const uint4 r = philox4x32_10(make_uint4(0u, a.frame, kStreamSystematic, 0u), make_uint2(a.seed_lo, a.seed_hi));
+          u0 = u01_co(r.x, r.y);
+        }
+        u = ((double)s + u0) / (double)a.P;
+      } else if (a.U) {
+        u = a.U[s];
+      } else {
+        const uint4 r = philox4x32_10(make_uint4((unsigned)s, a.frame, kStreamResample, 0u), make_uint2(a.seed_lo, a.seed_hi));
+        u = u01_co(r.x, r.y);
+      }
+      long long lo = 0, hi = a.P;               // first index with cum >= u
+      while (hi - lo > 0) {
+        const long long mid = lo + (hi - lo) / 2;
+        if (a.cum[mid] < u) lo = mid + 1; else hi = mid;
+      }
+      idx = lo;
+    }
+    cnew = a.cls_src[idx];
+    if (!a.identity) {
+      a.ridx[s] = (int)idx;
+      a.cls_dst[s] = cnew;
+      for (int j = 0; j < d; ++j) a.X_dst[s * d + j] = a.X_src[idx * d + j];
+    }
+    // read-outs: post-resample class/state at slot s, pre-resample ll/log_w at slot s
+    const double M = ord_dec(*a.gmax);
+    const double llv = a.ll[s];
+    const double lw = llv - M;
+    e2 = exp((llv + lw) - M);                  // ll + log_w - max(ll + log_w); that max is M
+    wv = a.e[s] / *a.total;
+  }
+  for (int k = 0; k < nq; ++k) {
+    double v = 0.0;
+    if (act) {
+      if (k < C) v = (cnew == k) ? e2 : 0.0;
+      else if (k == C) v = e2;
+      else v = a.X_src[idx * d + (k - C - 1)] * wv;
+    }
+    v = wave_sum(v);
+    if (lane == 0) red[w][k] = v;
+  }
+  __syncthreads();
+  if (tid < nq) {
+    double t = 0.0;
+    for (int v = 0; v < kB / 64; ++v) t += red[v][tid];
+    a.partials[(long long)blockIdx.x * nq + tid] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_readout(ResampleArgs a) {
+  __shared__ double red[4];
+  __shared__ double tot[kMaxReadout];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nq = a.C + 1 + a.d;
+  for (int k = 0; k < nq; ++k) {
+    double s = 0.0;
+    for (long long b = tid; b < a.nb; b += 256) s += a.partials[b * nq + k];
+    s = wave_sum(s);
+    if (lane == 0) red[w] = s;
+    __syncthreads();
+    if (tid == 0) tot[k] = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    double cl = 0.0;
+    for (int c = 0; c < a.C; ++c) cl += tot[c];
+    for (int c = 0; c < a.C; ++c) a.readout[c] = tot[c] / cl;   // class_probabilities
+    for (int j = 0; j < a.d; ++j) a.readout[a.C + j] = tot[a.C + 1 + j];  // current_state_mean
+    a.readout[a.C + a.d] = tot[a.C];                                       // log_likelihood()
+  }
+}
+
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(kB) void k_pack(PackArgs a) {
+  const long long r = (long long)blockIdx.x * kB + threadIdx.x;
+  if (r >= a.n) return;
+  const long long p = a.lo + r;
+  double* o = a.buf + r * (a.d + 2);
+  o[0] = a.ll[p];
+  o[1] = (double)a.cls[p];
+  for (int j = 0; j < a.d; ++j) o[2 + j] = a.X[p * a.d + j];
+}
+
+__global__ __launch_bounds__(kB) void k_unpack(PackArgs a) {
+  const long long p = (long long)blockIdx.x * kB + threadIdx.x;
+  if (p >= a.n) return;
+  const double* i = a.buf + p * (a.d + 2);
+  a.ll[p] = i[0];
+  a.cls[p] = (int)i[1];
+  for (int j = 0; j < a.d; ++j) a.X[p * a.d + j] = i[2 + j];
+}
+
+// ---------------------------------------------------------------------------------
+static inline unsigned nblk(long long n, int b) { return (unsigned)((n + b - 1) / b); }
+
+void launch_switch(const SwitchArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_switch, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+}
+void launch_scan_counts(const ScanArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, a);
+}
+void launch_group(const GroupArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_group, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+}
+void launch_dyn_finish(const DynFinishArgs& a, hipStream_t s) {
+  if (a.n_out > 0) hipLaunchKernelGGL(k_dyn_finish, dim3(nblk(a.n_out, kB)), dim3(kB), 0, s, a);
+}
+void launch_obs_finish(const ObsFinishArgs& a, hipStream_t s) {
+  if (a.n_out > 0) hipLaunchKernelGGL(k_obs_finish, dim3(nblk(a.n_out, kB / 64)), dim3(kB), 0, s, a);
+}
+void launch_normalise(const NormArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_norm_max, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+  hipLaunchKernelGGL(k_norm_exp_scan, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+  hipLaunchKernelGGL(k_norm_total, dim3(1), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(k_cdf, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+}
+void launch_resample(const ResampleArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_resample, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+  hipLaunchKernelGGL(k_readout, dim3(1), dim3(256), 0, s, a);
+}
+void launch_pack(const PackArgs& a, hipStream_t s) {
+  if (a.n > 0) hipLaunchKernelGGL(k_pack, dim3(nblk(a.n, kB)), dim3(kB), 0, s, a);
+}
+void launch_unpack(const PackArgs& a, hipStream_t s) {
+  if (a.n > 0) hipLaunchKernelGGL(k_unpack, dim3(nblk(a.n, kB)), dim3(kB), 0, s, a);
+}
+
+}  // namespace gpmdm

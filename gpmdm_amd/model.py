@@ -1,0 +1,423 @@
+"""GPMDM host model: the part of the reference ``GPMDM`` class the particle filter needs.
+
+Mirrors ``/root/reference/gpmdm/gpmdm.py`` (class GPMDM, lines 18-1414) for construction,
+data registry, latent initialisation, kernel-inverse precompute, persistence and the two
+predictive maps; the predictive maps and everything per frame run in libgpmdm_hip.so.
+Training (``train_adam`` / ``gpdm_loss``, gpmdm.py:550-885) is out of scope:
+hyperparameters are passed in, or loaded from a saved model.
+
+Precompute follows the reference recipe (gpmdm.py:1284-1305) on class blocks only:
+``U = chol(K, upper)``, ``R = U^-1``, ``K^-1 = R R^T``.  The library keeps ``R`` (upper
+triangular) and the mean weights ``beta = K_y^-1 Y`` and ``alpha_c = A_c Xout_c``; the
+dense ``(C+1) x Nx x Nx`` masks of the reference are never formed.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _to_np(x, dtype=np.float64):
+    if isinstance(x, torch.Tensor):
+        x = x.detach().cpu().numpy()
+    return np.asarray(x, dtype=dtype)
+
+
+def _sq_dist(X1, X2, log_ls):
+    """gpmdm.py:483-517 (expansion form), used for the setup kernel matrices."""
+    ls = torch.exp(log_ls)
+    a = X1 / ls
+    b = X2 / ls
+    return (a * a).sum(1, keepdim=True) + (b * b).sum(1, keepdim=True).T - 2.0 * (a @ b.T)
+
+
+def _lin(X1, X2, log_c):
+    """gpmdm.py:520-548."""
+    S = torch.diag(torch.exp(log_c) ** 2)
+    o1 = torch.ones(X1.shape[0], 1, dtype=X1.dtype, device=X1.device)
+    o2 = torch.ones(X2.shape[0], 1, dtype=X2.dtype, device=X2.device)
+    X1 = torch.cat([X1, o1], 1)
+    X2 = torch.cat([X2, o2], 1)
+    return X1 @ (S @ X2.T)
+
+
+def _chol_inv_factor(K, what):
+    """Upper Cholesky + inverse as gpmdm.py:1287-1289; returns R = U^-1 (upper)."""
+    U, info = torch.linalg.cholesky_ex(K, upper=True)
+    if int(info) != 0:
+        # The reference ignores `info` and silently propagates garbage; we refuse.
+        raise RuntimeError(f"{what}: kernel matrix is not positive definite (cholesky info={int(info)})")
+    R = torch.inverse(U)
+    return torch.triu(R)
+
+
+class GPMDM:
+    """Gaussian Process Multi-Dynamical Model -- inference-side mirror of gpmdm.py:GPMDM.
+
+    Constructor arguments are those of the reference (gpmdm.py:96-109).  ``dtype`` must be
+    float64 (the reference default, required for parity: SURVEY.md §8(c)).  ``device`` is
+    the GPU the model lives on (default ``cuda:0``); ``flg_train_*`` are accepted and
+    ignored (no training here).
+    """
+
+    def __init__(self, D, d, n_classes, dyn_target, dyn_back_step,
+                 y_lambdas_init, y_lengthscales_init, y_sigma_n_init,
+                 x_lambdas_init, x_lengthscales_init, x_sigma_n_init, x_lin_coeff_init,
+                 flg_train_y_lambdas=True, flg_train_y_lengthscales=True, flg_train_y_sigma_n=True,
+                 flg_train_x_lambdas=True, flg_train_x_lengthscales=True,
+                 flg_train_x_sigma_n=True, flg_train_x_lin_coeff=True,
+                 sigma_n_num_Y=0., sigma_n_num_X=0.,
+                 dtype=torch.float64, device=None):
+        if dtype != torch.float64:
+            raise NotImplementedError("gpmdm_amd computes in float64 only (reference default, gpmdm.py:109)")
+        if dyn_target not in ("full", "delta") or dyn_back_step not in (1, 2):
+            raise ValueError("target must be either 'full' or 'delta' \n back_step must be either 1 or 2")
+        self.dtype = dtype
+        self.device = torch.device("cuda", 0) if device is None else torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("gpmdm_amd runs on the GPU: device must be a cuda (HIP) device")
+        self.D, self.d, self.n_classes = int(D), int(d), int(n_classes)
+        self.dyn_target, self.dyn_back_step = dyn_target, int(dyn_back_step)
+        f64 = dict(dtype=torch.float64)
+        self.y_log_lengthscales = torch.log(torch.as_tensor(_to_np(y_lengthscales_init), **f64)).reshape(-1)
+        self.y_log_lambdas = torch.log(torch.as_tensor(_to_np(y_lambdas_init), **f64)).reshape(-1)
+        self.y_log_sigma_n = torch.log(torch.as_tensor(float(y_sigma_n_init), **f64))
+        self.x_log_lengthscales = torch.log(torch.as_tensor(_to_np(x_lengthscales_init), **f64)).reshape(-1)
+        self.x_log_lambdas = torch.log(torch.as_tensor(_to_np(x_lambdas_init), **f64)).reshape(-1)
+        self.x_log_sigma_n = torch.log(torch.as_tensor(float(x_sigma_n_init), **f64))
+        self.x_log_lin_coeff = torch.log(torch.as_tensor(_to_np(x_lin_coeff_init), **f64)).reshape(-1)
+        self.sigma_n_num_Y = float(sigma_n_num_Y)
+        self.sigma_n_num_X = float(sigma_n_num_X)
+        self.class_aware_observations_list = [[] for _ in range(self.n_classes)]
+        self.X = None
+        self._handle = None
+        self._precompute_device = None   # None: CPU for N <= 4096, the model GPU above
+
+    # ---- reference API: data registry (gpmdm.py:239-309) -------------------------
+    def set_evaluation_mode(self):
+        """gpmdm.py:239-245 (no autograd state is kept here)."""
+        self.flg_trainable_list = []
+
+    def add_data(self, Y, class_index: int):
+        """gpmdm.py:281-298."""
+        if Y.shape[1] != self.D:
+            raise ValueError('Y must be a N x D matrix collecting observation data!')
+        self.class_aware_observations_list[class_index].append(Y)
+
+    @property
+    def observations_list(self):
+        return [seq for cls in self.class_aware_observations_list for seq in cls]
+
+    def get_Y(self) -> np.ndarray:
+        """gpmdm.py:779-793 (meanY = 0)."""
+        self.meanY = 0
+        return np.concatenate([_to_np(y) if isinstance(y, torch.Tensor) else np.asarray(y)
+                               for y in self.observations_list], 0) - self.meanY
+
+    def get_Y_for_class(self, class_index: int) -> np.ndarray:
+        """gpmdm.py:795-815."""
+        self.meanY = 0
+        return np.concatenate(self.class_aware_observations_list[class_index], 0) - self.meanY
+
+    def get_X_for_class(self, class_index: int) -> torch.Tensor:
+        """gpmdm.py:906-921."""
+        per = [sum(len(s) for s in self.class_aware_observations_list[i]) for i in range(self.n_classes)]
+        start = sum(per[:class_index])
+        return self.X[start:start + per[class_index], :]
+
+    def get_latent_sequences(self):
+        """gpmdm.py:887-904."""
+        X = self.X.numpy()
+        out, s = [], 0
+        for seq in self.observations_list:
+            out.append(X[s:s + len(seq)])
+            s += len(seq)
+        return out
+
+    def get_Xin_Xout_matrices(self, X=None, target=None, back_step=None):
+        """gpmdm.py:630-718 -- all four (target, back_step) modes."""
+        X = self.X if X is None else torch.as_tensor(X, dtype=torch.float64)
+        target = self.dyn_target if target is None else target
+        back_step = self.dyn_back_step if back_step is None else back_step
+        Xin, Xout, starts, s = [], [], [], 0
+        for seq in self.observations_list:
+            L = len(seq)
+            Xs = X[s:s + L]
+            starts.append(s)
+            s += L
+            if back_step == 1:
+                xi, xo = Xs[:-1], Xs[1:]
+                if target == "delta":
+                    xo = Xs[1:] - Xs[:-1]
+            elif back_step == 2:
+                xi = torch.cat((Xs[1:-1], Xs[:-2]), 1)
+                xo = Xs[2:] if target == "full" else Xs[2:] - Xs[1:-1]
+            else:
+                raise ValueError("target must be either 'full' or 'delta' \n back_step must be either 1 or 2")
+            if target not in ("full", "delta"):
+                raise ValueError("target must be either 'full' or 'delta' \n back_step must be either 1 or 2")
+            Xin.append(xi)
+            Xout.append(xo)
+        return torch.cat(Xin, 0), torch.cat(Xout, 0), starts
+
+    # ---- latent init + precompute (gpmdm.py:762-777, 1275-1305) ------------------
+    def init_X(self):
+        """PCA initialisation of the latents (gpmdm.py:762-777), then the precompute."""
+        from sklearn.decomposition import PCA   # the reference's own dependency (gpmdm.py:12)
+        X0 = PCA(n_components=self.d).fit_transform(self.get_Y())
+        self.X = torch.tensor(X0, dtype=torch.float64)
+        self._precompute_kernel_inverses()
+
+    def set_latents(self, X):
+        """Install trained latents (e.g. from a saved model) and rebuild the device model."""
+        self.X = torch.as_tensor(_to_np(X), dtype=torch.float64).clone()
+        self._precompute_kernel_inverses()
+
+    def _class_dynamics_rows(self):
+        """Number of dynamics pairs per class (rows of the class-c block of Xin)."""
+        lag = self.dyn_back_step
+        return [sum(len(s) - lag for s in cls) for cls in self.class_aware_observations_list]
+
+    def _precompute_kernel_inverses(self):
+        if self.dyn_back_step != 1:
+            raise NotImplementedError("the particle-filter path supports dyn_back_step=1 (as the "
+                                      "reference PF does, gpmdm_pf.py:164)")
+        N = self.X.shape[0]
+        dev = self._precompute_device or (torch.device("cpu") if N <= 4096 else self.device)
+        f64 = dict(dtype=torch.float64, device=dev)
+        X = self.X.to(**f64)
+        Y = torch.as_tensor(self.get_Y(), **f64)
+        eye = lambda n: torch.eye(n, **f64)  # noqa: E731
+        ylog_ls, xlog_ls = self.y_log_lengthscales.to(dev), self.x_log_lengthscales.to(dev)
+        xlog_c = self.x_log_lin_coeff.to(dev)
+        with torch.no_grad():
+            Ky = torch.exp(-_sq_dist(X, X, ylog_ls)) + torch.exp(self.y_log_sigma_n.to(dev)) ** 2 * eye(N) \
+                + self.sigma_n_num_Y ** 2 * eye(N)
+            Ry = _chol_inv_factor(Ky, "K_y")
+            del Ky
+            beta = (Ry @ Ry.T) @ Y
+            Xin, Xout, _ = self.get_Xin_Xout_matrices(X=X.cpu())
+            Xin, Xout = Xin.to(dev), Xout.to(dev)
+            rows = self._class_dynamics_rows()
+            off = 0
+            dyn = []
+            for c in range(self.n_classes):
+                n_c = rows[c]
+                if n_c <= 0:
+                    raise ValueError(f"class {c} has no dynamics pairs")
+                xi, xo = Xin[off:off + n_c], Xout[off:off + n_c]
+                off += n_c
+                K = torch.exp(-_sq_dist(xi, xi, xlog_ls)) + torch.exp(self.x_log_sigma_n.to(dev)) ** 2 * eye(n_c) \
+                    + self.sigma_n_num_X ** 2 * eye(n_c)
+                K = K + _lin(xi, xi, xlog_c)
+                K = K + 1e-6 * eye(n_c)
+                Rc = _chol_inv_factor(K, f"K_x class {c}")
+                alpha = (Rc @ Rc.T) @ xo
+                dyn.append((xi.cpu().numpy().copy(), Rc.cpu().numpy().copy(), alpha.cpu().numpy().copy()))
+            obs = (Ry.cpu().numpy().copy(), beta.cpu().numpy().copy())
+        self._upload(obs, dyn)
+
+    def _upload(self, obs, dyn):
+        lib = _lib.load()
+        C, d, D = self.n_classes, self.d, self.D
+        keep = []   # keep arrays alive during the call
+
+        def arr(a):
+            a = np.ascontiguousarray(a, dtype=np.float64)
+            keep.append(a)
+            return _lib.dptr(a)
+
+        Ry, beta = obs
+        desc = _lib.ModelDesc()
+        desc.N, desc.D, desc.d, desc.C = self.X.shape[0], D, d, C
+        desc.X = arr(self.X.numpy())
+        desc.obs_R = arr(Ry)
+        desc.obs_beta = arr(beta)
+        desc.y_lengthscales = arr(torch.exp(self.y_log_lengthscales).numpy())
+        desc.y_inv_lambda2 = arr((torch.exp(self.y_log_lambdas) ** -2).numpy())
+        nc = np.asarray([x[0].shape[0] for x in dyn], dtype=np.int64)
+        keep.append(nc)
+        desc.Nc = _lib.i64ptr(nc)
+        PtrArr = _lib._dp * C
+        xin_p = PtrArr(*[arr(x[0]) for x in dyn])
+        r_p = PtrArr(*[arr(x[1]) for x in dyn])
+        a_p = PtrArr(*[arr(x[2]) for x in dyn])
+        keep += [xin_p, r_p, a_p]
+        desc.Xin, desc.dyn_R, desc.dyn_alpha = xin_p, r_p, a_p
+        desc.x_lengthscales = arr(torch.exp(self.x_log_lengthscales).numpy())
+        desc.x_lin_coeff2 = arr((torch.exp(self.x_log_lin_coeff) ** 2).numpy())
+        desc.x_inv_lambda2 = arr((torch.exp(self.x_log_lambdas) ** -2).numpy())
+        handle = ctypes.c_void_p()
+        self._release()
+        _lib.check(lib.gpmdm_model_create(ctypes.byref(desc), self.device.index or 0, ctypes.byref(handle)),
+                   "gpmdm_model_create")
+        self._handle = handle
+
+    def _release(self):
+        if getattr(self, "_handle", None) is not None and self._handle.value:
+            _lib.load().gpmdm_model_destroy(self._handle)
+        self._handle = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        if self._handle is None:
+            raise RuntimeError("model not initialised: call init_X() (or load a saved model)")
+        return self._handle
+
+    # ---- predictive maps (gpmdm.py:923-963, 1032-1068) --------------------------
+    def _predict(self, Xstar, class_index=None):
+        xs = torch.as_tensor(Xstar, dtype=torch.float64)
+        out_dev = xs.device
+        xs = xs.to(self.device).contiguous()
+        n = xs.shape[0]
+        width = self.D if class_index is None else self.d
+        mu = torch.empty((n, width), dtype=torch.float64, device=self.device)
+        var = torch.empty((n, width), dtype=torch.float64, device=self.device)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        lib = _lib.load()
+        if class_index is None:
+            _lib.check(lib.gpmdm_predict_obs(self.handle, xs.data_ptr(), n, mu.data_ptr(), var.data_ptr(), stream),
+                       "map_x_to_y")
+        else:
+            _lib.check(lib.gpmdm_predict_dyn(self.handle, int(class_index), xs.data_ptr(), n,
+                                             mu.data_ptr(), var.data_ptr(), stream),
+                       "map_x_dynamics_for_class")
+        return mu.to(out_dev), var.to(out_dev)
+
+    def map_x_to_y(self, Xstar, flg_noise: bool = False):
+        """gpmdm.py:923-963: mean and diagonal variance of the observation GP at Xstar."""
+        mu, var = self._predict(Xstar)
+        if flg_noise:   # gpmdm.py:988-989
+            extra = float(torch.exp(self.y_log_sigma_n) ** 2) + self.sigma_n_num_Y ** 2
+            var = var + extra * (torch.exp(self.y_log_lambdas) ** -2).to(var.device)[None, :]
+        return mu, var
+
+    def map_x_dynamics_for_class(self, Xstar, class_index: int, flg_noise: bool = False):
+        """gpmdm.py:1032-1068: mean and diagonal variance of class c's dynamics GP."""
+        if not 0 <= int(class_index) < self.n_classes:
+            raise ValueError("class_index out of range")
+        mu, var = self._predict(Xstar, class_index)
+        if flg_noise:   # gpmdm.py:1095-1098
+            extra = float(torch.exp(self.x_log_sigma_n) ** 2) + self.sigma_n_num_X ** 2
+            var = var + extra * (torch.exp(self.x_log_lambdas) ** -2).to(var.device)[None, :]
+        return mu, var
+
+    # ---- persistence (gpmdm.py:1307-1414) ---------------------------------------
+    def config_dict(self):
+        return {
+            "D": self.D, "d": self.d, "n_classes": self.n_classes,
+            "dyn_target": self.dyn_target, "dyn_back_step": self.dyn_back_step,
+            "sigma_n_num_X": self.sigma_n_num_X, "sigma_n_num_Y": self.sigma_n_num_Y,
+            "y_lengthscales_init": torch.exp(self.y_log_lengthscales).tolist(),
+            "y_lambdas_init": torch.exp(self.y_log_lambdas).tolist(),
+            "y_sigma_n_init": float(torch.exp(self.y_log_sigma_n)),
+            "x_lengthscales_init": torch.exp(self.x_log_lengthscales).tolist(),
+            "x_lambdas_init": torch.exp(self.x_log_lambdas).tolist(),
+            "x_sigma_n_init": float(torch.exp(self.x_log_sigma_n)),
+            "x_lin_coeff_init": torch.exp(self.x_log_lin_coeff).tolist(),
+        }
+
+    def save(self, file_path) -> None:
+        """Save to a pickle-free ``.npz`` (the reference's torch.save dict holds numpy
+        arrays that torch>=2.6 refuses to load with weights_only=True)."""
+        arrays = {"X": self.X.numpy()}
+        seq_len = []
+        for c, cls in enumerate(self.class_aware_observations_list):
+            for k, y in enumerate(cls):
+                arrays[f"obs_{c}_{k}"] = _to_np(y, np.float64 if np.asarray(y).dtype == np.float64 else np.float32)
+            seq_len.append(len(cls))
+        arrays["n_seq"] = np.asarray(seq_len, dtype=np.int64)
+        for k in ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n", "x_log_lengthscales",
+                  "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff"):
+            arrays[k] = getattr(self, k).numpy()
+        cfg = self.config_dict()
+        arrays["cfg_int"] = np.asarray([cfg["D"], cfg["d"], cfg["n_classes"], cfg["dyn_back_step"]], dtype=np.int64)
+        arrays["cfg_target"] = np.asarray([0 if cfg["dyn_target"] == "full" else 1], dtype=np.int64)
+        arrays["cfg_num"] = np.asarray([cfg["sigma_n_num_X"], cfg["sigma_n_num_Y"]], dtype=np.float64)
+        np.savez(file_path, **arrays)
+
+    @classmethod
+    def load(cls, file_path, flg_print: bool = False, device=None) -> "GPMDM":
+        """Load a model saved by ``save`` (.npz), or a reference ``.pth`` through
+        ``torch.load(weights_only=True)`` with numpy arrays allow-listed."""
+        path = Path(file_path)
+        if path.suffix == ".npz":
+            f = np.load(path, allow_pickle=False)
+            D, d, C, bs = (int(v) for v in f["cfg_int"])
+            target = "full" if int(f["cfg_target"][0]) == 0 else "delta"
+            m = cls(D=D, d=d, n_classes=C, dyn_target=target, dyn_back_step=bs,
+                    y_lambdas_init=np.exp(f["y_log_lambdas"]), y_lengthscales_init=np.exp(f["y_log_lengthscales"]),
+                    y_sigma_n_init=float(np.exp(f["y_log_sigma_n"])), x_lambdas_init=np.exp(f["x_log_lambdas"]),
+                    x_lengthscales_init=np.exp(f["x_log_lengthscales"]),
+                    x_sigma_n_init=float(np.exp(f["x_log_sigma_n"])),
+                    x_lin_coeff_init=np.exp(f["x_log_lin_coeff"]),
+                    sigma_n_num_X=float(f["cfg_num"][0]), sigma_n_num_Y=float(f["cfg_num"][1]), device=device)
+            for c in range(C):
+                for k in range(int(f["n_seq"][c])):
+                    m.add_data(f[f"obs_{c}_{k}"], c)
+            m.set_latents(f["X"])
+            return m
+        return cls._load_pth(path, device)
+
+    @classmethod
+    def _load_pth(cls, path, device):
+        """Reference checkpoint (gpmdm.py:1307-1414).  Only the safe loader is used."""
+        safe = [np.ndarray, np.dtype, np.core.multiarray._reconstruct] if hasattr(np, "core") else []
+        try:
+            safe.append(np.dtypes.Float32DType)
+            safe.append(np.dtypes.Float64DType)
+        except AttributeError:
+            pass
+        with torch.serialization.safe_globals(safe):
+            save_dict = torch.load(path, weights_only=True, map_location="cpu")
+        cfg, sd = save_dict["config_dict"], save_dict["state_dict"]
+        m = cls(D=cfg["D"], d=cfg["d"], n_classes=cfg["n_classes"], dyn_target=cfg["dyn_target"],
+                dyn_back_step=cfg["dyn_back_step"], y_lambdas_init=cfg["y_lambdas_init"],
+                y_lengthscales_init=cfg["y_lengthscales_init"], y_sigma_n_init=cfg["y_sigma_n_init"],
+                x_lambdas_init=cfg["x_lambdas_init"], x_lengthscales_init=cfg["x_lengthscales_init"],
+                x_sigma_n_init=cfg["x_sigma_n_init"], x_lin_coeff_init=cfg["x_lin_coeff_init"],
+                sigma_n_num_X=cfg["sigma_n_num_X"], sigma_n_num_Y=cfg["sigma_n_num_Y"], device=device)
+        m.class_aware_observations_list = cfg["class_aware_observations_list"]
+        for k in ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n", "x_log_lengthscales",
+                  "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff"):
+            setattr(m, k, sd[k].to(torch.float64).detach().clone())
+        m.set_latents(sd["X"])
+        return m
+
+    @classmethod
+    def from_arrays(cls, X, Y_sequences, y_log_lengthscales, y_log_lambdas, y_log_sigma_n,
+                    x_log_lengthscales, x_log_lambdas, x_log_sigma_n, x_log_lin_coeff,
+                    sigma_n_num_X=0.0, sigma_n_num_Y=0.0, dyn_target="full", device=None):
+        """Build from explicit latents / observations (Y_sequences[c] = list of arrays)."""
+        D = np.asarray(Y_sequences[0][0]).shape[1]
+        d = np.asarray(X).shape[1]
+        m = cls(D=D, d=d, n_classes=len(Y_sequences), dyn_target=dyn_target, dyn_back_step=1,
+                y_lambdas_init=np.exp(y_log_lambdas), y_lengthscales_init=np.exp(y_log_lengthscales),
+                y_sigma_n_init=float(np.exp(y_log_sigma_n)), x_lambdas_init=np.exp(x_log_lambdas),
+                x_lengthscales_init=np.exp(x_log_lengthscales), x_sigma_n_init=float(np.exp(x_log_sigma_n)),
+                x_lin_coeff_init=np.exp(x_log_lin_coeff), sigma_n_num_X=sigma_n_num_X,
+                sigma_n_num_Y=sigma_n_num_Y, device=device)
+        # keep the exact log parameters (exp/log round trips can move an ulp)
+        m.y_log_lengthscales = torch.as_tensor(np.asarray(y_log_lengthscales, dtype=np.float64))
+        m.y_log_lambdas = torch.as_tensor(np.asarray(y_log_lambdas, dtype=np.float64))
+        m.y_log_sigma_n = torch.as_tensor(float(y_log_sigma_n), dtype=torch.float64)
+        m.x_log_lengthscales = torch.as_tensor(np.asarray(x_log_lengthscales, dtype=np.float64))
+        m.x_log_lambdas = torch.as_tensor(np.asarray(x_log_lambdas, dtype=np.float64))
+        m.x_log_sigma_n = torch.as_tensor(float(x_log_sigma_n), dtype=torch.float64)
+        m.x_log_lin_coeff = torch.as_tensor(np.asarray(x_log_lin_coeff, dtype=np.float64))
+        for c, seqs in enumerate(Y_sequences):
+            for y in seqs:
+                m.add_data(np.asarray(y), c)
+        m.set_latents(X)
+        return m

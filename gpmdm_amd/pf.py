@@ -1,0 +1,243 @@
+"""GPMDM_PF -- drop-in mirror of ``/root/reference/gpmdm/gpmdm_pf.py`` on libgpmdm_hip.
+
+Same constructor, methods and properties as the reference class (gpmdm_pf.py:47-312);
+every per-frame computation runs in the HIP library.  Extra keyword options:
+
+* ``rng='torch'`` (default): the random draws come from torch's global CPU generator in
+  exactly the reference's order (``gpmdm_amd.replay``), so ``torch.manual_seed(s)``
+  reproduces the reference's sampling; ``rng='philox'`` draws on the device (no host
+  work per frame; the bench mode);
+* ``seed``: Philox key (default: drawn from torch's generator);
+* ``resample='multinomial'`` (reference, gpmdm_pf.py:211) or ``'systematic'``;
+* ``process_group``: a ``torch.distributed`` group to shard particles over (one process
+  per GPU; one all-gather of the packed particle rows per frame).
+
+Reference quirks kept for parity: log variance counted twice in the
+log-likelihood, float32 ``ln 2pi``, non-recursive weights, read-outs pairing
+post-resample classes/states with pre-resample weights, ``ll + log_w`` in the posterior,
+``log_likelihood()`` returning a sum of exponentials, ``dyn_target`` ignored.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib, replay
+from .model import GPMDM
+
+
+class GPMDM_PF:
+    def __init__(self, gpmdm: GPMDM, markov_switching_model, num_particles: int, *,
+                 rng: str = "torch", seed=None, resample: str = "multinomial", process_group=None):
+        self._gpmdm = gpmdm
+        self._gpmdm.set_evaluation_mode()
+        self._markov_switching_model = torch.as_tensor(markov_switching_model).type(self.dtype)
+        self._num_particles = int(num_particles)
+        if self._gpmdm.n_classes != self._markov_switching_model.size(0):
+            raise ValueError("Number of classes in the GPMDM model and the Markov model do not match")
+        if rng not in ("torch", "philox"):
+            raise ValueError("rng must be 'torch' or 'philox'")
+        if resample not in ("multinomial", "systematic"):
+            raise ValueError("resample must be 'multinomial' or 'systematic'")
+        self._rng = rng
+        self._resample_mode = resample
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if rng == "philox" else 0
+        self._seed = int(seed)
+        self._group = process_group
+        if process_group is not None:
+            import torch.distributed as dist
+            self._world, self._rank = dist.get_world_size(process_group), dist.get_rank(process_group)
+        else:
+            self._world, self._rank = 1, 0
+        lib = _lib.load()
+        T = np.ascontiguousarray(self._markov_switching_model.numpy(), dtype=np.float64)
+        h = ctypes.c_void_p()
+        _lib.check(lib.gpmdm_pf_create(
+            gpmdm.handle, _lib.dptr(T), self._num_particles,
+            _lib.GPMDM_RNG_REPLAY if rng == "torch" else _lib.GPMDM_RNG_PHILOX,
+            ctypes.c_uint64(self._seed & (2 ** 64 - 1)),
+            _lib.GPMDM_RESAMPLE_MULTINOMIAL if resample == "multinomial" else _lib.GPMDM_RESAMPLE_SYSTEMATIC,
+            self._world, self._rank, ctypes.byref(h)), "GPMDM_PF")
+        self._h = h
+        self._readout = None
+        if self._world > 1:
+            w, lo, hi = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+            lib.gpmdm_pf_exchange_width(h, ctypes.byref(w), ctypes.byref(lo), ctypes.byref(hi))
+            dev = self.device
+            self._send = torch.empty((hi.value - lo.value, w.value), dtype=torch.float64, device=dev)
+            self._recv = torch.empty((self._num_particles, w.value), dtype=torch.float64, device=dev)
+        self._init_particles()
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None) is not None and self._h.value:
+                _lib.load().gpmdm_pf_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    # ---- helpers --------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _divide_into_n_parts(self, x: int, n: int) -> list:
+        """gpmdm_pf.py:287-292."""
+        g, r = divmod(x, n)
+        return [g + (1 if i < r else 0) for i in range(n)]
+
+    # ---- reference API ----------------------------------------------------------
+    def _init_particles(self):
+        """gpmdm_pf.py:87-115: P_c particles per class drawn from that class's latents."""
+        counts = self._divide_into_n_parts(self._num_particles, self.num_classes)
+        sizes = [self._gpmdm.get_X_for_class(c).shape[0] for c in range(self.num_classes)]
+        idx = replay.init_draws(sizes, counts)
+        states = np.concatenate([self._gpmdm.get_X_for_class(c).numpy()[idx[c]] for c in range(self.num_classes)], 0)
+        classes = np.concatenate([np.full(counts[c], c, dtype=np.int64) for c in range(self.num_classes)])
+        states = np.ascontiguousarray(states, dtype=np.float64)
+        _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "init")
+        self._readout = None
+
+    def reset(self):
+        self._init_particles()
+
+    def update(self, z):
+        """gpmdm_pf.py:117-135: switch classes, propagate dynamics, weight, resample."""
+        z = np.ascontiguousarray(torch.as_tensor(z, dtype=torch.float64).cpu().numpy().reshape(-1))
+        if z.shape[0] != self.observation_dim:
+            raise ValueError(f"observation must have {self.observation_dim} values, got {z.shape[0]}")
+        lib, h, s = _lib.load(), self._h, self._stream()
+        P, C, d = self._num_particles, self.num_classes, self.latent_dim
+        if self._rng == "torch":
+            E = np.ascontiguousarray(replay.switch_draws(P, C))
+            counts = np.zeros(C, dtype=np.int64)
+            _lib.check(lib.gpmdm_pf_switch(h, _lib.dptr(E), _lib.i64ptr(counts), s), "switch")
+            normals = np.ascontiguousarray(replay.dynamics_draws(counts, d))
+            _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), _lib.dptr(normals), s), "propagate")
+            self._exchange(s)
+            U = replay.resample_draws(P if self._resample_mode == "multinomial" else 1)
+            _lib.check(lib.gpmdm_pf_resample(h, _lib.dptr(np.ascontiguousarray(U)), s), "resample")
+        else:
+            _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
+            _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), None, s), "propagate")
+            self._exchange(s)
+            _lib.check(lib.gpmdm_pf_resample(h, None, s), "resample")
+        self._readout = None
+
+    step = update    # north-star name (BASELINE.json): one filter step
+
+    def update_with_draws(self, z, exp_draws, normals, uniforms):
+        """One update with explicit random draws in the reference's order (replay: see
+        gpmdm_amd.replay): exp_draws P x C, normals (sum_c P_c) x d grouped by class,
+        uniforms P (multinomial) or 1 (systematic).  Requires rng='torch'."""
+        if self._rng != "torch":
+            raise ValueError("explicit draws need rng='torch' (replay mode)")
+        z = np.ascontiguousarray(torch.as_tensor(z, dtype=torch.float64).cpu().numpy().reshape(-1))
+        lib, h, s = _lib.load(), self._h, self._stream()
+        P, C, d = self._num_particles, self.num_classes, self.latent_dim
+        E = np.ascontiguousarray(exp_draws, dtype=np.float64).reshape(P, C)
+        _lib.check(lib.gpmdm_pf_switch(h, _lib.dptr(E), None, s), "switch")
+        nrm = np.ascontiguousarray(normals, dtype=np.float64).reshape(P, d)
+        _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), _lib.dptr(nrm), s), "propagate")
+        self._exchange(s)
+        U = np.ascontiguousarray(uniforms, dtype=np.float64).reshape(-1)
+        _lib.check(lib.gpmdm_pf_resample(h, _lib.dptr(U), s), "resample")
+        self._readout = None
+
+    def _exchange(self, s):
+        if self._world == 1:
+            return
+        import torch.distributed as dist
+        lib = _lib.load()
+        _lib.check(lib.gpmdm_pf_pack(self._h, self._send.data_ptr(), s), "pack")
+        dist.all_gather_into_tensor(self._recv, self._send, group=self._group)
+        _lib.check(lib.gpmdm_pf_unpack(self._h, self._recv.data_ptr(), s), "unpack")
+
+    def _read(self):
+        if self._readout is None:
+            C, d = self.num_classes, self.latent_dim
+            post, mean, lik = np.zeros(C), np.zeros(d), np.zeros(1)
+            _lib.check(_lib.load().gpmdm_pf_read(self._h, _lib.dptr(post), _lib.dptr(mean), _lib.dptr(lik),
+                                                 self._stream()), "read")
+            self._readout = (post, mean, float(lik[0]))
+        return self._readout
+
+    def log_likelihood(self) -> float:
+        """gpmdm_pf.py:215-222 (as in the reference: sum exp(ll + log_w - max), not a log)."""
+        return self._read()[2]
+
+    def class_probabilities(self) -> torch.Tensor:
+        """gpmdm_pf.py:224-248."""
+        return torch.tensor(self._read()[0], dtype=torch.float64)
+
+    def get_most_likely_class(self) -> int:
+        """gpmdm_pf.py:250-254."""
+        return int(torch.argmax(self.class_probabilities()).item())
+
+    def current_state_mean(self) -> torch.Tensor:
+        """gpmdm_pf.py:256-262."""
+        return torch.tensor(self._read()[1], dtype=torch.float64)
+
+    def predict(self) -> torch.Tensor:
+        """Dynamics-only one-step prediction of the latent mean: the average over the
+        current particles of each particle's class dynamics-GP mean (gpmdm.py:1032-1068).
+        Does not change the filter state and draws no random numbers."""
+        st = self.export_state()
+        X, cls = st["states"], st["classes"]
+        acc = np.zeros(self.latent_dim)
+        for c in range(self.num_classes):
+            m = cls == c
+            if m.any():
+                mu, _ = self._gpmdm.map_x_dynamics_for_class(torch.as_tensor(X[m]), c)
+                acc += mu.cpu().numpy().sum(0)
+        return torch.tensor(acc / X.shape[0], dtype=torch.float64)
+
+    # ---- introspection (tests, checkpoint of the filter state) --------------------
+    def export_state(self) -> dict:
+        P, d = self._num_particles, self.latent_dim
+        out = dict(states=np.zeros((P, d)), classes=np.zeros(P, dtype=np.int64), ll=np.zeros(P),
+                   log_w=np.zeros(P), w=np.zeros(P), resample_idx=np.zeros(P, dtype=np.int64))
+        _lib.check(_lib.load().gpmdm_pf_export(
+            self._h, _lib.dptr(out["states"]), _lib.i64ptr(out["classes"]), _lib.dptr(out["ll"]),
+            _lib.dptr(out["log_w"]), _lib.dptr(out["w"]), _lib.i64ptr(out["resample_idx"]), self._stream()),
+            "export")
+        return out
+
+    def load_state(self, states, classes):
+        """Set the particle states/classes (e.g. a reference pre-step state)."""
+        states = np.ascontiguousarray(states, dtype=np.float64).reshape(self._num_particles, self.latent_dim)
+        classes = np.ascontiguousarray(classes, dtype=np.int64).reshape(self._num_particles)
+        _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "load_state")
+        self._readout = None
+
+    def enable_timing(self, on: bool = True):
+        _lib.check(_lib.load().gpmdm_pf_enable_timing(self._h, 1 if on else 0))
+
+    def stage_times(self) -> dict:
+        ms = np.zeros(len(_lib.STAGES))
+        n = np.zeros(len(_lib.STAGES), dtype=np.int64)
+        _lib.check(_lib.load().gpmdm_pf_stage_times(self._h, _lib.dptr(ms), _lib.i64ptr(n)))
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(_lib.STAGES)}
+
+    # ---- properties (gpmdm_pf.py:267-285) ------------------------------------------
+    @property
+    def latent_dim(self):
+        return self._gpmdm.d
+
+    @property
+    def observation_dim(self):
+        return self._gpmdm.D
+
+    @property
+    def num_classes(self):
+        return self._gpmdm.n_classes
+
+    @property
+    def dtype(self):
+        return self._gpmdm.dtype
+
+    @property
+    def device(self):
+        return self._gpmdm.device

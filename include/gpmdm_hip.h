@@ -1,0 +1,166 @@
+/*
+ * gpmdm_hip.h -- C ABI of libgpmdm_hip.so, the MI355X (gfx950) engine for the GPMDM
+ * particle-filter inference step.
+ *
+ * The reference (Priyanshu4/gpmdm) is pure Python: its "boundary" is the class API of
+ * gpmdm/gpmdm_pf.py (GPMDM_PF) and the two predictive maps of gpmdm/gpmdm.py it calls.
+ * There is no FFI in the reference; each entry point below names the reference call it
+ * replaces (file:line under /root/reference).  The Python mirror of the reference API
+ * (gpmdm_amd.GPMDM / gpmdm_amd.GPMDM_PF) binds these through ctypes; INTEGRATION.md
+ * shows the binding.
+ *
+ * Conventions
+ *   - every function returns int: 0 = ok, < 0 = error (see GPMDM_E_*); the message of
+ *     the last error on the calling thread is gpmdm_last_error();
+ *   - all floating point is IEEE fp64, row-major, contiguous; class ids are int64 at the
+ *     boundary (int32 on the device);
+ *   - "host" pointers are ordinary CPU memory; "device" pointers are HIP device memory
+ *     owned by the caller (e.g. torch tensors' data_ptr());
+ *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).  A handle keeps
+ *     no stream of its own: launches go to the stream given to each call;
+ *   - a handle is not thread-safe; distinct handles are independent.
+ */
+#ifndef GPMDM_HIP_H
+#define GPMDM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPMDM_OK 0
+#define GPMDM_E_INVALID (-1)   /* bad argument / shape (reference raises ValueError) */
+#define GPMDM_E_HIP (-2)       /* HIP runtime failure */
+#define GPMDM_E_NOMEM (-3)     /* device allocation failed */
+#define GPMDM_E_STATE (-4)     /* call out of order (e.g. step before init) */
+
+#define GPMDM_RNG_REPLAY 0     /* draws supplied by the caller (torch-order replay) */
+#define GPMDM_RNG_PHILOX 1     /* draws generated on the device (Philox4x32-10) */
+
+#define GPMDM_RESAMPLE_MULTINOMIAL 0  /* torch.multinomial(w, P, True): inverse CDF (reference) */
+#define GPMDM_RESAMPLE_SYSTEMATIC 1   /* systematic resampling: one uniform per step */
+
+typedef struct gpmdm_model* gpmdm_model_t;
+typedef struct gpmdm_pf* gpmdm_pf_t;
+
+/*
+ * Model descriptor: everything the per-frame path reads, precomputed on the host the
+ * way gpmdm.py:1284-1305 (_precompute_kernel_inverses) does, restricted to class blocks.
+ * The library copies every array to the device; the caller may free them on return.
+ *
+ *   obs_R      N x N   upper-triangular U_y^-1 with K_y = U_y^T U_y, so K_y^-1 = R R^T
+ *                      (gpmdm.py:1286-1289)
+ *   obs_beta   N x D   K_y^-1 Y  (the mean weights of map_x_to_y, gpmdm.py:957)
+ *   dyn_R[c]   Nc x Nc upper-triangular U_c^-1 of the class-c block of K_x (gpmdm.py:1299-1305)
+ *   dyn_alpha[c] Nc x d  A_c Xout_c  (mean weights of map_x_dynamics_for_class, gpmdm.py:1064)
+ */
+typedef struct gpmdm_model_desc {
+  int64_t N;                     /* training latents (rows of X, Y) */
+  int32_t D;                     /* observation dimension */
+  int32_t d;                     /* latent dimension (<= 32) */
+  int32_t C;                     /* classes */
+  int32_t reserved;
+  const double* X;               /* N x d latents (particle initialisation is host-side) */
+  const double* obs_R;           /* N x N */
+  const double* obs_beta;        /* N x D */
+  const double* y_lengthscales;  /* d  : exp(y_log_lengthscales) */
+  const double* y_inv_lambda2;   /* D  : exp(y_log_lambdas)^-2 */
+  const int64_t* Nc;             /* C  : dynamics rows per class */
+  const double* const* Xin;      /* C pointers, Nc x d : dynamics inputs of class c */
+  const double* const* dyn_R;    /* C pointers, Nc x Nc */
+  const double* const* dyn_alpha;/* C pointers, Nc x d */
+  const double* x_lengthscales;  /* d   : exp(x_log_lengthscales) */
+  const double* x_lin_coeff2;    /* d+1 : exp(x_log_lin_coeff)^2 (bias last) */
+  const double* x_inv_lambda2;   /* d   : exp(x_log_lambdas)^-2 */
+} gpmdm_model_desc;
+
+/* Upload a model (replaces the device-side state GPMDM holds after GPMDM.load /
+ * init_X + _precompute_kernel_inverses, gpmdm.py:762-777, 1349-1414). */
+int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* out);
+int gpmdm_model_destroy(gpmdm_model_t model);
+
+/* GPMDM.map_x_to_y(Xstar, flg_noise=False)  (gpmdm.py:923-963).
+ * Xs_dev: n x d; mu_dev, var_dev: n x D (device, caller-owned). */
+int gpmdm_predict_obs(gpmdm_model_t model, const double* Xs_dev, int64_t n,
+                      double* mu_dev, double* var_dev, void* stream);
+
+/* GPMDM.map_x_dynamics_for_class(Xstar, c, flg_noise=False)  (gpmdm.py:1032-1068).
+ * Xs_dev: n x d; mu_dev, var_dev: n x d (device, caller-owned). */
+int gpmdm_predict_dyn(gpmdm_model_t model, int c, const double* Xs_dev, int64_t n,
+                      double* mu_dev, double* var_dev, void* stream);
+
+/* GPMDM_PF(gpmdm, markov_switching_model, num_particles)  (gpmdm_pf.py:47-85).
+ * T: C x C host.  Ranks own the contiguous particle range
+ * [rank*P/n_ranks, (rank+1)*P/n_ranks); particle state is replicated on every rank
+ * (the exchange is done by the caller: gpmdm_pf_pack / gpmdm_pf_unpack). */
+int gpmdm_pf_create(gpmdm_model_t model, const double* T, int64_t P, int rng_mode,
+                    uint64_t seed, int resample_mode, int n_ranks, int rank,
+                    gpmdm_pf_t* out);
+int gpmdm_pf_destroy(gpmdm_pf_t pf);
+
+/* _init_particles / reset()  (gpmdm_pf.py:87-115, 264-265): states P x d, classes P
+ * (host).  Clears weights to 1/P and log-likelihoods to 0 as the reference does. */
+int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes);
+
+/* _propogate_markov_switching  (gpmdm_pf.py:137-151).  exp_draws: P x C host (replay)
+ * or NULL (philox).  class_counts: C host, or NULL; when given, the post-switch class
+ * counts are copied back synchronously (the replay caller needs them to draw the
+ * per-class normals of the next stage). */
+int gpmdm_pf_switch(gpmdm_pf_t pf, const double* exp_draws, int64_t* class_counts,
+                    void* stream);
+
+/* _propogate_dynamics + _update_weights' likelihoods for this rank's particles
+ * (gpmdm_pf.py:153-192).  z: D host.  normals: (sum_c P_c) x d host in the reference's
+ * per-class order (replay) or NULL (philox). */
+int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* z, const double* normals, void* stream);
+
+/* Multi-rank exchange: pack this rank's rows [lo, hi) as (hi-lo) x (d+2) doubles
+ * {ll, class, state[d]}; unpack all P rows after an all-gather. */
+int gpmdm_pf_exchange_width(gpmdm_pf_t pf, int64_t* width, int64_t* lo, int64_t* hi);
+int gpmdm_pf_pack(gpmdm_pf_t pf, double* send_dev, void* stream);
+int gpmdm_pf_unpack(gpmdm_pf_t pf, const double* recv_dev, void* stream);
+
+/* _update_weights' normalisation + _resample + the read-outs  (gpmdm_pf.py:194-262,
+ * 302-312).  uniforms: P host (replay, multinomial), 1 host (replay, systematic) or NULL. */
+int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream);
+
+/* update(z) in one call  (gpmdm_pf.py:117-135): switch + propagate + resample.
+ * Single-rank only; replay draws must all be given (use the staged calls when the
+ * per-class normal counts are not known in advance). */
+int gpmdm_pf_step(gpmdm_pf_t pf, const double* z, const double* exp_draws,
+                  const double* normals, const double* uniforms, void* stream);
+
+/* class_probabilities() / current_state_mean() / log_likelihood()
+ * (gpmdm_pf.py:224-262, 215-222).  Synchronises `stream`; any pointer may be NULL. */
+int gpmdm_pf_read(gpmdm_pf_t pf, double* posterior, double* mean, double* lik, void* stream);
+
+/* Export the full particle state to host (any pointer may be NULL): states P x d,
+ * classes P, ll P, log_w P, w P, resample indices P (of the last resample). */
+int gpmdm_pf_export(gpmdm_pf_t pf, double* states, int64_t* classes, double* ll,
+                    double* log_w, double* w, int64_t* resample_idx, void* stream);
+
+/* Per-stage device time (HIP events on the launch stream).  enable=1 starts recording,
+ * 0 stops.  gpmdm_pf_stage_times synchronises and returns, per stage, the summed
+ * milliseconds and the number of launches since the last call (then resets). */
+#define GPMDM_STAGE_SWITCH 0
+#define GPMDM_STAGE_DYN_GEMM 1
+#define GPMDM_STAGE_DYN_FINISH 2
+#define GPMDM_STAGE_OBS_GEMM 3
+#define GPMDM_STAGE_OBS_FINISH 4
+#define GPMDM_STAGE_RESAMPLE 5
+#define GPMDM_N_STAGES 6
+int gpmdm_pf_enable_timing(gpmdm_pf_t pf, int enable);
+int gpmdm_pf_stage_times(gpmdm_pf_t pf, double* ms, int64_t* launches);
+
+/* Message of the last failed call on this thread ("" if none). */
+const char* gpmdm_last_error(void);
+
+/* Library version string. */
+const char* gpmdm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GPMDM_HIP_H */
