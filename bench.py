@@ -1,0 +1,229 @@
+"""Benchmark: GPMDM particle-filter step on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Workload (BASELINE.json configs[1]): N=2000 training latents, D=62, d=3, C=2 classes,
+P=100,000 particles per GPU (weak scaling: P_total = 100k x GPUs), synthetic model and
+observation stream.  One step = ``update(z)`` + ``class_probabilities()``
++ ``current_state_mean()``, the notebook's per-frame loop (test_gpmdm_pf.ipynb:197-201),
+with device-side Philox draws and the reference's multinomial resampling.
+
+Prints ONE JSON line (rank 0) with the contract fields plus:
+  roofline      dominant kernel (observation-GP tile kernel) vs the FP64 MFMA peak;
+                achieved = algorithmic FLOPs per launch (SURVEY §8(d) dense form,
+                2N^2 + 2ND per particle) / mean launch time from HIP events on the
+                launch stream; traffic = HBM bytes per launch from the committed rocprofv3
+                PMC summary (profiles/), or null
+  cpu_baseline  the CPU oracle (numpy fp64, BLAS threads stated) on a bounded sample
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "particle-steps/sec (P×timesteps) + achieved HBM GB/s, N=2000 D=62 d=3"
+FP64_MFMA_PEAK_TFLOPS = 78.6          # MI355X spec (dense FP64 matrix); measured 77.1 (profiles/)
+WORKLOAD = dict(C=2, S=5, L=200, D=62, d=3, P_per_gpu=100_000)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_model(device):
+    from gpmdm_amd import GPMDM, synthetic
+    w = WORKLOAD
+    data = synthetic.make_sequences(w["C"], w["S"], w["L"], w["D"], w["d"], seed=0)
+    hp = synthetic.default_hyperparameters(w["D"], w["d"], 0.1)
+    m = GPMDM(D=w["D"], d=w["d"], n_classes=w["C"], dyn_target="full", dyn_back_step=1, device=device, **hp)
+    for c in range(w["C"]):
+        for y in data.sequences[c]:
+            m.add_data(y, c)
+    m.init_X()
+    return m, data
+
+
+def obs_kernel_flops(N, D, Nr_tile=128, bk=16):
+    """Algorithmic (dense-form) and executed FLOPs per particle of the
+    observation-GP tile kernel."""
+    alg = 2.0 * N * N + 2.0 * N * D
+    ncols = -(-(N + D) // Nr_tile) * Nr_tile
+    executed = 0.0
+    for J in range(ncols // Nr_tile):
+        kmax = min(N, (J + 1) * Nr_tile)
+        executed += 2.0 * Nr_tile * (-(-kmax // bk) * bk)
+    return alg, executed
+
+
+def pmc_traffic():
+    """HBM bytes per launch of the obs tile kernel from the committed PMC summary."""
+    p = ROOT / "profiles" / "pmc_summary.json"
+    if not p.exists():
+        return None
+    try:
+        j = json.loads(p.read_text())
+        return j.get("obs_gemm_hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(data, budget_s=12.0):
+    """The numpy oracle on the same workload shape, bounded sample (P_sample particles)."""
+    from oracle import gpmdm_oracle as O
+    from gpmdm_amd import synthetic
+    import torch
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    w = WORKLOAD
+    from sklearn.decomposition import PCA
+    Y = np.concatenate([y for c in data.sequences for y in c]).astype(np.float64)
+    X = PCA(n_components=w["d"]).fit_transform(Y)
+    hp = synthetic.default_hyperparameters(w["D"], w["d"], 0.1)
+    m = O.OracleModel(X=X, Y=Y, seq_lengths=[[w["L"]] * w["S"]] * w["C"],
+                      y_log_lengthscales=np.log(hp["y_lengthscales_init"]), y_log_lambdas=np.log(hp["y_lambdas_init"]),
+                      y_log_sigma_n=np.log(0.1), x_log_lengthscales=np.log(hp["x_lengthscales_init"]),
+                      x_log_lambdas=np.log(hp["x_lambdas_init"]), x_log_sigma_n=np.log(0.1),
+                      x_log_lin_coeff=np.log(hp["x_lin_coeff_init"])).precompute()
+    T = synthetic.markov_matrix(w["C"])
+    Ps = 2000
+    rng = np.random.RandomState(0)
+    parts = [rng.randint(0, m.X_for_class(c).shape[0], Ps // w["C"]) for c in range(w["C"])]
+    s, c = O.init_particles(m, Ps, parts)
+    z = data.observation_stream(64, seed=1)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        r = O.step(m, T, s, c, z[steps % 64], rng.exponential(size=(Ps, w["C"])), rng.randn(Ps, w["d"]), rng.rand(Ps))
+        s, c = r.states, r.classes
+        steps += 1
+        el = time.perf_counter() - t0
+        if el > budget_s or steps >= 50:
+            break
+    del torch
+    return {"value": Ps * steps / el, "unit": "particle-steps/s", "cores": int(cores), "kind": "port",
+            "sample": f"oracle (numpy fp64 restatement) N=2000 D=62 d=3 C=2, P={Ps} particles x {steps} steps "
+                      f"in {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        group = dist.group.WORLD
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from gpmdm_amd import GPMDM_PF, build
+    from gpmdm_amd import _lib
+    build.build()
+    _lib.load()
+    t_setup = time.perf_counter()
+    model, data = build_model(device)
+    P_total = WORKLOAD["P_per_gpu"] * world
+    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]], dtype=torch.float64)
+    torch.manual_seed(11)
+    pf = GPMDM_PF(model, T, P_total, rng="philox", seed=11, process_group=group)
+    zs = data.observation_stream(args.warmup + args.steps, seed=1)
+    log(f"[bench] rank {rank}/{world} setup {time.perf_counter() - t_setup:.1f}s, P_total={P_total}")
+
+    def one(k):
+        pf.update(zs[k])
+        pf.get_most_likely_class()
+        pf.class_probabilities()
+        pf.current_state_mean()
+
+    for k in range(args.warmup):
+        one(k)
+    torch.cuda.synchronize()
+    pf.stage_times()                # drop warm-up records
+    pf.enable_timing(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one(args.warmup + k)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    pf.enable_timing(False)
+    stages = pf.stage_times()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    post = pf.class_probabilities().numpy()
+
+    N, D, d = model.X.shape[0], model.D, model.d
+    P_local = P_total // world
+    alg, executed = obs_kernel_flops(N, D)
+    obs_ms, obs_n = stages["obs_gemm"]
+    obs_launch_s = obs_ms / max(obs_n, 1) / 1e3
+    achieved = alg * P_local / obs_launch_s / 1e12
+    rec = {
+        "metric": METRIC,
+        "value": P_total * args.steps / elapsed,
+        "unit": "particle-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (SURVEY §8(d) generator; random-phase sinusoid mocap surrogate, PCA latents)",
+        "config": {"workload": "configs[1]: N=2000 D=62 d=3 C=2, P=100k particles per GPU, philox draws, "
+                               "multinomial resampling",
+                   "N": N, "D": D, "d": d, "C": model.n_classes, "P_per_gpu": P_local, "P_total": P_total,
+                   "parallelism": f"particles sharded over {world} GPU(s), one all-gather per step"},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": pmc_traffic(),
+                     "kernel": "k_gp_tile<3,false> (observation GP)",
+                     "flops_per_particle_algorithmic": alg, "flops_per_particle_executed": executed,
+                     "executed_tflops": executed * P_local / obs_launch_s / 1e12,
+                     "launch_ms": obs_launch_s * 1e3},
+        "stages_ms_per_step": {k: v[0] / max(v[1], 1) for k, v in stages.items()},
+        "posterior_last": [float(x) for x in post],
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            rec["cpu_baseline"] = cpu_baseline(data)
+        except Exception as e:  # the baseline is reported, never the target
+            log(f"[bench] cpu baseline failed: {e!r}")
+            rec["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
