@@ -59,64 +59,95 @@ inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
 
 bool supported_d(int d) { return (d >= 1 && d <= 16) || d == 24 || d == 32; }
 
-// One GP's device image: scaled inputs, raw inputs, and B = [R | M] zero padded.
+// One GP's device image: scaled inputs (+ squared norms), raw inputs, and B = [R | M] in
+// MFMA-fragment order.
+//
+// Fragment layout (consumed by gp_tile.hip): column block J (256 columns) stores
+// ksteps(block_kmax(J)) K-steps; each K-step holds 4 waves x 1024 doubles, and inside a
+// wave's 1024 doubles the value v = 2q + e of lane l sits at q*128 + 2l + e, where
+// v = kk*4 + nt is the B operand of MFMA sub-step kk (K=4) for column tile nt:
+//   B[row = 16 ks + 4 kk + (l >> 4)][col = 256 J + 64 w + 16 nt + (l & 15)].
+// A lane's 16 values are therefore 8 x 16-byte loads, each wave-instruction reading one
+// contiguous 1 KiB.  Rows below the diagonal of R are never stored (triangular skip).
 struct GpImage {
-  int n_rows = 0, n_m = 0, n_j = 0, k_pad = 0;
-  long long ld = 0;
+  int n_rows = 0, n_m = 0, n_j = 0, n_wc = 0;
   double* Xs = nullptr;   // n_rows x d, inputs / lengthscales
+  double* Xsq = nullptr;  // n_rows
   double* Xl = nullptr;   // n_rows x d, raw inputs (dynamics)
-  double* B = nullptr;
+  double* Bf = nullptr;
 
   void release() {
     dfree(Xs);
+    dfree(Xsq);
     dfree(Xl);
-    dfree(B);
+    dfree(Bf);
   }
   SegDesc seg() const {
     SegDesc s{};
     s.Xs = Xs;
+    s.Xsq = Xsq;
     s.Xl = Xl;
-    s.B = B;
-    s.ld = ld;
+    s.Bf = Bf;
     s.n_rows = n_rows;
     s.n_m = n_m;
     s.n_j = n_j;
+    s.n_wc = n_wc;
     return s;
   }
-  int n_parts() const { return 2 * (int)cdiv(n_rows, kNT); }
+  int n_parts() const { return (int)cdiv(n_rows, kNB); }   // column blocks holding R columns
 };
 
-// Build B = [triu(R) | M] in row chunks and upload it; inputs scaled by the lengthscales.
 int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const double* ls,
                 bool keep_raw, const double* R, const double* M) {
   g.n_rows = n_rows;
   g.n_m = n_m;
-  g.ld = cdiv(n_rows + n_m, kNT) * kNT;
-  g.n_j = (int)(g.ld / kNT);
-  g.k_pad = (int)(cdiv(n_rows, kBK) * kBK);
-  std::vector<double> xs((size_t)n_rows * d);
-  for (long long i = 0; i < n_rows; ++i)
-    for (int j = 0; j < d; ++j) xs[i * d + j] = X[i * d + j] / ls[j];
+  g.n_wc = (int)cdiv(n_rows + n_m, kWC);
+  g.n_j = (int)cdiv(g.n_wc, 4);
+  std::vector<double> xs((size_t)n_rows * d), xsq(n_rows, 0.0);
+  for (long long i = 0; i < n_rows; ++i) {
+    double s = 0.0;
+    for (int j = 0; j < d; ++j) {
+      const double v = X[i * d + j] / ls[j];
+      xs[i * d + j] = v;
+      s += v * v;
+    }
+    xsq[i] = s;
+  }
   TRY(dalloc(&g.Xs, xs.size()));
   HIPCHK(hipMemcpy(g.Xs, xs.data(), xs.size() * sizeof(double), hipMemcpyHostToDevice));
+  TRY(dalloc(&g.Xsq, xsq.size()));
+  HIPCHK(hipMemcpy(g.Xsq, xsq.data(), xsq.size() * sizeof(double), hipMemcpyHostToDevice));
   if (keep_raw) {
     TRY(dalloc(&g.Xl, (size_t)n_rows * d));
     HIPCHK(hipMemcpy(g.Xl, X, (size_t)n_rows * d * sizeof(double), hipMemcpyHostToDevice));
   }
-  TRY(dalloc(&g.B, (size_t)g.k_pad * g.ld));
-  HIPCHK(hipMemset(g.B, 0, (size_t)g.k_pad * g.ld * sizeof(double)));
-  const long long chunk = 512;
-  std::vector<double> buf((size_t)chunk * g.ld);
-  for (long long r0 = 0; r0 < n_rows; r0 += chunk) {
-    const long long nr = std::min(chunk, (long long)n_rows - r0);
-    std::fill(buf.begin(), buf.begin() + nr * g.ld, 0.0);
-    for (long long r = 0; r < nr; ++r) {
-      const long long i = r0 + r;
-      double* row = buf.data() + r * g.ld;
-      for (long long j = i; j < n_rows; ++j) row[j] = R[i * n_rows + j];   // upper triangle only
-      for (int j = 0; j < n_m; ++j) row[n_rows + j] = M[i * n_m + j];
-    }
-    HIPCHK(hipMemcpy(g.B + r0 * g.ld, buf.data(), (size_t)nr * g.ld * sizeof(double), hipMemcpyHostToDevice));
+  long long total = 0;
+  for (int J = 0; J < g.n_j; ++J) total += (long long)ksteps(block_kmax(J, n_rows)) * kFragStep;
+  TRY(dalloc(&g.Bf, (size_t)total));
+  auto val = [&](long long row, long long col) -> double {
+    if (row >= n_rows) return 0.0;
+    if (col < n_rows) return row <= col ? R[row * n_rows + col] : 0.0;   // upper triangle of R
+    const long long j = col - n_rows;
+    return j < n_m ? M[row * n_m + j] : 0.0;
+  };
+  long long off = 0;
+  std::vector<double> buf;
+  for (int J = 0; J < g.n_j; ++J) {
+    const int nks = ksteps(block_kmax(J, n_rows));
+    buf.assign((size_t)nks * kFragStep, 0.0);
+    for (int ks = 0; ks < nks; ++ks)
+      for (int w = 0; w < 4; ++w) {
+        double* dst = buf.data() + ((size_t)ks * 4 + w) * 1024;
+        for (int l = 0; l < 64; ++l)
+          for (int v = 0; v < 16; ++v) {
+            const int kk = v >> 2, nt = v & 3;
+            const long long row = (long long)ks * kBK + kk * 4 + (l >> 4);
+            const long long col = (long long)J * kNB + w * kWC + nt * 16 + (l & 15);
+            dst[(v >> 1) * 128 + 2 * l + (v & 1)] = val(row, col);
+          }
+      }
+    HIPCHK(hipMemcpy(g.Bf + off, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice));
+    off += (long long)buf.size();
   }
   return GPMDM_OK;
 }

@@ -9,27 +9,29 @@ namespace gpmdm {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------------
-// Fused GP tile "GEMM" geometry (see gp_tile.hip and DESIGN.md §3).
-//   one workgroup = 4 waves = a PT x NT tile of V = K* . B, where K* (particles x training
-//   rows) is generated on the fly and B = [R | M] is the extended weight matrix.
+// Fused GP tile geometry (see gp_tile.hip and DESIGN.md §3).
+//   one workgroup = 4 waves = 64 particles x 256 columns of V = K* . B, where K*
+//   (particles x training rows) is generated on the fly and B = [R | M] is the extended
+//   weight matrix stored in MFMA-fragment order (each wave owns 64 columns).
 // ---------------------------------------------------------------------------------
-constexpr int kPT = 128;          // particles per tile (MFMA M)
-constexpr int kNT = 128;          // columns of B per tile (MFMA N)
+constexpr int kPT = 64;           // particles per tile (MFMA M)
+constexpr int kWC = 64;           // columns per wave
+constexpr int kNB = 256;          // columns per workgroup (4 waves)
 constexpr int kBK = 16;           // training rows per K-step (4 x K=4 MFMA sub-steps)
-constexpr int kLDA = kPT + 16;    // LDS row strides (doubles): +128 B shifts rows by 32 banks
-constexpr int kLDB = kNT + 16;
+constexpr int kLDA = kPT + 16;    // LDS row stride (doubles): rows k, k+1 land 32 banks apart
+constexpr int kFragStep = 4 * 1024;  // doubles of B fragments per (block, K-step): 4 waves x 64 lanes x 16
 constexpr int kMaxSeg = 8;        // segments (classes) per launch
 constexpr int kMaxD = 32;         // latent dimension limit
 
 struct SegDesc {                  // one GP: the observation GP, or the class-c dynamics GP
   const double* Xs;               // n_rows x d : training inputs / lengthscales
+  const double* Xsq;              // n_rows     : |Xs_i|^2
   const double* Xl;               // n_rows x d : raw training inputs (linear kernel; dyn only)
-  const double* B;                // k_pad x ld : [R | M], zero padded (k_pad = ceil(n_rows/BK)*BK)
-  long long ld;                   // columns of B (multiple of kNT)
+  const double* Bf;               // B = [triu(R) | M] in fragment order (see capi.hip)
   int n_rows;                     // training rows = R columns
   int n_m;                        // mean columns (D or d)
-  int n_j;                        // column blocks = ld / kNT
-  int pad_;
+  int n_j;                        // column blocks of 256
+  int n_wc;                       // wave-columns (64 wide) holding real columns
 };
 
 struct TileParams {
@@ -46,11 +48,18 @@ struct TileParams {
   const double* X;                // particle rows, n x d
   double ls[kMaxD];               // RBF lengthscales
   double lin_c2[kMaxD + 1];       // linear-kernel c^2, bias last (dyn only)
-  double* qpart;                  // [2*J + wn][ld_q]: partial sums of (R^T k)^2
+  double* qpart;                  // [J][ld_q]: partial sums of (R^T k)^2 per column block
   long long ld_q;
   double* mu;                     // [out][ld_mu] mean columns
   long long ld_mu;
 };
+
+// Column-block geometry shared by the host (fragment layout) and the kernel.
+__host__ __device__ inline int block_kmax(int J, int n_rows) {   // rows column block J needs
+  const int hi = (J + 1) * kNB;
+  return hi < n_rows ? hi : n_rows;
+}
+__host__ __device__ inline int ksteps(int kmax) { return (kmax + kBK - 1) / kBK; }
 
 void launch_gp_tile(const TileParams& p, int d, bool dyn, hipStream_t stream);
 

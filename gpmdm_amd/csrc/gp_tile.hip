@@ -1,35 +1,77 @@
-// Fused GP predictive tile for gfx950: kernel row generation + FP64 MFMA contraction.
+// Fused GP predictive tile for gfx950: kernel-row generation + FP64 MFMA contraction.
 //
-// Replaces, for a tile of 128 particles x 128 columns:
+// Replaces, for a tile of 64 particles x 256 columns:
 //   observation GP  (gpmdm.py:955-959)  Ky* = exp(-|x*-X|^2/l^2),
 //                   mean = Ky*^T beta, var-quadratic form = Ky*^T Ky^-1 Ky*
 //   dynamics GP     (gpmdm.py:1061-1065) Kx* = RBF + linear kernel over the class-c rows,
 //                   mean = Kx*^T alpha_c, quadratic form = Kx*^T A_c Kx*
 // With K^-1 = R R^T (R = U^-1 from the reference's own Cholesky recipe, gpmdm.py:1286-1289)
-// the quadratic form is |R^T k|^2; R is upper triangular, so column block J only needs
-// training rows [0, (J+1)*NT): half the dense FLOPs.  B = [R | M] carries the mean
-// weights M (beta or alpha_c) as extra columns, so one pass produces both.
+// the quadratic form is |R^T k|^2.  R is upper triangular, so column block J only needs
+// training rows [0, (J+1)*256), and each wave stops at its own 64 columns: about half the
+// dense FLOPs.  B = [R | M] carries the mean weights M (beta or alpha_c) as extra columns,
+// so one pass produces both.
 //
-// Per workgroup (256 threads, 4 waves as 2 (M) x 2 (N), each wave 64 x 64 = 4x4 MFMA
-// 16x16 tiles of v_mfma_f64_16x16x4_f64):
-//   K-step of 16 training rows: each thread generates 8 kernel values (exp in fp64) and
-//   loads 4 x 16 B of B; they go to the other LDS buffer while the MFMAs of the current
-//   step run (double-buffered, one barrier per step).
-//   Epilogue: R columns -> per-row sum of squares (16-lane xor reduction) written as a
-//   partial per (column block, wave column); mean columns -> written to mu.
-// Workgroups are ordered heavy-first (largest column block first) so the triangular
-// imbalance is absorbed by the dispatcher, and consecutive workgroups share a B panel
-// (same J) so each XCD's L2 holds the panel its CUs stream.
+// Workgroup = 4 waves; wave w owns columns [256J + 64w, +64) for all 64 particles
+// (4 x 4 tiles of v_mfma_f64_16x16x4_f64, 128 accumulator VGPRs).  Per K-step of 16
+// training rows:
+//   * K* tile (64 x 16) generated once per workgroup: each thread makes 4 values
+//     (expansion-form distance as gpmdm.py:508-515, table-driven fp64 exp), stored to a
+//     double-buffered LDS image that all 4 waves read as A fragments;
+//   * B fragments stream from HBM/L2 straight into VGPRs (8 x 16 B per lane, one K-step
+//     ahead): B is stored in fragment order, so no LDS round trip and no re-layout;
+//   * one barrier per K-step.  Two workgroups per CU overlap each other's barriers.
+// Workgroups are ordered heavy-first (column block J descending), which both balances the
+// triangular work and makes concurrent workgroups share a B panel in each XCD's L2.
 #include "common.h"
 
 namespace gpmdm {
 
+// 2^(j/64), j = 0..63 (correctly rounded).
+__constant__ double kExp2Tab[64] = {
+    1.0, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
+    1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
+    1.0905077326652577, 1.102382583307841, 1.1143867425958924, 1.1265216186082418,
+    1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
+    1.189207115002721, 1.202156731452703, 1.215247359980469, 1.22848053610687,
+    1.241857812073484, 1.255380757024691, 1.2690509571917332, 1.2828700160787783,
+    1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.339667524053303,
+    1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
+    1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
+    1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
+    1.5422108254079407, 1.559004400237837, 1.5759808451078865, 1.593142151342267,
+    1.6104903319492543, 1.6280274218573478, 1.645755478153965, 1.6636765803267364,
+    1.681792830507429, 1.7001063537185235, 1.718619298122478, 1.7373338352737062,
+    1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
+    1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
+    1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951
+};
+
+// exp(x) for x <= ~0 (kernel values): x = 64 n / ln2-reduced, 5-term polynomial on
+// |r| <= ln2/128, 2^(j/64) table, ldexp.  <= 2 ulp; underflows to 0 like exp().
+__device__ __forceinline__ double exp_table(double x, const double* tab) {
+  x = fmax(x, -746.0);
+  const double n = __builtin_rint(x * 92.33248261689366);          // 64 / ln 2
+  double r = fma(n, -0.010830424696905538, x);                    // ln2/64, Cody-Waite hi
+  r = fma(n, 6.563929801064195e-13, r);                           //          ... lo
+  double p = fma(r, 1.0 / 120.0, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p *= r;                                                          // e^r - 1
+  const int ni = (int)n;
+  const double t = tab[ni & 63];
+  return ldexp(fma(t, p, t), ni >> 6);
+}
+
 template <int DI, bool DYN>
-__global__ __launch_bounds__(256, (DI <= 12 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
+__global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
   __shared__ double As[2][kBK][kLDA];
-  __shared__ double Bs[2][kBK][kLDB];
+  __shared__ double tab[64];
+  __shared__ double qred[4][kPT];
 
   const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x;
   const int J = prm.n_j_max - 1 - b / prm.tiles_ub;
   // tile index within this launch's segments (a launch may cover classes c0..c0+7)
@@ -40,133 +82,137 @@ __global__ __launch_bounds__(256, (DI <= 12 ? 2 : 1)) void k_gp_tile(const TileP
     if (t >= prm.seg_tile_start[s] && t < prm.seg_tile_start[s + 1]) c = s;
   c = __builtin_amdgcn_readfirstlane(c);
   if (c < 0) return;
-  const SegDesc sg = prm.seg[c];
-  if (J >= sg.n_j) return;
+  const int n_j = prm.seg[c].n_j;
+  if (J >= n_j) return;
+  const double* __restrict__ Xs = prm.seg[c].Xs;
+  const double* __restrict__ Xsq = prm.seg[c].Xsq;
+  const double* __restrict__ Xl = prm.seg[c].Xl;
+  const double* __restrict__ Bf = prm.seg[c].Bf;
+  const int n_rows = prm.seg[c].n_rows;
+  const int n_m = prm.seg[c].n_m;
+  const int n_wc = prm.seg[c].n_wc;
+
+  if (tid < 64) tab[tid] = kExp2Tab[tid];
 
   const int seg_begin = prm.seg_pos_begin[c];
   const int pos0 = seg_begin + (t - prm.seg_tile_start[c]) * kPT;
   const int pos_end = prm.seg_pos_end[c];
   const int out_base = prm.seg_out_base[c] - seg_begin;   // out = out_base + pos
 
-  // ---- particle coordinates of this thread's tile row ------------------------------
-  const int m = tid & (kPT - 1);
-  const int kh = __builtin_amdgcn_readfirstlane(tid >> 7);   // 0/1: even/odd K rows
+  // ---- this thread's particle (generation role: particle m, rows w + 4s) ----------
+  const int m = lane;
   int pos = pos0 + m;
-  if (pos >= pos_end) pos = pos0;                             // clamp (results unused)
+  if (pos >= pos_end) pos = pos0;                          // clamp (results unused)
   const int prow = prm.perm ? prm.perm[pos] : pos;
-  double a[DI];
+  double a2[DI];                                           // 2 x / l
   double u[DYN ? DI : 1];
-  double ubias = 0.0;
+  double asq = 0.0, ubias = 0.0;
 #pragma unroll
   for (int j = 0; j < DI; ++j) {
     const double x = prm.X[(long long)prow * DI + j];
-    a[j] = x / prm.ls[j];
+    const double xs = x / prm.ls[j];
+    asq = fma(xs, xs, asq);
+    a2[j] = 2.0 * xs;
     if constexpr (DYN) u[j] = prm.lin_c2[j] * x;
   }
   if constexpr (DYN) ubias = prm.lin_c2[DI];
 
-  const int n_rows = sg.n_rows;
-  const double* __restrict__ Xs = sg.Xs;
-  const double* __restrict__ Xl = sg.Xl;
-  const double* __restrict__ Bg = sg.B + (long long)J * kNT;
-  const long long ldb = sg.ld;
+  // ---- K ranges ------------------------------------------------------------------
+  const int nks = ksteps(block_kmax(J, n_rows));
+  const int wc = J * 4 + w;                                 // this wave's 64 columns
+  const int col_hi = J * kNB + (w + 1) * kWC;
+  const int nks_w = wc < n_wc ? ksteps(col_hi <= n_rows ? col_hi : n_rows) : 0;
+  long long boff = 0;                                       // fragments of blocks < J
+  for (int jj = 0; jj < J; ++jj) boff += (long long)ksteps(block_kmax(jj, n_rows)) * kFragStep;
+  const double* __restrict__ Bw = Bf + boff + w * 1024 + lane * 2;
 
-  auto gen = [&](int ks, double (&v)[8]) {
+  auto gen = [&](int ks, double (&v)[4]) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int i = ks * kBK + kh + 2 * s;                    // wave-uniform row
+    for (int s = 0; s < 4; ++s) {
+      const int i = ks * kBK + w + 4 * s;                  // wave-uniform training row
       double val = 0.0;
       if (i < n_rows) {
-        const double* xr = Xs + (long long)i * DI;
-        double dist = 0.0;
+        double x = -(asq + Xsq[i]);
 #pragma unroll
-        for (int j = 0; j < DI; ++j) {
-          const double dd = a[j] - xr[j];
-          dist = fma(dd, dd, dist);
-        }
-        val = exp(-dist);
+        for (int j = 0; j < DI; ++j) x = fma(a2[j], Xs[(long long)i * DI + j], x);
+        val = exp_table(x, tab);
         if constexpr (DYN) {
-          const double* xl = Xl + (long long)i * DI;
           double l = ubias;
 #pragma unroll
-          for (int j = 0; j < DI; ++j) l = fma(u[j], xl[j], l);
+          for (int j = 0; j < DI; ++j) l = fma(u[j], Xl[(long long)i * DI + j], l);
           val += l;
         }
       }
       v[s] = val;
     }
   };
-  const int brow = tid >> 6;          // 0..3
-  const int bcol = (tid & 63) * 2;    // 2 doubles (16 B) per lane: one row per wave-instruction
-  auto loadB = [&](int ks, double2 (&r)[4]) {
+  auto loadB = [&](int ks, double (&bb)[16]) {
+    if (ks < nks_w) {
+      const double* src = Bw + (long long)ks * kFragStep;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const long long row = (long long)ks * kBK + brow + 4 * q;
-      r[q] = *reinterpret_cast<const double2*>(Bg + row * ldb + bcol);
+      for (int q = 0; q < 8; ++q) {
+        const double2 x = *reinterpret_cast<const double2*>(src + q * 128);
+        bb[2 * q] = x.x;
+        bb[2 * q + 1] = x.y;
+      }
     }
   };
-  auto store = [&](int buf, const double (&v)[8], const double2 (&r)[4]) {
+  auto store = [&](int buf, const double (&v)[4]) {
 #pragma unroll
-    for (int s = 0; s < 8; ++s) As[buf][kh + 2 * s][m] = v[s];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) *reinterpret_cast<double2*>(&Bs[buf][brow + 4 * q][bcol]) = r[q];
+    for (int s = 0; s < 4; ++s) As[buf][w + 4 * s][m] = v[s];
   };
 
-  // K range: column j of R needs rows i <= j; mean columns need every row.
-  const int kmax = min(n_rows, (J + 1) * kNT);
-  const int nks = (kmax + kBK - 1) / kBK;
-
-  const int lane = tid & 63;
-  const int w = tid >> 6;
-  const int wm = w & 1, wn = w >> 1;
   const int li = lane & 15, lk = lane >> 4;
-
   d4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
 
+  double bcur[16], bnext[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) bcur[i] = bnext[i] = 0.0;
+  __syncthreads();                                           // table ready
   {
-    double v[8];
-    double2 r[4];
+    double v[4];
     gen(0, v);
-    loadB(0, r);
-    store(0, v, r);
+    store(0, v);
+    loadB(0, bcur);
   }
   __syncthreads();
 
   for (int ks = 0; ks < nks; ++ks) {
     const int buf = ks & 1;
     const bool more = ks + 1 < nks;
-    double v[8];
-    double2 r[4];
+    double v[4];
     if (more) {
-      loadB(ks + 1, r);
+      loadB(ks + 1, bnext);
       gen(ks + 1, v);
     }
+    if (ks < nks_w) {
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      double af[4], bf[4];
+      for (int kk = 0; kk < 4; ++kk) {
+        double af[4];
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) af[mt] = As[buf][kk * 4 + lk][wm * 64 + mt * 16 + li];
+        for (int mt = 0; mt < 4; ++mt) af[mt] = As[buf][kk * 4 + lk][mt * 16 + li];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) bf[nt] = Bs[buf][kk * 4 + lk][wn * 64 + nt * 16 + li];
+        for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bf[nt], acc[mt][nt], 0, 0, 0);
+          for (int nt = 0; nt < 4; ++nt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bcur[kk * 4 + nt], acc[mt][nt], 0, 0, 0);
+      }
     }
-    if (more) store(buf ^ 1, v, r);
+    if (more) store(buf ^ 1, v);
     __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bcur[i] = bnext[i];
   }
 
   // ---- epilogue --------------------------------------------------------------------
   // C/D layout of v_mfma_f64_16x16x4_f64: lane l, reg r -> row (l>>4) + 4r, col l&15.
-  const int colw = J * kNT + wn * 64;
-  const bool all_r = (J + 1) * kNT <= n_rows;
-  if (J * kNT < n_rows) {
+  const int colw = J * kNB + w * kWC;
+  const bool has_r = J * kNB < n_rows;
+  if (has_r) {
     double qs[4][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -176,16 +222,8 @@ __global__ __launch_bounds__(256, (DI <= 12 ? 2 : 1)) void k_gp_tile(const TileP
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           const double x = acc[mt][nt][r];
-          const int col = colw + nt * 16 + li;
-          if (all_r || col < n_rows) s = fma(x, x, s);
+          if (colw + nt * 16 + li < n_rows) s = fma(x, x, s);
         }
-        qs[mt][r] = s;
-      }
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double s = qs[mt][r];
         s += __shfl_xor(s, 1);
         s += __shfl_xor(s, 2);
         s += __shfl_xor(s, 4);
@@ -193,29 +231,33 @@ __global__ __launch_bounds__(256, (DI <= 12 ? 2 : 1)) void k_gp_tile(const TileP
         qs[mt][r] = s;
       }
     if (li == 0) {
-      double* qp = prm.qpart + (long long)(2 * J + wn) * prm.ld_q;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int p = pos0 + wm * 64 + mt * 16 + lk + 4 * r;
-          if (p < pos_end) qp[out_base + p] = qs[mt][r];
-        }
+        for (int r = 0; r < 4; ++r) qred[w][mt * 16 + lk + 4 * r] = qs[mt][r];
     }
   }
-  if (!all_r) {
+  if (colw + kWC > n_rows) {                                  // mean columns
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
       const int jm = colw + nt * 16 + li - n_rows;
-      if (jm >= 0 && jm < sg.n_m) {
+      if (jm >= 0 && jm < n_m) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int p = pos0 + wm * 64 + mt * 16 + lk + 4 * r;
+            const int p = pos0 + mt * 16 + lk + 4 * r;
             if (p < pos_end) prm.mu[(long long)(out_base + p) * prm.ld_mu + jm] = acc[mt][nt][r];
           }
       }
+    }
+  }
+  if (has_r) {
+    __syncthreads();
+    if (tid < kPT) {
+      const int p = pos0 + tid;
+      if (p < pos_end)
+        prm.qpart[(long long)J * prm.ld_q + out_base + p] = (qred[0][tid] + qred[1][tid]) + (qred[2][tid] + qred[3][tid]);
     }
   }
 }
