@@ -63,7 +63,16 @@ __device__ __forceinline__ double exp_table(double x, const double* tab) {
   return ldexp(fma(t, p, t), ni >> 6);
 }
 
-template <int DI, bool DYN>
+// VAR: experiment switches for tools/microbench/tile_bench.hip (production uses 0).
+//   bit 0: no per-wave triangular skip (every wave multiplies the block's full K range)
+//   bit 1: ablation -- replace the kernel-value generation by a cheap stand-in
+//   bit 2: ablation -- generation reads no training rows (constant row)
+//   bit 3: ablation -- no barrier in the K loop (wrong results; timing only)
+//   bit 4: ablation -- no generation and no A stores at all (MFMA + B stream bound)
+//   bit 5: ablation -- no B loads (B operands stay in registers)
+//   bit 6: ablation -- no LDS A-fragment reads (A operands from registers)
+//   bit 7: ablation -- every block runs the full K range (no triangular schedule)
+template <int DI, bool DYN, int VAR = 0>
 __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
   __shared__ double As[2][kBK][kLDA];
   __shared__ double tab[64];
@@ -118,43 +127,60 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
   if constexpr (DYN) ubias = prm.lin_c2[DI];
 
   // ---- K ranges ------------------------------------------------------------------
-  const int nks = ksteps(block_kmax(J, n_rows));
+  const int nks = (VAR & 128) ? ksteps(n_rows) : ksteps(block_kmax(J, n_rows));
   const int wc = J * 4 + w;                                 // this wave's 64 columns
   const int col_hi = J * kNB + (w + 1) * kWC;
-  const int nks_w = wc < n_wc ? ksteps(col_hi <= n_rows ? col_hi : n_rows) : 0;
+  int nks_w = wc < n_wc ? ksteps(col_hi <= n_rows ? col_hi : n_rows) : 0;
+  if constexpr (VAR & 129) nks_w = wc < n_wc ? nks : 0;
   long long boff = 0;                                       // fragments of blocks < J
   for (int jj = 0; jj < J; ++jj) boff += (long long)ksteps(block_kmax(jj, n_rows)) * kFragStep;
   const double* __restrict__ Bw = Bf + boff + w * 1024 + lane * 2;
 
+  // Branch-free generation (rows past n_rows are clamped, then zeroed) so the scalar row
+  // loads batch and the fp64 work can interleave with the MFMAs of the same K-step.
+  const int last_row = n_rows - 1;
   auto gen = [&](int ks, double (&v)[4]) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int i = ks * kBK + w + 4 * s;                  // wave-uniform training row
-      double val = 0.0;
-      if (i < n_rows) {
-        double x = -(asq + Xsq[i]);
+      const int ic = i < last_row ? i : last_row;
+      double x;
+      if constexpr (VAR & 4) {
+        x = -(asq + 0.5 * i);
 #pragma unroll
-        for (int j = 0; j < DI; ++j) x = fma(a2[j], Xs[(long long)i * DI + j], x);
-        val = exp_table(x, tab);
-        if constexpr (DYN) {
-          double l = ubias;
+        for (int j = 0; j < DI; ++j) x = fma(a2[j], 0.25 * j, x);
+      } else {
+        x = -(asq + Xsq[ic]);
 #pragma unroll
-          for (int j = 0; j < DI; ++j) l = fma(u[j], Xl[(long long)i * DI + j], l);
-          val += l;
-        }
+        for (int j = 0; j < DI; ++j) x = fma(a2[j], Xs[(long long)ic * DI + j], x);
       }
-      v[s] = val;
+      double val;
+      if constexpr (VAR & 2) val = fma(x, 1e-3, 1.0);
+      else val = exp_table(x, tab);
+      if constexpr (DYN) {
+        double l = ubias;
+#pragma unroll
+        for (int j = 0; j < DI; ++j) l = fma(u[j], Xl[(long long)ic * DI + j], l);
+        val += l;
+      }
+      v[s] = i < n_rows ? val : 0.0;
     }
   };
+  // B prefetch: unconditional (clamped to the wave's last K-step) so no branch sits
+  // between the loads and the registers they fill.
+  const int ks_last = nks_w > 0 ? nks_w - 1 : 0;
   auto loadB = [&](int ks, double (&bb)[16]) {
-    if (ks < nks_w) {
-      const double* src = Bw + (long long)ks * kFragStep;
+    if constexpr (VAR & 32) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const double2 x = *reinterpret_cast<const double2*>(src + q * 128);
-        bb[2 * q] = x.x;
-        bb[2 * q + 1] = x.y;
-      }
+      for (int q = 0; q < 16; ++q) bb[q] = bb[q] * 0.999 + 1e-3 * (ks & 1);
+      return;
+    }
+    const double* src = Bw + (long long)(ks < ks_last ? ks : ks_last) * kFragStep;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const double2 x = *reinterpret_cast<const double2*>(src + q * 128);
+      bb[2 * q] = x.x;
+      bb[2 * q + 1] = x.y;
     }
   };
   auto store = [&](int buf, const double (&v)[4]) {
@@ -169,43 +195,64 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
 
-  double bcur[16], bnext[16];
+  auto mfma_step = [&](int buf, const double (&bc)[16]) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) bcur[i] = bnext[i] = 0.0;
+    for (int kk = 0; kk < 4; ++kk) {
+      double af[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        if constexpr (VAR & 64) af[mt] = asq + mt + kk + buf;
+        else af[mt] = As[buf][kk * 4 + lk][mt * 16 + li];
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bc[kk * 4 + nt], acc[mt][nt], 0, 0, 0);
+    }
+  };
+  // one K-step with MFMAs: prefetch B(ks+1) into bn, generate K*(ks+1), MFMA on bc
+  // (the generation for ks+1 = nks is harmless: clamped rows, stored to a buffer that is
+  // never read again)
+  auto full_step = [&](int ks, const double (&bc)[16], double (&bn)[16]) {
+    double v[4];
+    loadB(ks + 1, bn);
+    if constexpr (!(VAR & 16)) gen(ks + 1, v);
+    mfma_step(ks & 1, bc);
+    if constexpr (!(VAR & 16)) store((ks + 1) & 1, v);
+    if constexpr (!(VAR & 8)) __syncthreads();
+  };
+
+  double b0[16], b1[16];
+  if constexpr (VAR & 32) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) { b0[q] = 1e-3 * q + lane; b1[q] = 2e-3 * q; }
+  }
   __syncthreads();                                           // table ready
   {
     double v[4];
     gen(0, v);
     store(0, v);
-    loadB(0, bcur);
+    loadB(0, b0);
   }
   __syncthreads();
 
-  for (int ks = 0; ks < nks; ++ks) {
-    const int buf = ks & 1;
-    const bool more = ks + 1 < nks;
+  // Phase 1: K-steps this wave multiplies (ping-pong B registers, no copies).
+  int ks = 0;
+  for (; ks + 1 < nks_w; ks += 2) {
+    full_step(ks, b0, b1);
+    full_step(ks + 1, b1, b0);
+  }
+  if (ks < nks_w) {
+    full_step(ks, b0, b1);
+    ++ks;
+  }
+  // Phase 2: the rest of the block's K range (other waves' columns): generate only.
+  for (; ks < nks; ++ks) {
     double v[4];
-    if (more) {
-      loadB(ks + 1, bnext);
-      gen(ks + 1, v);
-    }
-    if (ks < nks_w) {
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        double af[4];
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) af[mt] = As[buf][kk * 4 + lk][mt * 16 + li];
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-            acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bcur[kk * 4 + nt], acc[mt][nt], 0, 0, 0);
-      }
-    }
-    if (more) store(buf ^ 1, v);
+    gen(ks + 1, v);
+    store((ks + 1) & 1, v);
     __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 16; ++i) bcur[i] = bnext[i];
   }
 
   // ---- epilogue --------------------------------------------------------------------

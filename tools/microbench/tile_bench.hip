@@ -1,0 +1,93 @@
+// A/B timing of k_gp_tile variants (template VAR bits, see gp_tile.hip) on the
+// config-2 observation GP shape: N=2000, D=62, d=3, P=100k.  Variants run interleaved in
+// one process (cdna_hip_programming.md §5.4 rule 24); prints the median per variant.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/microbench/tile_bench.hip -o tools/microbench/tile_bench
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../../gpmdm_amd/csrc/gp_tile.hip"
+
+using namespace gpmdm;
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+template <int VAR>
+void launch_var(const TileParams& p, hipStream_t s) {
+  hipLaunchKernelGGL((k_gp_tile<3, false, VAR>), dim3(p.n_j_max * p.tiles_ub), dim3(256), 0, s, p);
+}
+
+int main(int argc, char** argv) {
+  const int N = 2000, D = 62, d = 3;
+  const int P = argc > 1 ? atoi(argv[1]) : 100000;
+  std::mt19937_64 rng(1);
+  std::normal_distribution<double> nd(0.0, 1.0);
+  const int n_wc = (N + D + kWC - 1) / kWC, n_j = (n_wc + 3) / 4;
+  long long total = 0;
+  for (int J = 0; J < n_j; ++J) total += (long long)ksteps(block_kmax(J, N)) * kFragStep;
+  std::vector<double> hB(total), hXs(N * d), hXsq(N), hX((size_t)P * d);
+  for (auto& v : hB) v = 0.01 * nd(rng);
+  for (int i = 0; i < N; ++i) {
+    double s = 0;
+    for (int j = 0; j < d; ++j) { hXs[i * d + j] = 2.0 * nd(rng); s += hXs[i * d + j] * hXs[i * d + j]; }
+    hXsq[i] = s;
+  }
+  for (auto& v : hX) v = 2.0 * nd(rng);
+  double *B, *Xs, *Xsq, *X, *q, *mu;
+  int* tab;
+  CK(hipMalloc(&B, total * 8)); CK(hipMalloc(&Xs, N * d * 8)); CK(hipMalloc(&Xsq, N * 8));
+  CK(hipMalloc(&X, (size_t)P * d * 8)); CK(hipMalloc(&q, (size_t)P * n_j * 8)); CK(hipMalloc(&mu, (size_t)P * D * 8));
+  CK(hipMalloc(&tab, 64));
+  CK(hipMemcpy(B, hB.data(), total * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(Xs, hXs.data(), N * d * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(Xsq, hXsq.data(), N * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(X, hX.data(), (size_t)P * d * 8, hipMemcpyHostToDevice));
+  const int ntiles = (P + kPT - 1) / kPT;
+  int ht[5] = {0, P, 0, 0, ntiles};
+  CK(hipMemcpy(tab, ht, sizeof(ht), hipMemcpyHostToDevice));
+  TileParams p{};
+  p.seg[0].Xs = Xs; p.seg[0].Xsq = Xsq; p.seg[0].Bf = B;
+  p.seg[0].n_rows = N; p.seg[0].n_m = D; p.seg[0].n_j = n_j; p.seg[0].n_wc = n_wc;
+  p.n_seg = 1; p.tiles_ub = ntiles; p.n_j_max = n_j;
+  p.seg_pos_begin = tab; p.seg_pos_end = tab + 1; p.seg_out_base = tab + 2; p.seg_tile_start = tab + 3;
+  p.X = X;
+  for (int j = 0; j < d; ++j) p.ls[j] = 1.0;
+  p.qpart = q; p.ld_q = P; p.mu = mu; p.ld_mu = D;
+
+  hipStream_t s = nullptr;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  typedef void (*L)(const TileParams&, hipStream_t);
+  L fns[] = {launch_var<0>, launch_var<112>, launch_var<113>, launch_var<240>, launch_var<248>, launch_var<128>, launch_var<1>};
+  const char* names[] = {"VAR0 production", "VAR112 pure MFMA (skip)", "VAR113 pure MFMA (no skip)",
+                         "VAR240 pure MFMA full-K blocks", "VAR248 same, no barrier", "VAR128 production ops, full-K",
+                         "VAR1 no skip"};
+  const int NV = 7, ROUNDS = 7;
+  std::vector<std::vector<float>> t(NV);
+  for (int v = 0; v < NV; ++v) fns[v](p, s);
+  CK(hipDeviceSynchronize());
+  for (int r = 0; r < ROUNDS; ++r)
+    for (int v = 0; v < NV; ++v) {
+      CK(hipEventRecord(e0, s));
+      for (int k = 0; k < 3; ++k) fns[v](p, s);
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      t[v].push_back(ms / 3);
+    }
+  // executed MFMA flops per launch (production schedule)
+  double rows = 0;
+  for (int wc = 0; wc < n_wc; ++wc) rows += ksteps(std::min((wc + 1) * kWC, N)) * kBK;
+  const double fl = 2.0 * kWC * rows * P;
+  // full-K schedule executed flops (VAR bit 7)
+  const double fl_full = 2.0 * kWC * n_wc * (double)ksteps(N) * kBK * P;
+  printf("(full-K schedule MFMA flops = %.3e per launch; production %.3e)\n", fl_full, fl);
+  for (int v = 0; v < NV; ++v) {
+    std::sort(t[v].begin(), t[v].end());
+    printf("%-30s median %.3f ms  min %.3f ms   (%.1f TF/s on the production schedule's MFMA flops)\n",
+           names[v], t[v][ROUNDS / 2], t[v][0], fl / t[v][ROUNDS / 2] / 1e9);
+  }
+  return 0;
+}
