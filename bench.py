@@ -53,7 +53,7 @@ def build_model(device):
     return m, data
 
 
-def obs_kernel_flops(N, D, nb=256, wc=64, bk=16):
+def obs_kernel_flops(N, D, bk=16):
     """FLOPs per particle of the observation-GP tile kernel.
 
     algorithmic: the implemented algorithm's useful work -- R^T k with R upper
@@ -61,17 +61,16 @@ def obs_kernel_flops(N, D, nb=256, wc=64, bk=16):
         mean k^T beta (2ND).  This is what roofline.achieved counts.
     dense_form: SURVEY §8(d)'s 2N^2 + 2ND (the reference's dense K^-1 quadratic form);
         it is twice the work actually required, so it is reported, not used as achieved.
-    executed: what the MFMAs issue (64-column wave tiles, 16-row K steps, zero padding).
+    executed: what the MFMAs issue: each 16-column tile runs K-steps of 16 rows up to its
+        diagonal (mean tiles: all rows).
     """
     algorithmic = N * (N + 1.0) + 2.0 * N + 2.0 * N * D
     dense_form = 2.0 * N * N + 2.0 * N * D
-    n_wc = -(-(N + D) // wc)
     rows = 0
-    for w in range(n_wc):
-        col_hi = (w + 1) * wc
-        kmax = min(col_hi, N)
+    for tc in range(-(-(N + D) // 16)):
+        kmax = min(tc * 16 + 16, N)
         rows += -(-kmax // bk) * bk
-    executed = 2.0 * wc * rows
+    executed = 2.0 * 16 * rows
     return algorithmic, dense_form, executed
 
 

@@ -65,8 +65,9 @@ bool supported_d(int d) { return (d >= 1 && d <= 16) || d == 24 || d == 32; }
 // Fragment layout (consumed by gp_tile.hip): column block J (256 columns) stores
 // ksteps(block_kmax(J)) K-steps; each K-step holds 4 waves x 1024 doubles, and inside a
 // wave's 1024 doubles the value v = 2q + e of lane l sits at q*128 + 2l + e, where
-// v = kk*4 + nt is the B operand of MFMA sub-step kk (K=4) for column tile nt:
-//   B[row = 16 ks + 4 kk + (l >> 4)][col = 256 J + 64 w + 16 nt + (l & 15)].
+// v = kk*4 + nt is the B operand of MFMA sub-step kk (K=4) for column tile nt of wave w,
+// whose 16 columns are interleaved with the other waves' tiles:
+//   B[row = 16 ks + 4 kk + (l >> 4)][col = 256 J + 16 (4 nt + w) + (l & 15)].
 // A lane's 16 values are therefore 8 x 16-byte loads, each wave-instruction reading one
 // contiguous 1 KiB.  Rows below the diagonal of R are never stored (triangular skip).
 struct GpImage {
@@ -142,7 +143,7 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
           for (int v = 0; v < 16; ++v) {
             const int kk = v >> 2, nt = v & 3;
             const long long row = (long long)ks * kBK + kk * 4 + (l >> 4);
-            const long long col = (long long)J * kNB + w * kWC + nt * 16 + (l & 15);
+            const long long col = (long long)J * kNB + 16 * (4 * nt + w) + (l & 15);
             dst[(v >> 1) * 128 + 2 * l + (v & 1)] = val(row, col);
           }
       }

@@ -11,9 +11,12 @@
 // dense FLOPs.  B = [R | M] carries the mean weights M (beta or alpha_c) as extra columns,
 // so one pass produces both.
 //
-// Workgroup = 4 waves; wave w owns columns [256J + 64w, +64) for all 64 particles
-// (4 x 4 tiles of v_mfma_f64_16x16x4_f64, 128 accumulator VGPRs).  Per K-step of 16
-// training rows:
+// Workgroup = 4 waves; wave w owns the four 16-column tiles at columns
+// 256J + 16(4t + w), t = 0..3 (interleaved, so all waves reach nearly the same K), for all
+// 64 particles (4 x 4 tiles of v_mfma_f64_16x16x4_f64, 128 accumulator VGPRs).  A tile of R
+// columns retires once K passes its diagonal: the K loop runs in phases with tiles
+// [T0, T1) active, so no MFMA multiplies the zero triangle and no wave idles while its
+// siblings (and the barrier) wait.  Per K-step of 16 training rows:
 //   * K* tile (64 x 16) generated once per workgroup: each thread makes 4 values
 //     (expansion-form distance as gpmdm.py:508-515, table-driven fp64 exp), stored to a
 //     double-buffered LDS image that all 4 waves read as A fragments;
@@ -22,6 +25,8 @@
 //   * one barrier per K-step.  Two workgroups per CU overlap each other's barriers.
 // Workgroups are ordered heavy-first (column block J descending), which both balances the
 // triangular work and makes concurrent workgroups share a B panel in each XCD's L2.
+#include <type_traits>
+
 #include "common.h"
 
 namespace gpmdm {
@@ -64,7 +69,7 @@ __device__ __forceinline__ double exp_table(double x, const double* tab) {
 }
 
 // VAR: experiment switches for tools/microbench/tile_bench.hip (production uses 0).
-//   bit 0: no per-wave triangular skip (every wave multiplies the block's full K range)
+//   bit 0: no tile retirement (every real tile runs to the block's last K-step)
 //   bit 1: ablation -- replace the kernel-value generation by a cheap stand-in
 //   bit 2: ablation -- generation reads no training rows (constant row)
 //   bit 3: ablation -- no barrier in the K loop (wrong results; timing only)
@@ -74,7 +79,11 @@ __device__ __forceinline__ double exp_table(double x, const double* tab) {
 //   bit 7: ablation -- every block runs the full K range (no triangular schedule)
 template <int DI, bool DYN, int VAR = 0>
 __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
+  constexpr int RW = DYN ? 2 * DI + 1 : DI + 1;             // row record: Xs[DI], |Xs|^2, (Xl[DI])
+  constexpr int NRV = kBK * RW;                              // row values per K-step
+  constexpr int RPT = (NRV + 255) / 256;                     // row values per thread
   __shared__ double As[2][kBK][kLDA];
+  __shared__ double RX[2][kBK][RW];
   __shared__ double tab[64];
   __shared__ double qred[4][kPT];
 
@@ -99,7 +108,7 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
   const double* __restrict__ Bf = prm.seg[c].Bf;
   const int n_rows = prm.seg[c].n_rows;
   const int n_m = prm.seg[c].n_m;
-  const int n_wc = prm.seg[c].n_wc;
+  const int n_cols = n_rows + n_m;
 
   if (tid < 64) tab[tid] = kExp2Tab[tid];
 
@@ -128,31 +137,73 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
 
   // ---- K ranges ------------------------------------------------------------------
   const int nks = (VAR & 128) ? ksteps(n_rows) : ksteps(block_kmax(J, n_rows));
-  const int wc = J * 4 + w;                                 // this wave's 64 columns
-  const int col_hi = J * kNB + (w + 1) * kWC;
-  int nks_w = wc < n_wc ? ksteps(col_hi <= n_rows ? col_hi : n_rows) : 0;
-  if constexpr (VAR & 129) nks_w = wc < n_wc ? nks : 0;
+  // this wave's tiles: columns 256J + 16(4t + w) .. +15.  T1 = real tiles, kend[t] = the
+  // K-step where tile t retires (R tile: past its last column's diagonal; tiles holding
+  // mean columns: all rows).  kend is non-decreasing in t.
+  int T1 = 0;
+  int kend[4];
+#pragma unroll
+  for (int tt = 0; tt < 4; ++tt) {
+    const int c0 = J * kNB + 16 * (4 * tt + w);
+    const bool real = c0 < n_cols;
+    if (real) T1 = tt + 1;
+    const int hi = c0 + 16;
+    int ke = (hi <= n_rows) ? ksteps(hi) : ksteps(n_rows);
+    if constexpr (VAR & 129) ke = nks;
+    kend[tt] = real ? (ke < nks ? ke : nks) : 0;
+  }
   long long boff = 0;                                       // fragments of blocks < J
   for (int jj = 0; jj < J; ++jj) boff += (long long)ksteps(block_kmax(jj, n_rows)) * kFragStep;
   const double* __restrict__ Bw = Bf + boff + w * 1024 + lane * 2;
+  // last K-step this wave multiplies (kend is non-decreasing over the real tiles; no
+  // runtime indexing of kend[], which would put it in scratch)
+  const int kmaxw = max(max(kend[0], kend[1]), max(kend[2], kend[3]));
+  const int ks_last = (kmaxw > 0 ? kmaxw : 1) - 1;
 
-  // Branch-free generation (rows past n_rows are clamped, then zeroed) so the scalar row
-  // loads batch and the fp64 work can interleave with the MFMAs of the same K-step.
+  // Training rows of a K-step are staged through an LDS ring (RX) one step ahead with
+  // vector loads, so generation reads them as LDS broadcasts: no scalar loads whose
+  // lgkmcnt(0) waits would serialise with the A-fragment reads.
   const int last_row = n_rows - 1;
+  auto load_rows = [&](int ks, double (&rr)[RPT]) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int idx = tid + 256 * k;
+      double v = 0.0;
+      if (idx < NRV) {
+        const int r = idx / RW, f = idx - (idx / RW) * RW;
+        int i = ks * kBK + r;
+        i = i < last_row ? i : last_row;
+        if (f < DI) v = Xs[(long long)i * DI + f];
+        else if (f == DI) v = Xsq[i];
+        else v = Xl[(long long)i * DI + (f - DI - 1)];
+      }
+      rr[k] = v;
+    }
+  };
+  auto store_rows = [&](int buf, const double (&rr)[RPT]) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int idx = tid + 256 * k;
+      if (idx < NRV) (&RX[buf][0][0])[idx] = rr[k];
+    }
+  };
+  // Branch-free generation (rows past n_rows are zeroed after the fact).
   auto gen = [&](int ks, double (&v)[4]) {
+    const int rb = ks & 1;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int i = ks * kBK + w + 4 * s;                  // wave-uniform training row
-      const int ic = i < last_row ? i : last_row;
+      const int r = w + 4 * s;
+      const int i = ks * kBK + r;                          // wave-uniform training row
+      const double* row = &RX[rb][r][0];
       double x;
       if constexpr (VAR & 4) {
         x = -(asq + 0.5 * i);
 #pragma unroll
         for (int j = 0; j < DI; ++j) x = fma(a2[j], 0.25 * j, x);
       } else {
-        x = -(asq + Xsq[ic]);
+        x = -(asq + row[DI]);
 #pragma unroll
-        for (int j = 0; j < DI; ++j) x = fma(a2[j], Xs[(long long)ic * DI + j], x);
+        for (int j = 0; j < DI; ++j) x = fma(a2[j], row[j], x);
       }
       double val;
       if constexpr (VAR & 2) val = fma(x, 1e-3, 1.0);
@@ -160,28 +211,28 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
       if constexpr (DYN) {
         double l = ubias;
 #pragma unroll
-        for (int j = 0; j < DI; ++j) l = fma(u[j], Xl[(long long)ic * DI + j], l);
+        for (int j = 0; j < DI; ++j) l = fma(u[j], row[DI + 1 + j], l);
         val += l;
       }
       v[s] = i < n_rows ? val : 0.0;
     }
   };
-  // B prefetch: unconditional (clamped to the wave's last K-step) so no branch sits
-  // between the loads and the registers they fill.
-  const int ks_last = nks_w > 0 ? nks_w - 1 : 0;
-  auto loadB = [&](int ks, double (&bb)[16]) {
+  // B fragments: one register set, refilled sub-step by sub-step for the next K-step right
+  // after the MFMAs that consumed it (so the prefetch needs no second set of registers).
+  // The address is clamped to the wave's last K-step so no branch guards the loads.
+  auto loadB_part = [&](int ks, int kk, double (&bb)[16]) {
     if constexpr (VAR & 32) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) bb[q] = bb[q] * 0.999 + 1e-3 * (ks & 1);
+      for (int q = 0; q < 4; ++q) bb[kk * 4 + q] = bb[kk * 4 + q] * 0.999 + 1e-3 * (ks & 1);
       return;
     }
-    const double* src = Bw + (long long)(ks < ks_last ? ks : ks_last) * kFragStep;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const double2 x = *reinterpret_cast<const double2*>(src + q * 128);
-      bb[2 * q] = x.x;
-      bb[2 * q + 1] = x.y;
-    }
+    const double* src = Bw + (long long)(ks < ks_last ? ks : ks_last) * kFragStep + kk * 256;
+    const double2 x0 = *reinterpret_cast<const double2*>(src);
+    const double2 x1 = *reinterpret_cast<const double2*>(src + 128);
+    bb[kk * 4 + 0] = x0.x;
+    bb[kk * 4 + 1] = x0.y;
+    bb[kk * 4 + 2] = x1.x;
+    bb[kk * 4 + 3] = x1.y;
   };
   auto store = [&](int buf, const double (&v)[4]) {
 #pragma unroll
@@ -195,7 +246,18 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
 
-  auto mfma_step = [&](int buf, const double (&bc)[16]) {
+  // One K-step with tiles [T0, T1) active: generate K*(ks+1) and stage rows(ks+2), then per
+  // sub-step kk: A fragments from LDS, MFMAs, refill B(ks+1) for kk.  (Generating for
+  // ks+1 = nks is harmless: clamped rows, stored to a buffer never read again.)
+  auto full_step = [&](auto t0c, auto t1c, int ks, double (&bb)[16]) {
+    constexpr int T0 = decltype(t0c)::value, T1c = decltype(t1c)::value;
+    const int buf = ks & 1;
+    double v[4];
+    double rr[RPT];
+    if constexpr (!(VAR & 16)) {
+      load_rows(ks + 2, rr);
+      gen(ks + 1, v);
+    }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       double af[4];
@@ -207,57 +269,84 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bc[kk * 4 + nt], acc[mt][nt], 0, 0, 0);
+        for (int nt = T0; nt < T1c; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bb[kk * 4 + nt], acc[mt][nt], 0, 0, 0);
+      loadB_part(ks + 1, kk, bb);
     }
-  };
-  // one K-step with MFMAs: prefetch B(ks+1) into bn, generate K*(ks+1), MFMA on bc
-  // (the generation for ks+1 = nks is harmless: clamped rows, stored to a buffer that is
-  // never read again)
-  auto full_step = [&](int ks, const double (&bc)[16], double (&bn)[16]) {
-    double v[4];
-    loadB(ks + 1, bn);
-    if constexpr (!(VAR & 16)) gen(ks + 1, v);
-    mfma_step(ks & 1, bc);
-    if constexpr (!(VAR & 16)) store((ks + 1) & 1, v);
+    if constexpr (!(VAR & 16)) {
+      store(buf ^ 1, v);
+      store_rows(buf, rr);
+    }
     if constexpr (!(VAR & 8)) __syncthreads();
   };
 
-  double b0[16], b1[16];
+  double bb[16];
   if constexpr (VAR & 32) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) { b0[q] = 1e-3 * q + lane; b1[q] = 2e-3 * q; }
+    for (int q = 0; q < 16; ++q) bb[q] = 1e-3 * q + lane;
   }
-  __syncthreads();                                           // table ready
+  {
+    double rr[RPT];
+    load_rows(0, rr);
+    store_rows(0, rr);
+    load_rows(1, rr);
+    store_rows(1, rr);
+  }
+  __syncthreads();                                           // table + rows of steps 0, 1
   {
     double v[4];
     gen(0, v);
     store(0, v);
-    loadB(0, b0);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) loadB_part(0, kk, bb);
   }
   __syncthreads();
 
-  // Phase 1: K-steps this wave multiplies (ping-pong B registers, no copies).
   int ks = 0;
-  for (; ks + 1 < nks_w; ks += 2) {
-    full_step(ks, b0, b1);
-    full_step(ks + 1, b1, b0);
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  // K-steps [ks, e) with tiles [T0, T1) active
+  auto run_phase = [&](auto t0c, auto t1c, int e) {
+    for (; ks < e; ++ks) full_step(t0c, t1c, ks, bb);
+  };
+  switch (T1) {
+    case 4:
+      run_phase(I0{}, I4{}, kend[0]);
+      run_phase(I1{}, I4{}, kend[1]);
+      run_phase(I2{}, I4{}, kend[2]);
+      run_phase(I3{}, I4{}, kend[3]);
+      break;
+    case 3:
+      run_phase(I0{}, I3{}, kend[0]);
+      run_phase(I1{}, I3{}, kend[1]);
+      run_phase(I2{}, I3{}, kend[2]);
+      break;
+    case 2:
+      run_phase(I0{}, I2{}, kend[0]);
+      run_phase(I1{}, I2{}, kend[1]);
+      break;
+    case 1:
+      run_phase(I0{}, I1{}, kend[0]);
+      break;
+    default:
+      break;
   }
-  if (ks < nks_w) {
-    full_step(ks, b0, b1);
-    ++ks;
-  }
-  // Phase 2: the rest of the block's K range (other waves' columns): generate only.
+  // the rest of the block's K range (other waves' tiles): generate only
   for (; ks < nks; ++ks) {
     double v[4];
+    double rr[RPT];
+    load_rows(ks + 2, rr);
     gen(ks + 1, v);
     store((ks + 1) & 1, v);
+    store_rows(ks & 1, rr);
     __syncthreads();
   }
 
   // ---- epilogue --------------------------------------------------------------------
   // C/D layout of v_mfma_f64_16x16x4_f64: lane l, reg r -> row (l>>4) + 4r, col l&15.
-  const int colw = J * kNB + w * kWC;
   const bool has_r = J * kNB < n_rows;
   if (has_r) {
     double qs[4][4];
@@ -269,7 +358,7 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           const double x = acc[mt][nt][r];
-          if (colw + nt * 16 + li < n_rows) s = fma(x, x, s);
+          if (J * kNB + 16 * (4 * nt + w) + li < n_rows) s = fma(x, x, s);
         }
         s += __shfl_xor(s, 1);
         s += __shfl_xor(s, 2);
@@ -284,10 +373,10 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
         for (int r = 0; r < 4; ++r) qred[w][mt * 16 + lk + 4 * r] = qs[mt][r];
     }
   }
-  if (colw + kWC > n_rows) {                                  // mean columns
+  if ((J + 1) * kNB > n_rows) {                               // mean columns
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const int jm = colw + nt * 16 + li - n_rows;
+      const int jm = J * kNB + 16 * (4 * nt + w) + li - n_rows;
       if (jm >= 0 && jm < n_m) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)

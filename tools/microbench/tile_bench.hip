@@ -60,11 +60,10 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   typedef void (*L)(const TileParams&, hipStream_t);
-  L fns[] = {launch_var<0>, launch_var<112>, launch_var<113>, launch_var<240>, launch_var<248>, launch_var<128>, launch_var<1>};
-  const char* names[] = {"VAR0 production", "VAR112 pure MFMA (skip)", "VAR113 pure MFMA (no skip)",
-                         "VAR240 pure MFMA full-K blocks", "VAR248 same, no barrier", "VAR128 production ops, full-K",
-                         "VAR1 no skip"};
-  const int NV = 7, ROUNDS = 7;
+  L fns[] = {launch_var<0>, launch_var<16>, launch_var<2>, launch_var<4>, launch_var<8>};
+  const char* names[] = {"VAR0 production", "VAR16 no gen/no A store", "VAR2 cheap exp", "VAR4 no row reads",
+                         "VAR8 no barrier"};
+  const int NV = 5, ROUNDS = 7;
   std::vector<std::vector<float>> t(NV);
   for (int v = 0; v < NV; ++v) fns[v](p, s);
   CK(hipDeviceSynchronize());
@@ -78,9 +77,12 @@ int main(int argc, char** argv) {
       t[v].push_back(ms / 3);
     }
   // executed MFMA flops per launch (production schedule)
-  double rows = 0;
-  for (int wc = 0; wc < n_wc; ++wc) rows += ksteps(std::min((wc + 1) * kWC, N)) * kBK;
-  const double fl = 2.0 * kWC * rows * P;
+  double rows = 0;   // per 16-column tile: rows up to its diagonal (or all, for mean tiles)
+  for (int tc = 0; tc * 16 < N + D; ++tc) {
+    const int hi = tc * 16 + 16;
+    rows += (double)ksteps(hi <= N ? hi : N) * kBK;
+  }
+  const double fl = 2.0 * 16 * rows * P;
   // full-K schedule executed flops (VAR bit 7)
   const double fl_full = 2.0 * kWC * n_wc * (double)ksteps(N) * kBK * P;
   printf("(full-K schedule MFMA flops = %.3e per launch; production %.3e)\n", fl_full, fl);
