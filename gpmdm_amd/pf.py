@@ -30,7 +30,8 @@ from .model import GPMDM
 
 class GPMDM_PF:
     def __init__(self, gpmdm: GPMDM, markov_switching_model, num_particles: int, *,
-                 rng: str = "torch", seed=None, resample: str = "multinomial", process_group=None):
+                 rng: str = "torch", seed=None, resample: str = "multinomial", process_group=None,
+                 shard=None, exchange=None):
         self._gpmdm = gpmdm
         self._gpmdm.set_evaluation_mode()
         self._markov_switching_model = torch.as_tensor(markov_switching_model).type(self.dtype)
@@ -47,9 +48,12 @@ class GPMDM_PF:
             seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if rng == "philox" else 0
         self._seed = int(seed)
         self._group = process_group
+        self._exchange_fn = exchange
         if process_group is not None:
             import torch.distributed as dist
             self._world, self._rank = dist.get_world_size(process_group), dist.get_rank(process_group)
+        elif shard is not None:                 # (world, rank) with a caller-driven exchange
+            self._world, self._rank = int(shard[0]), int(shard[1])
         else:
             self._world, self._rank = 1, 0
         lib = _lib.load()
@@ -149,11 +153,29 @@ class GPMDM_PF:
     def _exchange(self, s):
         if self._world == 1:
             return
-        import torch.distributed as dist
         lib = _lib.load()
         _lib.check(lib.gpmdm_pf_pack(self._h, self._send.data_ptr(), s), "pack")
-        dist.all_gather_into_tensor(self._recv, self._send, group=self._group)
+        if self._exchange_fn is not None:
+            self._exchange_fn(self._recv, self._send)
+        else:
+            from .distributed import allgather_rows
+            allgather_rows(self._recv, self._send, self._group)
         _lib.check(lib.gpmdm_pf_unpack(self._h, self._recv.data_ptr(), s), "unpack")
+
+    # staged update for callers that drive the exchange themselves (tests, schedulers)
+    def _stage_propagate(self, z):
+        z = np.ascontiguousarray(torch.as_tensor(z, dtype=torch.float64).cpu().numpy().reshape(-1))
+        lib, h, s = _lib.load(), self._h, self._stream()
+        _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
+        _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), None, s), "propagate")
+        _lib.check(lib.gpmdm_pf_pack(h, self._send.data_ptr(), s), "pack")
+        return self._send
+
+    def _stage_resample(self):
+        lib, h, s = _lib.load(), self._h, self._stream()
+        _lib.check(lib.gpmdm_pf_unpack(h, self._recv.data_ptr(), s), "unpack")
+        _lib.check(lib.gpmdm_pf_resample(h, None, s), "resample")
+        self._readout = None
 
     def _read(self):
         if self._readout is None:

@@ -1,0 +1,67 @@
+"""World-size-2 gloo tests of the multi-rank host path (CPU only)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, P, W, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gpmdm_amd.distributed import allgather_rows, shard_range
+        from gpmdm_amd import replay
+        lo, hi = shard_range(P, world, rank)
+        send = torch.arange(lo * W, hi * W, dtype=torch.float64).reshape(hi - lo, W)
+        recv = torch.full((P, W), -1.0, dtype=torch.float64)
+        allgather_rows(recv, send)
+        ok_rows = bool(torch.equal(recv, torch.arange(P * W, dtype=torch.float64).reshape(P, W)))
+        # replicated draws: every rank seeds torch identically and draws the same streams
+        torch.manual_seed(123)
+        E = replay.switch_draws(P, 3)
+        g = [torch.empty_like(torch.tensor(E)) for _ in range(world)]
+        dist.all_gather(g, torch.tensor(E))
+        ok_draws = all(torch.equal(g[0], x) for x in g)
+        out_q.put((rank, ok_rows, ok_draws))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("P", [8, 7])   # even and uneven shards
+def test_allgather_rows_two_ranks(P):
+    world, W = 2, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, P, W, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, ok_rows, ok_draws in res:
+        assert ok_rows, f"rank {rank}: gathered rows wrong"
+        assert ok_draws, f"rank {rank}: replicated draws differ"
+
+
+def test_shard_ranges_cover():
+    from gpmdm_amd.distributed import shard_range
+    for P in (1, 7, 100, 100_001):
+        for world in (1, 2, 3, 8):
+            r = [shard_range(P, world, k) for k in range(world)]
+            assert r[0][0] == 0 and r[-1][1] == P
+            assert all(r[k][1] == r[k + 1][0] for k in range(world - 1))

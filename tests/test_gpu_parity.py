@@ -214,3 +214,33 @@ def test_systematic_offspring_bounds(m1, fx_config1):
         n = np.bincount(st["resample_idx"], minlength=5000)
         Pw = 5000 * st["w"]
         assert np.all(n >= np.floor(Pw - 1e-9)) and np.all(n <= np.ceil(Pw + 1e-9))
+
+
+def test_two_rank_sharding_on_one_gpu(m2):
+    """Two handles with shard=(2, r) on one GPU, exchange done in-process: the device-side
+    slicing (class segments of [lo, hi), obs range, pack/unpack) gives bitwise the same
+    filter as one rank.  P = 10001 (uneven shards, not a multiple of the tile sizes)."""
+    from gpmdm_amd import GPMDM_PF
+    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
+    P = 10_001
+    Y = m2.get_Y()
+    pfs = []
+    for shard in (None, (2, 0), (2, 1)):
+        torch.manual_seed(3)
+        pfs.append(GPMDM_PF(m2, T, P, rng="philox", seed=77, shard=shard))
+    ref, r0, r1 = pfs
+    for k in range(3):
+        z = Y[40 + k]
+        ref.update(z)
+        s0 = r0._stage_propagate(z)
+        s1 = r1._stage_propagate(z)
+        full = torch.cat([s0, s1], 0)
+        r0._recv.copy_(full)
+        r1._recv.copy_(full)
+        r0._stage_resample()
+        r1._stage_resample()
+        a, b, c = ref.export_state(), r0.export_state(), r1.export_state()
+        for key in ("states", "classes", "ll", "resample_idx"):
+            assert np.array_equal(a[key], b[key]) and np.array_equal(a[key], c[key]), (k, key)
+        assert np.array_equal(ref.class_probabilities().numpy(), r0.class_probabilities().numpy())
+        assert np.array_equal(ref.current_state_mean().numpy(), r1.current_state_mean().numpy())
