@@ -56,6 +56,27 @@ def _chol_inv_factor(K, what):
     return torch.triu(R)
 
 
+def read_reference_checkpoint(path):
+    """(config_dict, state_dict) of a checkpoint written by the reference's GPMDM.save
+    (gpmdm.py:1307-1346): ``torch.save({'state_dict', 'config_dict'})``.  The reference's
+    own loader (gpmdm.py:1368) calls ``torch.load`` with the default, which torch >= 2.6
+    refuses for these files (numpy arrays in config_dict).  Here only the safe loader runs:
+    ``weights_only=True`` with numpy's array reconstruction allow-listed; nothing else is
+    unpickled."""
+    safe = [np.ndarray, np.dtype]
+    try:
+        safe.append(np._core.multiarray._reconstruct)
+    except AttributeError:
+        safe.append(np.core.multiarray._reconstruct)
+    for name in dir(np.dtypes):
+        obj = getattr(np.dtypes, name)
+        if isinstance(obj, type) and name.endswith("DType"):
+            safe.append(obj)
+    with torch.serialization.safe_globals(safe):
+        save_dict = torch.load(path, weights_only=True, map_location="cpu")
+    return save_dict["config_dict"], save_dict["state_dict"]
+
+
 class GPMDM:
     """Gaussian Process Multi-Dynamical Model -- inference-side mirror of gpmdm.py:GPMDM.
 
@@ -348,10 +369,13 @@ class GPMDM:
         np.savez(file_path, **arrays)
 
     @classmethod
-    def load(cls, file_path, flg_print: bool = False, device=None) -> "GPMDM":
-        """Load a model saved by ``save`` (.npz), or a reference ``.pth`` through
-        ``torch.load(weights_only=True)`` with numpy arrays allow-listed."""
+    def load(cls, file_path, flg_print: bool = False, device=None, upload: bool = True) -> "GPMDM":
+        """Load a model saved by ``save`` (.npz), or a reference ``.pth`` (gpmdm.py:1349-1414)
+        through ``torch.load(weights_only=True)`` with numpy arrays allow-listed.
+        ``upload=False`` stops before the device precompute (host-side inspection)."""
         path = Path(file_path)
+        names = ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n", "x_log_lengthscales",
+                 "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff")
         if path.suffix == ".npz":
             f = np.load(path, allow_pickle=False)
             D, d, C, bs = (int(v) for v in f["cfg_int"])
@@ -363,36 +387,31 @@ class GPMDM:
                     x_sigma_n_init=float(np.exp(f["x_log_sigma_n"])),
                     x_lin_coeff_init=np.exp(f["x_log_lin_coeff"]),
                     sigma_n_num_X=float(f["cfg_num"][0]), sigma_n_num_Y=float(f["cfg_num"][1]), device=device)
+            for k in names:   # exact log-parameters (exp/log round trips can move an ulp)
+                setattr(m, k, torch.as_tensor(np.asarray(f[k], dtype=np.float64)))
             for c in range(C):
                 for k in range(int(f["n_seq"][c])):
                     m.add_data(f[f"obs_{c}_{k}"], c)
-            m.set_latents(f["X"])
-            return m
-        return cls._load_pth(path, device)
-
-    @classmethod
-    def _load_pth(cls, path, device):
-        """Reference checkpoint (gpmdm.py:1307-1414).  Only the safe loader is used."""
-        safe = [np.ndarray, np.dtype, np.core.multiarray._reconstruct] if hasattr(np, "core") else []
-        try:
-            safe.append(np.dtypes.Float32DType)
-            safe.append(np.dtypes.Float64DType)
-        except AttributeError:
-            pass
-        with torch.serialization.safe_globals(safe):
-            save_dict = torch.load(path, weights_only=True, map_location="cpu")
-        cfg, sd = save_dict["config_dict"], save_dict["state_dict"]
-        m = cls(D=cfg["D"], d=cfg["d"], n_classes=cfg["n_classes"], dyn_target=cfg["dyn_target"],
-                dyn_back_step=cfg["dyn_back_step"], y_lambdas_init=cfg["y_lambdas_init"],
-                y_lengthscales_init=cfg["y_lengthscales_init"], y_sigma_n_init=cfg["y_sigma_n_init"],
-                x_lambdas_init=cfg["x_lambdas_init"], x_lengthscales_init=cfg["x_lengthscales_init"],
-                x_sigma_n_init=cfg["x_sigma_n_init"], x_lin_coeff_init=cfg["x_lin_coeff_init"],
-                sigma_n_num_X=cfg["sigma_n_num_X"], sigma_n_num_Y=cfg["sigma_n_num_Y"], device=device)
-        m.class_aware_observations_list = cfg["class_aware_observations_list"]
-        for k in ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n", "x_log_lengthscales",
-                  "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff"):
-            setattr(m, k, sd[k].to(torch.float64).detach().clone())
-        m.set_latents(sd["X"])
+            X = f["X"]
+        else:
+            cfg, sd = read_reference_checkpoint(path)
+            m = cls(D=cfg["D"], d=cfg["d"], n_classes=cfg["n_classes"], dyn_target=cfg["dyn_target"],
+                    dyn_back_step=cfg["dyn_back_step"], y_lambdas_init=cfg["y_lambdas_init"],
+                    y_lengthscales_init=cfg["y_lengthscales_init"], y_sigma_n_init=cfg["y_sigma_n_init"],
+                    x_lambdas_init=cfg["x_lambdas_init"], x_lengthscales_init=cfg["x_lengthscales_init"],
+                    x_sigma_n_init=cfg["x_sigma_n_init"], x_lin_coeff_init=cfg["x_lin_coeff_init"],
+                    sigma_n_num_X=cfg["sigma_n_num_X"], sigma_n_num_Y=cfg["sigma_n_num_Y"], device=device)
+            m.class_aware_observations_list = [list(c) for c in cfg["class_aware_observations_list"]]
+            for k in names:
+                setattr(m, k, sd[k].to(torch.float64).detach().clone())
+            X = sd["X"]
+        if flg_print:
+            for k in names:
+                print(k, "\t", getattr(m, k))
+        if upload:
+            m.set_latents(X)
+        else:
+            m.X = torch.as_tensor(_to_np(X), dtype=torch.float64).clone()
         return m
 
     @classmethod

@@ -244,3 +244,49 @@ def test_two_rank_sharding_on_one_gpu(m2):
             assert np.array_equal(a[key], b[key]) and np.array_equal(a[key], c[key]), (k, key)
         assert np.array_equal(ref.class_probabilities().numpy(), r0.class_probabilities().numpy())
         assert np.array_equal(ref.current_state_mean().numpy(), r1.current_state_mean().numpy())
+
+
+@pytest.mark.parametrize("C,d,D,L", [(5, 8, 24, 41), (8, 16, 40, 23), (1, 1, 5, 70)])
+def test_config3_and_config5_shapes_vs_oracle(C, d, D, L):
+    """The d / C instantiations of the BASELINE configs 3 (d=8, C=5) and 5 (d=16, C=8) at
+    small N, plus the degenerate C=1, d=1: predictive maps and one full resynced filter
+    step against the oracle."""
+    from gpmdm_amd import GPMDM, GPMDM_PF, synthetic, replay
+    from oracle import gpmdm_oracle as O
+    data = synthetic.make_sequences(C=C, S=3, L=L, D=D, d=d, seed=9)
+    rng = np.random.RandomState(10)
+    N = C * 3 * L
+    X = rng.randn(N, d)
+    lp = dict(y_log_lengthscales=np.log(rng.uniform(1.0, 2.5, d)), y_log_lambdas=np.log(rng.uniform(0.5, 2, D)),
+              y_log_sigma_n=np.log(0.15), x_log_lengthscales=np.log(rng.uniform(1.0, 2.5, d)),
+              x_log_lambdas=np.log(rng.uniform(0.5, 2, d)), x_log_sigma_n=np.log(0.12),
+              x_log_lin_coeff=np.log(rng.uniform(0.2, 0.8, d + 1)))
+    m = GPMDM.from_arrays(X, data.sequences, **lp)
+    om = O.OracleModel(X=X, Y=np.concatenate([y for c in data.sequences for y in c]).astype(np.float64),
+                       seq_lengths=[[L] * 3] * C, **lp).precompute()
+    xs = X[rng.randint(0, N, 333)] + 0.1 * rng.randn(333, d)
+    mu, var = m.map_x_to_y(torch.tensor(xs))
+    omu, ovar = om.map_x_to_y(xs)
+    assert nrel(mu.numpy(), omu) < 1e-8 and nrel(var.numpy(), ovar) < 1e-7
+    for c in range(C):
+        mu, var = m.map_x_dynamics_for_class(torch.tensor(xs), c)
+        omu, ovar = om.map_x_dynamics_for_class(xs, c)
+        assert nrel(mu.numpy(), omu) < 1e-8 and nrel(var.numpy(), ovar) < 1e-6
+    P = 777
+    T = synthetic.markov_matrix(C)
+    pf = GPMDM_PF(m, torch.tensor(T), P, rng="torch")
+    st0 = pf.export_state()
+    E = rng.exponential(size=(P, C))
+    cls1 = O.switch_classes(st0["classes"], T, E)
+    nrm = rng.randn(P, d)
+    u = rng.rand(P)
+    z = data.sequences[0][0][3].astype(np.float64)
+    pf.update_with_draws(z, E, nrm, u)
+    r = O.step(om, T, st0["states"], st0["classes"], z, E, nrm, u)
+    st = pf.export_state()
+    assert np.array_equal(cls1, r.classes_switched)
+    assert np.array_equal(st["classes"], r.classes)
+    assert nrel(st["states"], r.states) < 1e-6
+    assert nrel(st["w"], r.w) < 1e-5
+    assert np.max(np.abs(pf.class_probabilities().numpy() - r.posterior)) < 1e-6
+    assert nrel(pf.current_state_mean().numpy(), r.mean) < 1e-6

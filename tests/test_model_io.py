@@ -1,0 +1,56 @@
+"""Model I/O on the host (no GPU): the reference checkpoint format and our .npz."""
+import numpy as np
+import torch
+
+from gpmdm_amd import GPMDM
+from gpmdm_amd.model import read_reference_checkpoint
+
+
+def _reference_style_checkpoint(path):
+    """A file in the exact layout GPMDM.save writes (gpmdm.py:1316-1345): state_dict of
+    log-parameters and X, config_dict holding numpy observation arrays."""
+    rng = np.random.RandomState(0)
+    obs = [[rng.randn(6, 4).astype(np.float32), rng.randn(5, 4).astype(np.float32)],
+           [rng.randn(7, 4).astype(np.float32)]]
+    sd = {"y_log_lengthscales": torch.log(torch.tensor([1.1, 0.9], dtype=torch.float64)),
+          "y_log_lambdas": torch.zeros(4, dtype=torch.float64),
+          "y_log_sigma_n": torch.log(torch.tensor(0.1, dtype=torch.float64)),
+          "x_log_lengthscales": torch.zeros(2, dtype=torch.float64),
+          "x_log_lambdas": torch.zeros(2, dtype=torch.float64),
+          "x_log_sigma_n": torch.log(torch.tensor(0.2, dtype=torch.float64)),
+          "x_log_lin_coeff": torch.zeros(3, dtype=torch.float64),
+          "X": torch.tensor(rng.randn(18, 2))}
+    cfg = {"class_aware_observations_list": obs, "dyn_target": "full", "dyn_back_step": 1, "D": 4, "d": 2,
+           "n_classes": 2, "sigma_n_num_X": 0.0, "sigma_n_num_Y": 0.0, "dtype": "torch.float64",
+           "device": "cpu", "y_lengthscales_init": [1.1, 0.9], "y_lambdas_init": [1.0] * 4,
+           "y_sigma_n_init": 0.1, "x_lengthscales_init": [1.0, 1.0], "x_lambdas_init": [1.0, 1.0],
+           "x_sigma_n_init": 0.2, "x_lin_coeff_init": [1.0, 1.0, 1.0]}
+    torch.save({"state_dict": sd, "config_dict": cfg}, path)
+    return sd, cfg
+
+
+def test_reference_pth_loads_with_weights_only(tmp_path):
+    p = tmp_path / "model.pth"
+    sd, cfg = _reference_style_checkpoint(p)
+    cfg2, sd2 = read_reference_checkpoint(p)
+    assert cfg2["D"] == 4 and len(cfg2["class_aware_observations_list"][0]) == 2
+    assert np.array_equal(cfg2["class_aware_observations_list"][1][0], cfg["class_aware_observations_list"][1][0])
+    m = GPMDM.load(p, upload=False)
+    assert torch.equal(m.X, sd["X"])
+    assert torch.equal(m.y_log_lengthscales, sd["y_log_lengthscales"])
+    Xin, Xout, starts = m.get_Xin_Xout_matrices()
+    assert Xin.shape == (15, 2) and starts == [0, 6, 11]
+    assert torch.equal(m.get_X_for_class(1), sd["X"][11:])
+
+
+def test_npz_round_trip(tmp_path):
+    p = tmp_path / "model.pth"
+    _reference_style_checkpoint(p)
+    m = GPMDM.load(p, upload=False)
+    q = tmp_path / "model.npz"
+    m.save(q)
+    m2 = GPMDM.load(q, upload=False)
+    assert torch.equal(m2.X, m.X)
+    for k in ("y_log_lengthscales", "y_log_lambdas", "x_log_lin_coeff", "x_log_sigma_n"):
+        assert torch.equal(getattr(m2, k), getattr(m, k)), k
+    assert np.array_equal(m2.get_Y(), m.get_Y())
