@@ -62,16 +62,16 @@ bool supported_d(int d) { return (d >= 1 && d <= 16) || d == 24 || d == 32; }
 // One GP's device image: scaled inputs (+ squared norms), raw inputs, and B = [R | M] in
 // MFMA-fragment order.
 //
-// Fragment layout (consumed by gp_tile.hip): column block J (256 columns) stores
-// ksteps(block_kmax(J)) K-steps; each K-step holds 4 waves x 1024 doubles, and inside a
+// Fragment layout (consumed by gp_tile.hip): column block J (nb = 64*nw columns) stores
+// ksteps(block_kmax(J)) K-steps; each K-step holds nw waves x 1024 doubles, and inside a
 // wave's 1024 doubles the value v = 2q + e of lane l sits at q*128 + 2l + e, where
 // v = kk*4 + nt is the B operand of MFMA sub-step kk (K=4) for column tile nt of wave w,
 // whose 16 columns are interleaved with the other waves' tiles:
-//   B[row = 16 ks + 4 kk + (l >> 4)][col = 256 J + 16 (4 nt + w) + (l & 15)].
+//   B[row = 16 ks + 4 kk + (l >> 4)][col = nb J + 16 (nw nt + w) + (l & 15)].
 // A lane's 16 values are therefore 8 x 16-byte loads, each wave-instruction reading one
 // contiguous 1 KiB.  Rows below the diagonal of R are never stored (triangular skip).
 struct GpImage {
-  int n_rows = 0, n_m = 0, n_j = 0, n_wc = 0;
+  int n_rows = 0, n_m = 0, n_j = 0, n_wc = 0, nw = 4;
   double* Xs = nullptr;   // n_rows x d, inputs / lengthscales
   double* Xsq = nullptr;  // n_rows
   double* Xl = nullptr;   // n_rows x d, raw inputs (dynamics)
@@ -95,15 +95,17 @@ struct GpImage {
     s.n_wc = n_wc;
     return s;
   }
-  int n_parts() const { return (int)cdiv(n_rows, kNB); }   // column blocks holding R columns
+  int n_parts() const { return (int)cdiv(n_rows, 64 * nw); }   // column blocks holding R columns
 };
 
 int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const double* ls,
-                bool keep_raw, const double* R, const double* M) {
+                bool keep_raw, const double* R, const double* M, int nw) {
+  const int nb = 64 * nw, fs = nw * 1024;
+  g.nw = nw;
   g.n_rows = n_rows;
   g.n_m = n_m;
   g.n_wc = (int)cdiv(n_rows + n_m, kWC);
-  g.n_j = (int)cdiv(g.n_wc, 4);
+  g.n_j = (int)cdiv(n_rows + n_m, nb);
   std::vector<double> xs((size_t)n_rows * d), xsq(n_rows, 0.0);
   for (long long i = 0; i < n_rows; ++i) {
     double s = 0.0;
@@ -123,7 +125,7 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
     HIPCHK(hipMemcpy(g.Xl, X, (size_t)n_rows * d * sizeof(double), hipMemcpyHostToDevice));
   }
   long long total = 0;
-  for (int J = 0; J < g.n_j; ++J) total += (long long)ksteps(block_kmax(J, n_rows)) * kFragStep;
+  for (int J = 0; J < g.n_j; ++J) total += (long long)ksteps(block_kmax(J, n_rows, nb)) * fs;
   TRY(dalloc(&g.Bf, (size_t)total));
   auto val = [&](long long row, long long col) -> double {
     if (row >= n_rows) return 0.0;
@@ -134,16 +136,16 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
   long long off = 0;
   std::vector<double> buf;
   for (int J = 0; J < g.n_j; ++J) {
-    const int nks = ksteps(block_kmax(J, n_rows));
-    buf.assign((size_t)nks * kFragStep, 0.0);
+    const int nks = ksteps(block_kmax(J, n_rows, nb));
+    buf.assign((size_t)nks * fs, 0.0);
     for (int ks = 0; ks < nks; ++ks)
-      for (int w = 0; w < 4; ++w) {
-        double* dst = buf.data() + ((size_t)ks * 4 + w) * 1024;
+      for (int w = 0; w < nw; ++w) {
+        double* dst = buf.data() + ((size_t)ks * nw + w) * 1024;
         for (int l = 0; l < 64; ++l)
           for (int v = 0; v < 16; ++v) {
             const int kk = v >> 2, nt = v & 3;
             const long long row = (long long)ks * kBK + kk * 4 + (l >> 4);
-            const long long col = (long long)J * kNB + 16 * (4 * nt + w) + (l & 15);
+            const long long col = (long long)J * nb + 16 * (nw * nt + w) + (l & 15);
             dst[(v >> 1) * 128 + 2 * l + (v & 1)] = val(row, col);
           }
       }
@@ -276,8 +278,10 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
   m->x_ls.assign(desc->x_lengthscales, desc->x_lengthscales + d);
   m->x_lin_c2.assign(desc->x_lin_coeff2, desc->x_lin_coeff2 + d + 1);
   m->x_il2.assign(desc->x_inv_lambda2, desc->x_inv_lambda2 + d);
+  const int nw = desc->tile_waves == 0 ? kDefaultNW : desc->tile_waves;
+  if (nw != 4 && nw != 8) { delete m; return fail(GPMDM_E_INVALID, "tile_waves must be 0, 4 or 8"); }
   int rc = build_image(m->obs, (int)m->N, d, m->D, desc->X, desc->y_lengthscales, false,
-                       desc->obs_R, desc->obs_beta);
+                       desc->obs_R, desc->obs_beta, nw);
   if (rc) { delete m; return rc; }
   m->dyn.resize(m->C);
   for (int c = 0; c < m->C; ++c) {
@@ -286,7 +290,7 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
       return fail(GPMDM_E_INVALID, "class " + std::to_string(c) + " has no dynamics rows");
     }
     rc = build_image(m->dyn[c], (int)desc->Nc[c], d, d, desc->Xin[c], desc->x_lengthscales, true,
-                     desc->dyn_R[c], desc->dyn_alpha[c]);
+                     desc->dyn_R[c], desc->dyn_alpha[c], nw);
     if (rc) { delete m; return rc; }
   }
   rc = dalloc(&m->y_il2_dev, m->D);
@@ -328,6 +332,7 @@ int gpmdm_predict_obs(gpmdm_model_t m, const double* Xs, int64_t n, double* mu, 
   TileParams tp{};
   tp.seg[0] = m->obs.seg();
   tp.n_seg = 1;
+  tp.nw = m->obs.nw;
   tp.tiles_ub = (int)cdiv(n, kPT);
   tp.n_j_max = m->obs.n_j;
   tp.seg_pos_begin = m->tab + 0;
@@ -373,6 +378,7 @@ int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, doubl
   TileParams tp{};
   tp.seg[0] = g.seg();
   tp.n_seg = 1;
+  tp.nw = g.nw;
   tp.tiles_ub = (int)cdiv(n, kPT);
   tp.n_j_max = g.n_j;
   tp.seg_pos_begin = m->tab + 0;
@@ -639,6 +645,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
         njm = std::max(njm, m->dyn[c0 + k].n_j);
       }
       tp.n_seg = ns;
+      tp.nw = m->dyn[c0].nw;
       tp.tiles_ub = (int)(cdiv(nl, kPT) + ns);
       tp.n_j_max = njm;
       tp.seg_pos_begin = pf->seg_begin() + c0;
@@ -684,6 +691,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     TileParams tp{};
     tp.seg[0] = m->obs.seg();
     tp.n_seg = 1;
+    tp.nw = m->obs.nw;
     tp.tiles_ub = (int)cdiv(nl, kPT);
     tp.n_j_max = m->obs.n_j;
     tp.seg_pos_begin = pf->obs_tab + 0;

@@ -10,16 +10,15 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------------
 // Fused GP tile geometry (see gp_tile.hip and DESIGN.md §3).
-//   one workgroup = 4 waves = 64 particles x 256 columns of V = K* . B, where K*
+//   one workgroup = NW waves = 64 particles x 64*NW columns of V = K* . B, where K*
 //   (particles x training rows) is generated on the fly and B = [R | M] is the extended
-//   weight matrix stored in MFMA-fragment order (each wave owns 64 columns).
+//   weight matrix stored in MFMA-fragment order (each wave owns 4 tiles of 16 columns).
 // ---------------------------------------------------------------------------------
 constexpr int kPT = 64;           // particles per tile (MFMA M)
 constexpr int kWC = 64;           // columns per wave
-constexpr int kNB = 256;          // columns per workgroup (4 waves)
 constexpr int kBK = 16;           // training rows per K-step (4 x K=4 MFMA sub-steps)
 constexpr int kLDA = kPT + 16;    // LDS row stride (doubles): rows k, k+1 land 32 banks apart
-constexpr int kFragStep = 4 * 1024;  // doubles of B fragments per (block, K-step): 4 waves x 64 lanes x 16
+constexpr int kDefaultNW = 4;     // waves per workgroup unless the model asks otherwise
 constexpr int kMaxSeg = 8;        // segments (classes) per launch
 constexpr int kMaxD = 32;         // latent dimension limit
 
@@ -39,7 +38,7 @@ struct TileParams {
   int n_seg;
   int tiles_ub;                   // grid = n_j_max * tiles_ub workgroups
   int n_j_max;
-  int pad_;
+  int nw;                         // waves per workgroup (4 or 8): fragment layout of B
   const int* seg_pos_begin;       // [n_seg]   first position (device)
   const int* seg_pos_end;         // [n_seg]
   const int* seg_out_base;        // [n_seg]   output row of the first position
@@ -55,8 +54,9 @@ struct TileParams {
 };
 
 // Column-block geometry shared by the host (fragment layout) and the kernel.
-__host__ __device__ inline int block_kmax(int J, int n_rows) {   // rows column block J needs
-  const int hi = (J + 1) * kNB;
+// A block of nw waves spans nb = 64*nw columns; its K range ends at min(n_rows, (J+1)*nb).
+__host__ __device__ inline int block_kmax(int J, int n_rows, int nb) {
+  const int hi = (J + 1) * nb;
   return hi < n_rows ? hi : n_rows;
 }
 __host__ __device__ inline int ksteps(int kmax) { return (kmax + kBK - 1) / kBK; }

@@ -77,15 +77,19 @@ __device__ __forceinline__ double exp_table(double x, const double* tab) {
 //   bit 5: ablation -- no B loads (B operands stay in registers)
 //   bit 6: ablation -- no LDS A-fragment reads (A operands from registers)
 //   bit 7: ablation -- every block runs the full K range (no triangular schedule)
-template <int DI, bool DYN, int VAR = 0>
-__global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
+template <int DI, bool DYN, int VAR = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
+  constexpr int NT = 64 * NW;                                // threads
+  constexpr int NB = 64 * NW;                                // columns per block
+  constexpr int FS = NW * 1024;                              // fragment doubles per K-step
+  constexpr int GV = kBK / NW;                               // K* values per thread per K-step
   constexpr int RW = DYN ? 2 * DI + 1 : DI + 1;             // row record: Xs[DI], |Xs|^2, (Xl[DI])
   constexpr int NRV = kBK * RW;                              // row values per K-step
-  constexpr int RPT = (NRV + 255) / 256;                     // row values per thread
+  constexpr int RPT = (NRV + NT - 1) / NT;                   // row values per thread
   __shared__ double As[2][kBK][kLDA];
   __shared__ double RX[2][kBK][RW];
   __shared__ double tab[64];
-  __shared__ double qred[4][kPT];
+  __shared__ double qred[NW][kPT];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -136,15 +140,15 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
   if constexpr (DYN) ubias = prm.lin_c2[DI];
 
   // ---- K ranges ------------------------------------------------------------------
-  const int nks = (VAR & 128) ? ksteps(n_rows) : ksteps(block_kmax(J, n_rows));
-  // this wave's tiles: columns 256J + 16(4t + w) .. +15.  T1 = real tiles, kend[t] = the
+  const int nks = (VAR & 128) ? ksteps(n_rows) : ksteps(block_kmax(J, n_rows, NB));
+  // this wave's tiles: columns NB*J + 16(NW t + w) .. +15.  T1 = real tiles, kend[t] = the
   // K-step where tile t retires (R tile: past its last column's diagonal; tiles holding
   // mean columns: all rows).  kend is non-decreasing in t.
   int T1 = 0;
   int kend[4];
 #pragma unroll
   for (int tt = 0; tt < 4; ++tt) {
-    const int c0 = J * kNB + 16 * (4 * tt + w);
+    const int c0 = J * NB + 16 * (NW * tt + w);
     const bool real = c0 < n_cols;
     if (real) T1 = tt + 1;
     const int hi = c0 + 16;
@@ -153,7 +157,7 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
     kend[tt] = real ? (ke < nks ? ke : nks) : 0;
   }
   long long boff = 0;                                       // fragments of blocks < J
-  for (int jj = 0; jj < J; ++jj) boff += (long long)ksteps(block_kmax(jj, n_rows)) * kFragStep;
+  for (int jj = 0; jj < J; ++jj) boff += (long long)ksteps(block_kmax(jj, n_rows, NB)) * FS;
   const double* __restrict__ Bw = Bf + boff + w * 1024 + lane * 2;
   // last K-step this wave multiplies (kend is non-decreasing over the real tiles; no
   // runtime indexing of kend[], which would put it in scratch)
@@ -167,7 +171,7 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
   auto load_rows = [&](int ks, double (&rr)[RPT]) {
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-      const int idx = tid + 256 * k;
+      const int idx = tid + NT * k;
       double v = 0.0;
       if (idx < NRV) {
         const int r = idx / RW, f = idx - (idx / RW) * RW;
@@ -183,16 +187,16 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
   auto store_rows = [&](int buf, const double (&rr)[RPT]) {
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-      const int idx = tid + 256 * k;
+      const int idx = tid + NT * k;
       if (idx < NRV) (&RX[buf][0][0])[idx] = rr[k];
     }
   };
   // Branch-free generation (rows past n_rows are zeroed after the fact).
-  auto gen = [&](int ks, double (&v)[4]) {
+  auto gen = [&](int ks, double (&v)[GV]) {
     const int rb = ks & 1;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int r = w + 4 * s;
+    for (int s = 0; s < GV; ++s) {
+      const int r = w + NW * s;
       const int i = ks * kBK + r;                          // wave-uniform training row
       const double* row = &RX[rb][r][0];
       double x;
@@ -226,7 +230,7 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
       for (int q = 0; q < 4; ++q) bb[kk * 4 + q] = bb[kk * 4 + q] * 0.999 + 1e-3 * (ks & 1);
       return;
     }
-    const double* src = Bw + (long long)(ks < ks_last ? ks : ks_last) * kFragStep + kk * 256;
+    const double* src = Bw + (long long)(ks < ks_last ? ks : ks_last) * FS + kk * 256;
     const double2 x0 = *reinterpret_cast<const double2*>(src);
     const double2 x1 = *reinterpret_cast<const double2*>(src + 128);
     bb[kk * 4 + 0] = x0.x;
@@ -234,9 +238,9 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
     bb[kk * 4 + 2] = x1.x;
     bb[kk * 4 + 3] = x1.y;
   };
-  auto store = [&](int buf, const double (&v)[4]) {
+  auto store = [&](int buf, const double (&v)[GV]) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) As[buf][w + 4 * s][m] = v[s];
+    for (int s = 0; s < GV; ++s) As[buf][w + NW * s][m] = v[s];
   };
 
   const int li = lane & 15, lk = lane >> 4;
@@ -252,7 +256,7 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
   auto full_step = [&](auto t0c, auto t1c, int ks, double (&bb)[16]) {
     constexpr int T0 = decltype(t0c)::value, T1c = decltype(t1c)::value;
     const int buf = ks & 1;
-    double v[4];
+    double v[GV];
     double rr[RPT];
     if constexpr (!(VAR & 16)) {
       load_rows(ks + 2, rr);
@@ -294,7 +298,7 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
   }
   __syncthreads();                                           // table + rows of steps 0, 1
   {
-    double v[4];
+    double v[GV];
     gen(0, v);
     store(0, v);
 #pragma unroll
@@ -336,7 +340,7 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
   }
   // the rest of the block's K range (other waves' tiles): generate only
   for (; ks < nks; ++ks) {
-    double v[4];
+    double v[GV];
     double rr[RPT];
     load_rows(ks + 2, rr);
     gen(ks + 1, v);
@@ -347,7 +351,7 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
 
   // ---- epilogue --------------------------------------------------------------------
   // C/D layout of v_mfma_f64_16x16x4_f64: lane l, reg r -> row (l>>4) + 4r, col l&15.
-  const bool has_r = J * kNB < n_rows;
+  const bool has_r = J * NB < n_rows;
   if (has_r) {
     double qs[4][4];
 #pragma unroll
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           const double x = acc[mt][nt][r];
-          if (J * kNB + 16 * (4 * nt + w) + li < n_rows) s = fma(x, x, s);
+          if (J * NB + 16 * (NW * nt + w) + li < n_rows) s = fma(x, x, s);
         }
         s += __shfl_xor(s, 1);
         s += __shfl_xor(s, 2);
@@ -373,10 +377,10 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
         for (int r = 0; r < 4; ++r) qred[w][mt * 16 + lk + 4 * r] = qs[mt][r];
     }
   }
-  if ((J + 1) * kNB > n_rows) {                               // mean columns
+  if ((J + 1) * NB > n_rows) {                                // mean columns
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const int jm = J * kNB + 16 * (4 * nt + w) + li - n_rows;
+      const int jm = J * NB + 16 * (NW * nt + w) + li - n_rows;
       if (jm >= 0 && jm < n_m) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)
@@ -392,8 +396,12 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
     __syncthreads();
     if (tid < kPT) {
       const int p = pos0 + tid;
-      if (p < pos_end)
-        prm.qpart[(long long)J * prm.ld_q + out_base + p] = (qred[0][tid] + qred[1][tid]) + (qred[2][tid] + qred[3][tid]);
+      if (p < pos_end) {
+        double q = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) q += qred[ww][tid];
+        prm.qpart[(long long)J * prm.ld_q + out_base + p] = q;
+      }
     }
   }
 }
@@ -401,10 +409,17 @@ __global__ __launch_bounds__(256, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TilePa
 template <int DI>
 static void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
   const dim3 grid((unsigned)(p.n_j_max * p.tiles_ub));
-  if (dyn)
-    hipLaunchKernelGGL((k_gp_tile<DI, true>), grid, dim3(256), 0, stream, p);
-  else
-    hipLaunchKernelGGL((k_gp_tile<DI, false>), grid, dim3(256), 0, stream, p);
+  if (p.nw == 8) {
+    if (dyn)
+      hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 8>), grid, dim3(512), 0, stream, p);
+    else
+      hipLaunchKernelGGL((k_gp_tile<DI, false, 0, 8>), grid, dim3(512), 0, stream, p);
+  } else {
+    if (dyn)
+      hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4>), grid, dim3(256), 0, stream, p);
+    else
+      hipLaunchKernelGGL((k_gp_tile<DI, false, 0, 4>), grid, dim3(256), 0, stream, p);
+  }
 }
 
 void launch_gp_tile(const TileParams& p, int d, bool dyn, hipStream_t stream) {

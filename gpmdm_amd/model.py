@@ -14,6 +14,7 @@ dense ``(C+1) x Nx x Nx`` masks of the reference are never formed.
 from __future__ import annotations
 
 import ctypes
+import os
 from pathlib import Path
 
 import numpy as np
@@ -118,6 +119,8 @@ class GPMDM:
         self.X = None
         self._handle = None
         self._precompute_device = None   # None: CPU for N <= 4096, the model GPU above
+        # waves per GP-tile workgroup (4 or 8; 0 = library default); env override for A/B runs
+        self.tile_waves = int(os.environ.get("GPMDM_TILE_WAVES", "0"))
 
     # ---- reference API: data registry (gpmdm.py:239-309) -------------------------
     def set_evaluation_mode(self):
@@ -256,6 +259,7 @@ class GPMDM:
         Ry, beta = obs
         desc = _lib.ModelDesc()
         desc.N, desc.D, desc.d, desc.C = self.X.shape[0], D, d, C
+        desc.tile_waves = self.tile_waves
         desc.X = arr(self.X.numpy())
         desc.obs_R = arr(Ry)
         desc.obs_beta = arr(beta)

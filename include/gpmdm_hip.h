@@ -60,7 +60,7 @@ typedef struct gpmdm_model_desc {
   int32_t D;                     /* observation dimension */
   int32_t d;                     /* latent dimension (<= 32) */
   int32_t C;                     /* classes */
-  int32_t reserved;
+  int32_t tile_waves;            /* waves per GP-tile workgroup: 0 = default (4), 4 or 8 */
   const double* X;               /* N x d latents (particle initialisation is host-side) */
   const double* obs_R;           /* N x N */
   const double* obs_beta;        /* N x D */

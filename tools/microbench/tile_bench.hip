@@ -1,6 +1,6 @@
-// A/B timing of k_gp_tile variants (template VAR bits, see gp_tile.hip) on the
-// config-2 observation GP shape: N=2000, D=62, d=3, P=100k.  Variants run interleaved in
-// one process (cdna_hip_programming.md §5.4 rule 24); prints the median per variant.
+// A/B timing of k_gp_tile variants on the config-2 observation GP shape (N=2000, D=62,
+// d=3, P=100k): template VAR bits (see gp_tile.hip) and NW (waves per workgroup).
+// Variants run interleaved in one process (cdna_hip_programming.md §5.4 rule 24).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/microbench/tile_bench.hip -o tools/microbench/tile_bench
 #include <algorithm>
 #include <cstdio>
@@ -14,9 +14,9 @@ using namespace gpmdm;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
-template <int VAR>
+template <int VAR, int NW>
 void launch_var(const TileParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((k_gp_tile<3, false, VAR>), dim3(p.n_j_max * p.tiles_ub), dim3(256), 0, s, p);
+  hipLaunchKernelGGL((k_gp_tile<3, false, VAR, NW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, p);
 }
 
 int main(int argc, char** argv) {
@@ -24,72 +24,77 @@ int main(int argc, char** argv) {
   const int P = argc > 1 ? atoi(argv[1]) : 100000;
   std::mt19937_64 rng(1);
   std::normal_distribution<double> nd(0.0, 1.0);
-  const int n_wc = (N + D + kWC - 1) / kWC, n_j = (n_wc + 3) / 4;
-  long long total = 0;
-  for (int J = 0; J < n_j; ++J) total += (long long)ksteps(block_kmax(J, N)) * kFragStep;
-  std::vector<double> hB(total), hXs(N * d), hXsq(N), hX((size_t)P * d);
-  for (auto& v : hB) v = 0.01 * nd(rng);
+  std::vector<double> hXs(N * d), hXsq(N), hX((size_t)P * d);
   for (int i = 0; i < N; ++i) {
     double s = 0;
     for (int j = 0; j < d; ++j) { hXs[i * d + j] = 2.0 * nd(rng); s += hXs[i * d + j] * hXs[i * d + j]; }
     hXsq[i] = s;
   }
   for (auto& v : hX) v = 2.0 * nd(rng);
-  double *B, *Xs, *Xsq, *X, *q, *mu;
+  double *Xs, *Xsq, *X, *q, *mu;
   int* tab;
-  CK(hipMalloc(&B, total * 8)); CK(hipMalloc(&Xs, N * d * 8)); CK(hipMalloc(&Xsq, N * 8));
-  CK(hipMalloc(&X, (size_t)P * d * 8)); CK(hipMalloc(&q, (size_t)P * n_j * 8)); CK(hipMalloc(&mu, (size_t)P * D * 8));
+  CK(hipMalloc(&Xs, N * d * 8)); CK(hipMalloc(&Xsq, N * 8));
+  CK(hipMalloc(&X, (size_t)P * d * 8)); CK(hipMalloc(&q, (size_t)P * 16 * 8)); CK(hipMalloc(&mu, (size_t)P * D * 8));
   CK(hipMalloc(&tab, 64));
-  CK(hipMemcpy(B, hB.data(), total * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(Xs, hXs.data(), N * d * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(Xsq, hXsq.data(), N * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(X, hX.data(), (size_t)P * d * 8, hipMemcpyHostToDevice));
   const int ntiles = (P + kPT - 1) / kPT;
   int ht[5] = {0, P, 0, 0, ntiles};
   CK(hipMemcpy(tab, ht, sizeof(ht), hipMemcpyHostToDevice));
-  TileParams p{};
-  p.seg[0].Xs = Xs; p.seg[0].Xsq = Xsq; p.seg[0].Bf = B;
-  p.seg[0].n_rows = N; p.seg[0].n_m = D; p.seg[0].n_j = n_j; p.seg[0].n_wc = n_wc;
-  p.n_seg = 1; p.tiles_ub = ntiles; p.n_j_max = n_j;
-  p.seg_pos_begin = tab; p.seg_pos_end = tab + 1; p.seg_out_base = tab + 2; p.seg_tile_start = tab + 3;
-  p.X = X;
-  for (int j = 0; j < d; ++j) p.ls[j] = 1.0;
-  p.qpart = q; p.ld_q = P; p.mu = mu; p.ld_mu = D;
+  TileParams pp[2];
+  for (int v = 0; v < 2; ++v) {
+    const int nw = v == 0 ? 4 : 8, nb = 64 * nw;
+    const int n_j = (N + D + nb - 1) / nb;
+    long long total = 0;
+    for (int J = 0; J < n_j; ++J) total += (long long)ksteps(block_kmax(J, N, nb)) * nw * 1024;
+    std::vector<double> hB(total);
+    for (auto& x : hB) x = 0.01 * nd(rng);
+    double* B;
+    CK(hipMalloc(&B, total * 8));
+    CK(hipMemcpy(B, hB.data(), total * 8, hipMemcpyHostToDevice));
+    TileParams& p = pp[v];
+    p = TileParams{};
+    p.seg[0].Xs = Xs; p.seg[0].Xsq = Xsq; p.seg[0].Bf = B;
+    p.seg[0].n_rows = N; p.seg[0].n_m = D; p.seg[0].n_j = n_j; p.seg[0].n_wc = (N + D + 63) / 64;
+    p.n_seg = 1; p.tiles_ub = ntiles; p.n_j_max = n_j; p.nw = nw;
+    p.seg_pos_begin = tab; p.seg_pos_end = tab + 1; p.seg_out_base = tab + 2; p.seg_tile_start = tab + 3;
+    p.X = X;
+    for (int j = 0; j < d; ++j) p.ls[j] = 1.0;
+    p.qpart = q; p.ld_q = P; p.mu = mu; p.ld_mu = D;
+  }
 
   hipStream_t s = nullptr;
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   typedef void (*L)(const TileParams&, hipStream_t);
-  L fns[] = {launch_var<0>, launch_var<16>, launch_var<2>, launch_var<4>, launch_var<8>};
-  const char* names[] = {"VAR0 production", "VAR16 no gen/no A store", "VAR2 cheap exp", "VAR4 no row reads",
-                         "VAR8 no barrier"};
-  const int NV = 5, ROUNDS = 7;
+  struct V { L fn; int pi; const char* name; };
+  V vars[] = {{launch_var<0, 4>, 0, "NW4 production"}, {launch_var<0, 8>, 1, "NW8 production"},
+              {launch_var<16, 4>, 0, "NW4 no gen"}, {launch_var<16, 8>, 1, "NW8 no gen"},
+              {launch_var<8, 8>, 1, "NW8 no barrier (ablation)"}};
+  const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
   std::vector<std::vector<float>> t(NV);
-  for (int v = 0; v < NV; ++v) fns[v](p, s);
+  for (int v = 0; v < NV; ++v) vars[v].fn(pp[vars[v].pi], s);
   CK(hipDeviceSynchronize());
   for (int r = 0; r < ROUNDS; ++r)
     for (int v = 0; v < NV; ++v) {
       CK(hipEventRecord(e0, s));
-      for (int k = 0; k < 3; ++k) fns[v](p, s);
+      for (int k = 0; k < 3; ++k) vars[v].fn(pp[vars[v].pi], s);
       CK(hipEventRecord(e1, s));
       CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       t[v].push_back(ms / 3);
     }
-  // executed MFMA flops per launch (production schedule)
   double rows = 0;   // per 16-column tile: rows up to its diagonal (or all, for mean tiles)
   for (int tc = 0; tc * 16 < N + D; ++tc) {
     const int hi = tc * 16 + 16;
     rows += (double)ksteps(hi <= N ? hi : N) * kBK;
   }
   const double fl = 2.0 * 16 * rows * P;
-  // full-K schedule executed flops (VAR bit 7)
-  const double fl_full = 2.0 * kWC * n_wc * (double)ksteps(N) * kBK * P;
-  printf("(full-K schedule MFMA flops = %.3e per launch; production %.3e)\n", fl_full, fl);
   for (int v = 0; v < NV; ++v) {
     std::sort(t[v].begin(), t[v].end());
-    printf("%-30s median %.3f ms  min %.3f ms   (%.1f TF/s on the production schedule's MFMA flops)\n",
-           names[v], t[v][ROUNDS / 2], t[v][0], fl / t[v][ROUNDS / 2] / 1e9);
+    printf("%-30s median %.3f ms  min %.3f ms   (%.1f TF/s executed MFMA)\n", vars[v].name, t[v][ROUNDS / 2],
+           t[v][0], fl / t[v][ROUNDS / 2] / 1e9);
   }
   return 0;
 }
