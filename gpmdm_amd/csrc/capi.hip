@@ -59,6 +59,8 @@ inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
 
 bool supported_d(int d) { return (d >= 1 && d <= 16) || d == 24 || d == 32; }
 
+constexpr double kLog2eX64 = 92.33248261689366;   // 64 / ln 2, as in gp_tile.hip
+
 // One GP's device image: scaled inputs (+ squared norms), raw inputs, and B = [R | M] in
 // MFMA-fragment order.
 //
@@ -70,24 +72,29 @@ bool supported_d(int d) { return (d >= 1 && d <= 16) || d == 24 || d == 32; }
 //   B[row = 16 ks + 4 kk + (l >> 4)][col = nb J + 16 (nw nt + w) + (l & 15)].
 // A lane's 16 values are therefore 8 x 16-byte loads, each wave-instruction reading one
 // contiguous 1 KiB.  Rows below the diagonal of R are never stored (triangular skip).
+//
+// Dynamics images also carry H = (X~ C^2)^T B ((d+1) x cols, X~ = [Xin, 1], C^2 the linear
+// kernel's coefficients, gpmdm.py:493-506): the linear kernel's share of K* B, seeded into
+// the accumulators by MFMA.  Hf[((J kh_n + kh) nw + w) 256 + 4 l + nt] =
+//   H[row = 4 kh + (l >> 4)][col = nb J + 16 (nw nt + w) + (l & 15)].
 struct GpImage {
   int n_rows = 0, n_m = 0, n_j = 0, n_wc = 0, nw = 4;
   double* Xs = nullptr;   // n_rows x d, inputs / lengthscales
   double* Xsq = nullptr;  // n_rows
-  double* Xl = nullptr;   // n_rows x d, raw inputs (dynamics)
+  double* Hf = nullptr;   // dynamics only
   double* Bf = nullptr;
 
   void release() {
     dfree(Xs);
     dfree(Xsq);
-    dfree(Xl);
+    dfree(Hf);
     dfree(Bf);
   }
   SegDesc seg() const {
     SegDesc s{};
     s.Xs = Xs;
     s.Xsq = Xsq;
-    s.Xl = Xl;
+    s.Hf = Hf;
     s.Bf = Bf;
     s.n_rows = n_rows;
     s.n_m = n_m;
@@ -99,7 +106,7 @@ struct GpImage {
 };
 
 int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const double* ls,
-                bool keep_raw, const double* R, const double* M, int nw) {
+                const double* lin_c2, const double* R, const double* M, int nw) {
   const int nb = 64 * nw, fs = nw * 1024;
   g.nw = nw;
   g.n_rows = n_rows;
@@ -114,16 +121,12 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
       xs[i * d + j] = v;
       s += v * v;
     }
-    xsq[i] = s;
+    xsq[i] = s * kLog2eX64;   // pre-scaled for the kernel's exp2 (gp_tile.hip)
   }
   TRY(dalloc(&g.Xs, xs.size()));
   HIPCHK(hipMemcpy(g.Xs, xs.data(), xs.size() * sizeof(double), hipMemcpyHostToDevice));
   TRY(dalloc(&g.Xsq, xsq.size()));
   HIPCHK(hipMemcpy(g.Xsq, xsq.data(), xsq.size() * sizeof(double), hipMemcpyHostToDevice));
-  if (keep_raw) {
-    TRY(dalloc(&g.Xl, (size_t)n_rows * d));
-    HIPCHK(hipMemcpy(g.Xl, X, (size_t)n_rows * d * sizeof(double), hipMemcpyHostToDevice));
-  }
   long long total = 0;
   for (int J = 0; J < g.n_j; ++J) total += (long long)ksteps(block_kmax(J, n_rows, nb)) * fs;
   TRY(dalloc(&g.Bf, (size_t)total));
@@ -133,6 +136,31 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
     const long long j = col - n_rows;
     return j < n_m ? M[row * n_m + j] : 0.0;
   };
+  if (lin_c2) {
+    const long long n_cols = (long long)n_rows + n_m;
+    std::vector<double> H((size_t)(d + 1) * n_cols, 0.0);
+    for (long long i = 0; i < n_rows; ++i)
+      for (long long col = 0; col < n_cols; ++col) {
+        const double b = val(i, col);
+        if (b == 0.0) continue;
+        for (int k = 0; k < d; ++k) H[k * n_cols + col] += lin_c2[k] * X[i * d + k] * b;
+        H[(size_t)d * n_cols + col] += lin_c2[d] * b;
+      }
+    const int kh_n = lin_substeps(d);
+    std::vector<double> hf((size_t)g.n_j * kh_n * nw * 256, 0.0);
+    for (int J = 0; J < g.n_j; ++J)
+      for (int kh = 0; kh < kh_n; ++kh)
+        for (int w = 0; w < nw; ++w)
+          for (int l = 0; l < 64; ++l)
+            for (int nt = 0; nt < 4; ++nt) {
+              const int row = 4 * kh + (l >> 4);
+              const long long col = (long long)J * nb + 16 * (nw * nt + w) + (l & 15);
+              if (row <= d && col < n_cols)
+                hf[(((size_t)J * kh_n + kh) * nw + w) * 256 + 4 * l + nt] = H[row * n_cols + col];
+            }
+    TRY(dalloc(&g.Hf, hf.size()));
+    HIPCHK(hipMemcpy(g.Hf, hf.data(), hf.size() * sizeof(double), hipMemcpyHostToDevice));
+  }
   long long off = 0;
   std::vector<double> buf;
   for (int J = 0; J < g.n_j; ++J) {
@@ -280,7 +308,7 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
   m->x_il2.assign(desc->x_inv_lambda2, desc->x_inv_lambda2 + d);
   const int nw = desc->tile_waves == 0 ? kDefaultNW : desc->tile_waves;
   if (nw != 4 && nw != 8) { delete m; return fail(GPMDM_E_INVALID, "tile_waves must be 0, 4 or 8"); }
-  int rc = build_image(m->obs, (int)m->N, d, m->D, desc->X, desc->y_lengthscales, false,
+  int rc = build_image(m->obs, (int)m->N, d, m->D, desc->X, desc->y_lengthscales, nullptr,
                        desc->obs_R, desc->obs_beta, nw);
   if (rc) { delete m; return rc; }
   m->dyn.resize(m->C);
@@ -289,7 +317,8 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
       delete m;
       return fail(GPMDM_E_INVALID, "class " + std::to_string(c) + " has no dynamics rows");
     }
-    rc = build_image(m->dyn[c], (int)desc->Nc[c], d, d, desc->Xin[c], desc->x_lengthscales, true,
+    rc = build_image(m->dyn[c], (int)desc->Nc[c], d, d, desc->Xin[c], desc->x_lengthscales,
+                     m->x_lin_c2.data(),
                      desc->dyn_R[c], desc->dyn_alpha[c], nw);
     if (rc) { delete m; return rc; }
   }
@@ -314,8 +343,6 @@ int gpmdm_model_destroy(gpmdm_model_t m) {
 static void fill_tile_common(TileParams& tp, const gpmdm_model* m, bool dyn) {
   const int d = m->d;
   for (int j = 0; j < d; ++j) tp.ls[j] = dyn ? m->x_ls[j] : m->y_ls[j];
-  if (dyn)
-    for (int j = 0; j <= d; ++j) tp.lin_c2[j] = m->x_lin_c2[j];
 }
 
 int gpmdm_predict_obs(gpmdm_model_t m, const double* Xs, int64_t n, double* mu, double* var, void* stream) {

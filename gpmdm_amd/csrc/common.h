@@ -24,8 +24,8 @@ constexpr int kMaxD = 32;         // latent dimension limit
 
 struct SegDesc {                  // one GP: the observation GP, or the class-c dynamics GP
   const double* Xs;               // n_rows x d : training inputs / lengthscales
-  const double* Xsq;              // n_rows     : |Xs_i|^2
-  const double* Xl;               // n_rows x d : raw training inputs (linear kernel; dyn only)
+  const double* Xsq;              // n_rows     : |Xs_i|^2 * 64/ln2 (pre-scaled for exp2)
+  const double* Hf;               // dyn only: H = (Xin C^2)^T B, (d+1) x cols, fragment order
   const double* Bf;               // B = [triu(R) | M] in fragment order (see capi.hip)
   int n_rows;                     // training rows = R columns
   int n_m;                        // mean columns (D or d)
@@ -46,7 +46,6 @@ struct TileParams {
   const int* perm;                // position -> particle row (nullptr: identity)
   const double* X;                // particle rows, n x d
   double ls[kMaxD];               // RBF lengthscales
-  double lin_c2[kMaxD + 1];       // linear-kernel c^2, bias last (dyn only)
   double* qpart;                  // [J][ld_q]: partial sums of (R^T k)^2 per column block
   long long ld_q;
   double* mu;                     // [out][ld_mu] mean columns
@@ -60,6 +59,8 @@ __host__ __device__ inline int block_kmax(int J, int n_rows, int nb) {
   return hi < n_rows ? hi : n_rows;
 }
 __host__ __device__ inline int ksteps(int kmax) { return (kmax + kBK - 1) / kBK; }
+// Dynamics linear kernel: K=4 MFMA sub-steps covering the d+1 rows of H.
+__host__ __device__ inline int lin_substeps(int d) { return (d + 1 + 3) / 4; }
 
 void launch_gp_tile(const TileParams& p, int d, bool dyn, hipStream_t stream);
 

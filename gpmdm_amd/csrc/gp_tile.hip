@@ -5,6 +5,11 @@
 //                   mean = Ky*^T beta, var-quadratic form = Ky*^T Ky^-1 Ky*
 //   dynamics GP     (gpmdm.py:1061-1065) Kx* = RBF + linear kernel over the class-c rows,
 //                   mean = Kx*^T alpha_c, quadratic form = Kx*^T A_c Kx*
+// The linear kernel (gpmdm.py:493-506) is rank d+1: k_lin(p, i) = x~_p^T C^2 x~_i with
+// x~ = [x, 1], so its contribution to V = K* B is x~_p^T H with H = (X~ C^2)^T B, a
+// (d+1)-row matrix precomputed on the host.  It is added to the accumulators after the K
+// loop by ceil((d+1)/4) extra MFMA sub-steps, and the K loop generates only the RBF part
+// (the same code as the observation GP).
 // With K^-1 = R R^T (R = U^-1 from the reference's own Cholesky recipe, gpmdm.py:1286-1289)
 // the quadratic form is |R^T k|^2.  R is upper triangular, so column block J only needs
 // training rows [0, (J+1)*256), and each wave stops at its own 64 columns: about half the
@@ -51,21 +56,25 @@ __constant__ double kExp2Tab[64] = {
     1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951
 };
 
-// exp(x) for x <= ~0 (kernel values): x = 64 n / ln2-reduced, 5-term polynomial on
-// |r| <= ln2/128, 2^(j/64) table, ldexp.  <= 2 ulp; underflows to 0 like exp().
-__device__ __forceinline__ double exp_table(double x, const double* tab) {
-  x = fmax(x, -746.0);
-  const double n = __builtin_rint(x * 92.33248261689366);          // 64 / ln 2
-  double r = fma(n, -0.010830424696905538, x);                    // ln2/64, Cody-Waite hi
-  r = fma(n, 6.563929801064195e-13, r);                           //          ... lo
-  double p = fma(r, 1.0 / 120.0, 1.0 / 24.0);
-  p = fma(p, r, 1.0 / 6.0);
-  p = fma(p, r, 0.5);
-  p = fma(p, r, 1.0);
-  p *= r;                                                          // e^r - 1
+// The kernel value is exp(x), x = -(|a|^2 + |b|^2) + 2 a.b (expansion form of
+// gpmdm.py:508-515).  Every term arrives pre-multiplied by 64/ln2 (particle side in the
+// kernel prologue, |b|^2 on the host), so the fma chain yields t = 64 x / ln2 directly and
+// exp(x) = 2^(t/64): n = rint(t), f = t - n (exact, Sterbenz), 2^(f/64) - 1 by a degree-5
+// polynomial in f (|f| <= 1/2, truncation < 2^-55), table 2^(j/64), ldexp.  No clamp is
+// needed: v_cvt_i32_f64 saturates and ldexp underflows to 0 exactly like exp().
+constexpr double kLog2eX64 = 92.33248261689366;   // 64 / ln 2 (host and device)
+
+__device__ __forceinline__ double exp2_64(double t, const double* tab) {
+  const double n = __builtin_rint(t);
+  const double f = t - n;
+  double p = fma(f, 1.2417843701716925e-12, 5.732851688640402e-10);
+  p = fma(p, f, 2.1173137155464776e-07);
+  p = fma(p, f, 5.86490495505617e-05);
+  p = fma(p, f, 0.010830424696249145);
+  p *= f;                                                          // 2^(f/64) - 1
   const int ni = (int)n;
-  const double t = tab[ni & 63];
-  return ldexp(fma(t, p, t), ni >> 6);
+  const double tj = tab[ni & 63];
+  return ldexp(fma(tj, p, tj), ni >> 6);
 }
 
 // VAR: experiment switches for tools/microbench/tile_bench.hip (production uses 0).
@@ -83,7 +92,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 8 ? 2 : 1)) void k_gp_tile(const Ti
   constexpr int NB = 64 * NW;                                // columns per block
   constexpr int FS = NW * 1024;                              // fragment doubles per K-step
   constexpr int GV = kBK / NW;                               // K* values per thread per K-step
-  constexpr int RW = DYN ? 2 * DI + 1 : DI + 1;             // row record: Xs[DI], |Xs|^2, (Xl[DI])
+  constexpr int RW = DI + 1;                                 // row record: Xs[DI], |Xs|^2
   constexpr int NRV = kBK * RW;                              // row values per K-step
   constexpr int RPT = (NRV + NT - 1) / NT;                   // row values per thread
   __shared__ double As[2][kBK][kLDA];
@@ -108,7 +117,6 @@ __global__ __launch_bounds__(64 * NW, (DI <= 8 ? 2 : 1)) void k_gp_tile(const Ti
   if (J >= n_j) return;
   const double* __restrict__ Xs = prm.seg[c].Xs;
   const double* __restrict__ Xsq = prm.seg[c].Xsq;
-  const double* __restrict__ Xl = prm.seg[c].Xl;
   const double* __restrict__ Bf = prm.seg[c].Bf;
   const int n_rows = prm.seg[c].n_rows;
   const int n_m = prm.seg[c].n_m;
@@ -126,18 +134,16 @@ __global__ __launch_bounds__(64 * NW, (DI <= 8 ? 2 : 1)) void k_gp_tile(const Ti
   int pos = pos0 + m;
   if (pos >= pos_end) pos = pos0;                          // clamp (results unused)
   const int prow = prm.perm ? prm.perm[pos] : pos;
-  double a2[DI];                                           // 2 x / l
-  double u[DYN ? DI : 1];
-  double asq = 0.0, ubias = 0.0;
+  double a2[DI];                                           // 2 (x / l) (64 / ln 2)
+  double asq = 0.0;
 #pragma unroll
   for (int j = 0; j < DI; ++j) {
     const double x = prm.X[(long long)prow * DI + j];
     const double xs = x / prm.ls[j];
     asq = fma(xs, xs, asq);
-    a2[j] = 2.0 * xs;
-    if constexpr (DYN) u[j] = prm.lin_c2[j] * x;
+    a2[j] = (2.0 * kLog2eX64) * xs;
   }
-  if constexpr (DYN) ubias = prm.lin_c2[DI];
+  asq *= kLog2eX64;                                        // |x / l|^2 (64 / ln 2)
 
   // ---- K ranges ------------------------------------------------------------------
   const int nks = (VAR & 128) ? ksteps(n_rows) : ksteps(block_kmax(J, n_rows, NB));
@@ -177,9 +183,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 8 ? 2 : 1)) void k_gp_tile(const Ti
         const int r = idx / RW, f = idx - (idx / RW) * RW;
         int i = ks * kBK + r;
         i = i < last_row ? i : last_row;
-        if (f < DI) v = Xs[(long long)i * DI + f];
-        else if (f == DI) v = Xsq[i];
-        else v = Xl[(long long)i * DI + (f - DI - 1)];
+        v = f < DI ? Xs[(long long)i * DI + f] : Xsq[i];
       }
       rr[k] = v;
     }
@@ -211,13 +215,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 8 ? 2 : 1)) void k_gp_tile(const Ti
       }
       double val;
       if constexpr (VAR & 2) val = fma(x, 1e-3, 1.0);
-      else val = exp_table(x, tab);
-      if constexpr (DYN) {
-        double l = ubias;
-#pragma unroll
-        for (int j = 0; j < DI; ++j) l = fma(u[j], row[DI + 1 + j], l);
-        val += l;
-      }
+      else val = exp2_64(x, tab);
       v[s] = i < n_rows ? val : 0.0;
     }
   };
@@ -347,6 +345,34 @@ __global__ __launch_bounds__(64 * NW, (DI <= 8 ? 2 : 1)) void k_gp_tile(const Ti
     store((ks + 1) & 1, v);
     store_rows(ks & 1, rr);
     __syncthreads();
+  }
+
+  if constexpr (DYN) {
+    // Linear-kernel share: acc += X~ H for this block.  A fragment: lane l holds
+    // x~[particle mt*16 + (l&15)][4 kh + (l>>4)]; B fragment: Hf[J][kh][w][l][nt].
+    constexpr int KH = (DI + 1 + 3) / 4;
+    const double* __restrict__ Hw = prm.seg[c].Hf + ((long long)J * KH * NW + w) * 256 + lane * 4;
+    int prw[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      int pp = pos0 + mt * 16 + li;
+      if (pp >= pos_end) pp = pos0;
+      prw[mt] = prm.perm ? prm.perm[pp] : pp;
+    }
+#pragma unroll
+    for (int kh = 0; kh < KH; ++kh) {
+      const int k = 4 * kh + lk;
+      const double2 h0 = *reinterpret_cast<const double2*>(Hw + (long long)kh * NW * 256);
+      const double2 h1 = *reinterpret_cast<const double2*>(Hw + (long long)kh * NW * 256 + 2);
+      const double hb[4] = {h0.x, h0.y, h1.x, h1.y};
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const double xa = k < DI ? prm.X[(long long)prw[mt] * DI + (k < DI ? k : 0)] : (k == DI ? 1.0 : 0.0);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, hb[nt], acc[mt][nt], 0, 0, 0);
+      }
+    }
   }
 
   // ---- epilogue --------------------------------------------------------------------
