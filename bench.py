@@ -1,6 +1,6 @@
 """Benchmark: GPMDM particle-filter step on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config {2,3,4,5}]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Workload (BASELINE.json configs[1]): N=2000 training latents, D=62, d=3, C=2 classes,
@@ -8,6 +8,8 @@ P=100,000 particles per GPU (weak scaling: P_total = 100k x GPUs), synthetic mod
 observation stream.  One step = ``update(z)`` + ``class_probabilities()``
 + ``current_state_mean()``, the notebook's per-frame loop (test_gpmdm_pf.ipynb:197-201),
 with device-side Philox draws and the reference's multinomial resampling.
+``--config 3|4|5`` runs the other BASELINE.json configurations (per-GPU share of P for
+the 8-GPU ones); they are not the headline line.
 
 Prints ONE JSON line (rank 0) with the contract fields plus:
   roofline      dominant kernel (observation-GP tile kernel) vs the FP64 MFMA peak;
@@ -33,7 +35,15 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "particle-steps/sec (P×timesteps) + achieved HBM GB/s, N=2000 D=62 d=3"
 FP64_MFMA_PEAK_TFLOPS = 78.6          # MI355X spec (dense FP64 matrix); measured 77.1 (profiles/)
-WORKLOAD = dict(C=2, S=5, L=200, D=62, d=3, P_per_gpu=100_000)
+# per-GPU particles: configs 4 and 5 are quoted on 8 GPUs
+P_PER_GPU = {1: 100, 2: 100_000, 3: 100_000, 4: 125_000, 5: 125_000}
+WORKLOAD = None
+
+
+def workload(cfg):
+    from gpmdm_amd import synthetic
+    c = synthetic.CONFIGS[cfg]
+    return dict(cfg=cfg, C=c["C"], S=c["S"], L=c["L"], D=c["D"], d=c["d"], P_per_gpu=P_PER_GPU[cfg])
 
 
 def log(*a):
@@ -101,13 +111,14 @@ def cpu_baseline(data, budget_s=12.0):
     Y = np.concatenate([y for c in data.sequences for y in c]).astype(np.float64)
     X = PCA(n_components=w["d"]).fit_transform(Y)
     hp = synthetic.default_hyperparameters(w["D"], w["d"], 0.1)
+    N = Y.shape[0]
     m = O.OracleModel(X=X, Y=Y, seq_lengths=[[w["L"]] * w["S"]] * w["C"],
                       y_log_lengthscales=np.log(hp["y_lengthscales_init"]), y_log_lambdas=np.log(hp["y_lambdas_init"]),
                       y_log_sigma_n=np.log(0.1), x_log_lengthscales=np.log(hp["x_lengthscales_init"]),
                       x_log_lambdas=np.log(hp["x_lambdas_init"]), x_log_sigma_n=np.log(0.1),
                       x_log_lin_coeff=np.log(hp["x_lin_coeff_init"])).precompute()
     T = synthetic.markov_matrix(w["C"])
-    Ps = 2000
+    Ps = 2000 if N <= 2000 else 200
     rng = np.random.RandomState(0)
     parts = [rng.randint(0, m.X_for_class(c).shape[0], Ps // w["C"]) for c in range(w["C"])]
     s, c = O.init_particles(m, Ps, parts)
@@ -122,7 +133,7 @@ def cpu_baseline(data, budget_s=12.0):
             break
     del torch
     return {"value": Ps * steps / el, "unit": "particle-steps/s", "cores": int(cores), "kind": "port",
-            "sample": f"oracle (numpy fp64 restatement) N=2000 D=62 d=3 C=2, P={Ps} particles x {steps} steps "
+            "sample": f"oracle (numpy fp64 restatement) N={N} D={w['D']} d={w['d']} C={w['C']}, P={Ps} particles x {steps} steps "
                       f"in {el:.1f} s"}
 
 
@@ -132,7 +143,10 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 4, 5))
     args = ap.parse_args()
+    global WORKLOAD
+    WORKLOAD = workload(args.config)
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -155,7 +169,8 @@ def main():
     t_setup = time.perf_counter()
     model, data = build_model(device)
     P_total = WORKLOAD["P_per_gpu"] * world
-    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]], dtype=torch.float64)
+    from gpmdm_amd import synthetic
+    T = torch.from_numpy(synthetic.markov_matrix(WORKLOAD["C"]))
     torch.manual_seed(11)
     pf = GPMDM_PF(model, T, P_total, rng="philox", seed=11, process_group=group)
     zs = data.observation_stream(args.warmup + args.steps, seed=1)
@@ -209,13 +224,14 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (SURVEY §8(d) generator; random-phase sinusoid mocap surrogate, PCA latents)",
-        "config": {"workload": "configs[1]: N=2000 D=62 d=3 C=2, P=100k particles per GPU, philox draws, "
-                               "multinomial resampling",
+        "config": {"workload": f"configs[{WORKLOAD['cfg'] - 1}]: N={N} D={D} d={d} C={model.n_classes}, "
+                               f"P={P_local} particles per GPU, philox draws, multinomial resampling",
                    "N": N, "D": D, "d": d, "C": model.n_classes, "P_per_gpu": P_local, "P_total": P_total,
                    "parallelism": f"particles sharded over {world} GPU(s), one all-gather per step"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_MFMA_PEAK_TFLOPS, "traffic": pmc_traffic(),
-                     "kernel": "k_gp_tile<3,false> (observation GP)",
+                     "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
+                     "traffic": pmc_traffic() if WORKLOAD["cfg"] == 2 else None,
+                     "kernel": f"k_gp_tile<{d},false> (observation GP)",
                      "flops_per_particle_algorithmic": alg, "flops_per_particle_executed": executed,
                      "flops_per_particle_dense_form": dense,
                      "executed_tflops": executed * P_local / obs_launch_s / 1e12,

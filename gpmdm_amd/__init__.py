@@ -6,6 +6,7 @@ HIP kernels for gfx950 in ``libgpmdm_hip.so``.
 """
 from .model import GPMDM
 from .pf import GPMDM_PF
+from .bank import GPMDM_PF_Bank
 
-__all__ = ["GPMDM", "GPMDM_PF"]
+__all__ = ["GPMDM", "GPMDM_PF", "GPMDM_PF_Bank"]
 __version__ = "0.1.0"

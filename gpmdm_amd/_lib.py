@@ -41,6 +41,8 @@ _SIGS = {
     "gpmdm_predict_dyn": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "gpmdm_pf_create": (c_int, [c_void_p, _dp, c_int64, c_int, c_uint64, c_int, c_int, c_int, POINTER(c_void_p)]),
     "gpmdm_pf_destroy": (c_int, [c_void_p]),
+    "gpmdm_bank_create": (c_int, [c_void_p, _dp, c_int64, c_int64, c_uint64, c_int, POINTER(c_void_p)]),
+    "gpmdm_pf_shape": (c_int, [c_void_p, _i64p, _i64p]),
     "gpmdm_pf_init": (c_int, [c_void_p, _dp, _i64p]),
     "gpmdm_pf_switch": (c_int, [c_void_p, _dp, _i64p, c_void_p]),
     "gpmdm_pf_propagate": (c_int, [c_void_p, _dp, _dp, c_void_p]),
@@ -53,6 +55,8 @@ _SIGS = {
     "gpmdm_pf_export": (c_int, [c_void_p, _dp, _i64p, _dp, _dp, _dp, _i64p, c_void_p]),
     "gpmdm_pf_enable_timing": (c_int, [c_void_p, c_int]),
     "gpmdm_pf_stage_times": (c_int, [c_void_p, _dp, _i64p]),
+    "gpmdm_gp_factor": (c_int, [c_int, _dp, c_int64, c_int32, _dp, _dp, c_double, c_double, c_double,
+                                _dp, c_int64, _dp, _dp]),
     "gpmdm_last_error": (c_char_p, []),
     "gpmdm_version": (c_char_p, []),
 }

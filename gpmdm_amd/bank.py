@@ -1,0 +1,229 @@
+"""GPMDM_PF_Bank -- many independent particle filters sharing one GPMDM.
+
+The reference runs one ``GPMDM_PF`` per observation stream, one after another (the 39
+trials of ``test_gpmdm_pf.ipynb`` cell 4, each a fresh filter over the same model;
+SURVEY.md §8(f) row 3).  A bank runs F such filters as one device computation: the
+dynamics and observation GP tile kernels see all F x P particles at once (filling the
+GPU at the notebooks' P = 100), while normalisation, resampling and the read-outs run
+per filter.  Every filter keeps the reference's per-filter semantics
+(``gpmdm_pf.py:117-262``).
+
+Draws come from the device (Philox).  Filter f is keyed with ``seed + f``, so its
+trajectory is bit-identical to a single ``GPMDM_PF(..., rng='philox', seed=seed + f)``
+started from the same particles; the bank changes the schedule, not the numbers.
+
+With a ``process_group`` the filters are sharded over ranks (rank r owns filters
+``[r F / R, (r + 1) F / R)``, the particle-shard rule of ``gpmdm_pf_create``).  Filters
+are independent, so the step needs no collective at all; ``gather_readouts()`` is the
+only exchange and is optional.  ``shard=(world, rank)`` selects the same slice without a
+process group.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib, replay
+from .distributed import shard_range
+from .model import GPMDM
+
+
+class GPMDM_PF_Bank:
+    def __init__(self, gpmdm: GPMDM, markov_switching_model, num_filters: int, num_particles: int, *,
+                 seed=None, resample: str = "multinomial", process_group=None, shard=None):
+        self._gpmdm = gpmdm
+        self._gpmdm.set_evaluation_mode()
+        self._T = torch.as_tensor(markov_switching_model).type(torch.float64)
+        if self._gpmdm.n_classes != self._T.size(0):
+            raise ValueError("Number of classes in the GPMDM model and the Markov model do not match")
+        if resample not in ("multinomial", "systematic"):
+            raise ValueError("resample must be 'multinomial' or 'systematic'")
+        self._num_filters = int(num_filters)
+        self._num_particles = int(num_particles)
+        if self._num_filters < 1 or self._num_particles < 1:
+            raise ValueError("num_filters and num_particles must be positive")
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        self._seed = int(seed)
+        self._group = process_group
+        if process_group is not None:
+            import torch.distributed as dist
+            world, rank = dist.get_world_size(process_group), dist.get_rank(process_group)
+        elif shard is not None:                   # (world, rank) without a process group
+            world, rank = int(shard[0]), int(shard[1])
+        else:
+            world, rank = 1, 0
+        self._world, self._rank = world, rank
+        self._f_lo, self._f_hi = shard_range(self._num_filters, world, rank)
+        self._h = None
+        self._readout = None
+        if self.local_filters > 0:
+            T = np.ascontiguousarray(self._T.numpy(), dtype=np.float64)
+            h = ctypes.c_void_p()
+            _lib.check(_lib.load().gpmdm_bank_create(
+                gpmdm.handle, _lib.dptr(T), self.local_filters, self._num_particles,
+                ctypes.c_uint64((self._seed + self._f_lo) & (2 ** 64 - 1)),
+                _lib.GPMDM_RESAMPLE_MULTINOMIAL if resample == "multinomial" else _lib.GPMDM_RESAMPLE_SYSTEMATIC,
+                ctypes.byref(h)), "GPMDM_PF_Bank")
+            self._h = h
+            self._init_particles()
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None) is not None and self._h.value:
+                _lib.load().gpmdm_pf_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    # ---- state ----------------------------------------------------------------------
+    def _init_particles(self):
+        """gpmdm_pf.py:87-115 for every local filter.  Filter f's initial draws come from a
+        generator seeded with seed + f, so they do not depend on the rank count."""
+        C, P = self.num_classes, self._num_particles
+        g, r = divmod(P, C)
+        counts = [g + (1 if i < r else 0) for i in range(C)]
+        Xc = [self._gpmdm.get_X_for_class(c).numpy() for c in range(C)]
+        sizes = [x.shape[0] for x in Xc]
+        states, classes = [], []
+        for f in range(self._f_lo, self._f_hi):
+            gen = torch.Generator().manual_seed(self._seed + f)
+            idx = replay.init_draws(sizes, counts, generator=gen)
+            states.append(np.concatenate([Xc[c][idx[c]] for c in range(C)], 0))
+            classes.append(np.concatenate([np.full(counts[c], c, dtype=np.int64) for c in range(C)]))
+        self.load_state(np.stack(states), np.stack(classes))
+
+    def reset(self):
+        if self._h is not None:
+            self._init_particles()
+
+    def load_state(self, states, classes):
+        """states (F_local, P, d), classes (F_local, P)."""
+        Fl, P, d = self.local_filters, self._num_particles, self.latent_dim
+        states = np.ascontiguousarray(states, dtype=np.float64).reshape(Fl * P, d)
+        classes = np.ascontiguousarray(classes, dtype=np.int64).reshape(Fl * P)
+        _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "load_state")
+        self._readout = None
+
+    def export_state(self) -> dict:
+        Fl, P, d = self.local_filters, self._num_particles, self.latent_dim
+        n = Fl * P
+        out = dict(states=np.zeros((n, d)), classes=np.zeros(n, dtype=np.int64), ll=np.zeros(n),
+                   log_w=np.zeros(n), w=np.zeros(n), resample_idx=np.zeros(n, dtype=np.int64))
+        _lib.check(_lib.load().gpmdm_pf_export(
+            self._h, _lib.dptr(out["states"]), _lib.i64ptr(out["classes"]), _lib.dptr(out["ll"]),
+            _lib.dptr(out["log_w"]), _lib.dptr(out["w"]), _lib.i64ptr(out["resample_idx"]), self._stream()),
+            "export")
+        out["states"] = out["states"].reshape(Fl, P, d)
+        for k in ("classes", "ll", "log_w", "w", "resample_idx"):
+            out[k] = out[k].reshape(Fl, P)
+        return out
+
+    # ---- per-frame ------------------------------------------------------------------
+    def update(self, Z):
+        """One frame for every filter.  Z: (F, D) (all filters; each rank takes its rows)
+        or (F_local, D)."""
+        Z = np.asarray(torch.as_tensor(Z, dtype=torch.float64).cpu().numpy(), dtype=np.float64)
+        Z = Z.reshape(-1, self.observation_dim)
+        if Z.shape[0] == self._num_filters and self.local_filters != self._num_filters:
+            Z = Z[self._f_lo:self._f_hi]
+        if Z.shape[0] != self.local_filters:
+            raise ValueError(f"expected {self._num_filters} (or {self.local_filters} local) observations, "
+                             f"got {Z.shape[0]}")
+        self._readout = None
+        if self._h is None:
+            return
+        Z = np.ascontiguousarray(Z)
+        lib, h, s = _lib.load(), self._h, self._stream()
+        _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
+        _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(Z), None, s), "propagate")
+        _lib.check(lib.gpmdm_pf_resample(h, None, s), "resample")
+
+    step = update
+
+    def _read(self):
+        if self._readout is None:
+            Fl, C, d = self.local_filters, self.num_classes, self.latent_dim
+            post, mean, lik = np.zeros((Fl, C)), np.zeros((Fl, d)), np.zeros(Fl)
+            if self._h is not None:
+                _lib.check(_lib.load().gpmdm_pf_read(self._h, _lib.dptr(post), _lib.dptr(mean), _lib.dptr(lik),
+                                                     self._stream()), "read")
+            self._readout = (post, mean, lik)
+        return self._readout
+
+    def class_probabilities(self) -> torch.Tensor:
+        """(F_local, C): gpmdm_pf.py:224-248 per filter."""
+        return torch.tensor(self._read()[0], dtype=torch.float64)
+
+    def get_most_likely_class(self) -> torch.Tensor:
+        """(F_local,): gpmdm_pf.py:250-254 per filter (first maximum)."""
+        return torch.argmax(self.class_probabilities(), dim=1)
+
+    def current_state_mean(self) -> torch.Tensor:
+        """(F_local, d): gpmdm_pf.py:256-262 per filter."""
+        return torch.tensor(self._read()[1], dtype=torch.float64)
+
+    def log_likelihood(self) -> torch.Tensor:
+        """(F_local,): gpmdm_pf.py:215-222 per filter (a sum of exponentials, as there)."""
+        return torch.tensor(self._read()[2], dtype=torch.float64)
+
+    def gather_readouts(self) -> dict:
+        """All filters' read-outs on every rank (one all-gather of F x (C + d + 1))."""
+        post, mean, lik = self._read()
+        rows = np.concatenate([post, mean, lik[:, None]], 1)
+        if self._group is None:
+            full = rows
+        else:
+            import torch.distributed as dist
+            from .distributed import allgather_rows
+            dev = self.device if dist.get_backend(self._group) != "gloo" else torch.device("cpu")
+            send = torch.as_tensor(rows, dtype=torch.float64, device=dev)
+            recv = torch.empty((self._num_filters, rows.shape[1]), dtype=torch.float64, device=dev)
+            allgather_rows(recv, send, self._group)
+            full = recv.cpu().numpy()
+        C, d = self.num_classes, self.latent_dim
+        return dict(class_probabilities=torch.tensor(full[:, :C]),
+                    current_state_mean=torch.tensor(full[:, C:C + d]),
+                    log_likelihood=torch.tensor(full[:, C + d]))
+
+    # ---- properties -----------------------------------------------------------------
+    @property
+    def num_filters(self):
+        return self._num_filters
+
+    @property
+    def local_filters(self):
+        return self._f_hi - self._f_lo
+
+    @property
+    def filter_range(self):
+        return self._f_lo, self._f_hi
+
+    @property
+    def num_particles(self):
+        return self._num_particles
+
+    @property
+    def latent_dim(self):
+        return self._gpmdm.d
+
+    @property
+    def observation_dim(self):
+        return self._gpmdm.D
+
+    @property
+    def num_classes(self):
+        return self._gpmdm.n_classes
+
+    @property
+    def dtype(self):
+        return self._gpmdm.dtype
+
+    @property
+    def device(self):
+        return self._gpmdm.device

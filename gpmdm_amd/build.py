@@ -20,8 +20,8 @@ ROOT = PKG.parent
 CSRC = PKG / "csrc"
 OBJ = PKG / "_build"
 LIB = PKG / "libgpmdm_hip.so"
-SOURCES = ["gp_tile.hip", "pf_kernels.hip", "capi.hip"]
-HEADERS = [CSRC / "common.h", CSRC / "pf_kernels.h", ROOT / "include" / "gpmdm_hip.h"]
+SOURCES = ["gp_tile.hip", "pf_kernels.hip", "capi.hip", "precompute.hip"]
+HEADERS = [CSRC / "common.h", CSRC / "pf_kernels.h", CSRC / "status.h", ROOT / "include" / "gpmdm_hip.h"]
 ARCH = "gfx950"
 
 
@@ -60,7 +60,8 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         list(ex.map(run, jobs))
     objs = [str(OBJ / (s + ".o")) for s in SOURCES]
     if force or jobs or not LIB.exists():
-        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *objs])
+        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *objs,
+             "-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"])
     return LIB
 
 

@@ -10,52 +10,20 @@
 #include "../../include/gpmdm_hip.h"
 #include "common.h"
 #include "pf_kernels.h"
+#include "status.h"
 
 using namespace gpmdm;
 
-namespace {
-
+namespace gpmdm {
 thread_local std::string g_err;
-
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+}  // namespace gpmdm
 
-#define HIPCHK(expr)                                                                       \
-  do {                                                                                     \
-    hipError_t e_ = (expr);                                                                \
-    if (e_ != hipSuccess)                                                                  \
-      return fail(GPMDM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));         \
-  } while (0)
+namespace {
 
-#define CHECK(cond, msg)                                                                   \
-  do {                                                                                     \
-    if (!(cond)) return fail(GPMDM_E_INVALID, msg);                                        \
-  } while (0)
-
-#define TRY(expr)                                                                          \
-  do {                                                                                     \
-    int rc_ = (expr);                                                                      \
-    if (rc_ != GPMDM_OK) return rc_;                                                       \
-  } while (0)
-
-template <typename T>
-int dalloc(T** p, size_t n) {
-  *p = nullptr;
-  if (n == 0) n = 1;
-  hipError_t e = hipMalloc((void**)p, n * sizeof(T));
-  if (e != hipSuccess) return fail(GPMDM_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
-  return GPMDM_OK;
-}
-
-template <typename T>
-void dfree(T*& p) {
-  if (p) (void)hipFree((void*)p);
-  p = nullptr;
-}
-
-inline long long cdiv(long long a, long long b) { return (a + b - 1) / b; }
 
 bool supported_d(int d) { return (d >= 1 && d <= 16) || d == 24 || d == 32; }
 
@@ -218,8 +186,10 @@ struct gpmdm_model {
 
 struct gpmdm_pf {
   gpmdm_model* m = nullptr;
-  long long P = 0, lo = 0, hi = 0, nloc = 0;
-  int n_ranks = 1, rank = 0, rng_mode = 0, resample_mode = 0, nb = 0;
+  // P = all particles = F filters x Pf (a single filter: F = 1, Pf = P)
+  long long P = 0, Pf = 0, lo = 0, hi = 0, nloc = 0;
+  int F = 1;
+  int n_ranks = 1, rank = 0, rng_mode = 0, resample_mode = 0, nb = 0, nbf = 0;
   unsigned seed_lo = 0, seed_hi = 0, frame = 0;
   bool initialised = false, switched = false, propagated = false;
   // device state
@@ -438,11 +408,14 @@ int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, doubl
 }
 
 // ------------------------------------------------------------------------------------
-int gpmdm_pf_create(gpmdm_model_t m, const double* T, int64_t P, int rng_mode, uint64_t seed,
-                    int resample_mode, int n_ranks, int rank, gpmdm_pf_t* out) {
+static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, int rng_mode, uint64_t seed,
+                     int resample_mode, int n_ranks, int rank, gpmdm_pf_t* out) {
   CHECK(m && T && out, "null argument");
   *out = nullptr;
-  CHECK(P >= 1 && P < (1ll << 31) - 256, "num_particles out of range");
+  CHECK(Pf >= 1 && F >= 1 && F <= 65535 && F * Pf < (1ll << 31) - 256, "num_particles out of range");
+  CHECK(F == 1 || (rng_mode == GPMDM_RNG_PHILOX && n_ranks == 1),
+        "filter banks use device (philox) draws on one rank; shard filters, not particles");
+  const long long P = F * Pf;
   CHECK(rng_mode == GPMDM_RNG_REPLAY || rng_mode == GPMDM_RNG_PHILOX, "bad rng mode");
   CHECK(resample_mode == GPMDM_RESAMPLE_MULTINOMIAL || resample_mode == GPMDM_RESAMPLE_SYSTEMATIC,
         "bad resample mode");
@@ -451,6 +424,8 @@ int gpmdm_pf_create(gpmdm_model_t m, const double* T, int64_t P, int rng_mode, u
   auto* pf = new gpmdm_pf();
   pf->m = m;
   pf->P = P;
+  pf->Pf = Pf;
+  pf->F = (int)F;
   pf->n_ranks = n_ranks;
   pf->rank = rank;
   pf->lo = P * rank / n_ranks;
@@ -461,6 +436,7 @@ int gpmdm_pf_create(gpmdm_model_t m, const double* T, int64_t P, int rng_mode, u
   pf->seed_lo = (unsigned)(seed & 0xffffffffu);
   pf->seed_hi = (unsigned)(seed >> 32);
   pf->nb = (int)cdiv(P, 256);
+  pf->nbf = (int)cdiv(Pf, 256);
   const int C = m->C, d = m->d, D = m->D;
   int maxparts = 0;
   for (auto& g : m->dyn) maxparts = std::max(maxparts, g.n_parts());
@@ -484,21 +460,21 @@ int gpmdm_pf_create(gpmdm_model_t m, const double* T, int64_t P, int rng_mode, u
   ALLOC(mudyn, nl * d);
   ALLOC(qobs, (long long)m->obs.n_parts() * nl);
   ALLOC(muobs, nl * D);
-  ALLOC(z, D);
+  ALLOC(z, F * D);
   if (rng_mode == GPMDM_RNG_REPLAY) {
     ALLOC(E, P * C);
     ALLOC(normals, P * d);
     ALLOC(U, P);
   }
-  ALLOC(gmax, 1);
+  ALLOC(gmax, F);
   ALLOC(e, P);
   ALLOC(local, P);
-  ALLOC(blocksum, pf->nb);
-  ALLOC(blockoffw, pf->nb);
-  ALLOC(total, 1);
+  ALLOC(blocksum, F * pf->nbf);
+  ALLOC(blockoffw, F * pf->nbf);
+  ALLOC(total, F);
   ALLOC(cum, P);
-  ALLOC(partials, (long long)pf->nb * (C + 1 + d));
-  ALLOC(readout, C + d + 1);
+  ALLOC(partials, F * pf->nbf * (C + 1 + d));
+  ALLOC(readout, F * (C + d + 1));
 #undef ALLOC
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, kPT)};
   if (hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess ||
@@ -510,6 +486,23 @@ int gpmdm_pf_create(gpmdm_model_t m, const double* T, int64_t P, int rng_mode, u
   return GPMDM_OK;
 }
 
+int gpmdm_pf_create(gpmdm_model_t m, const double* T, int64_t P, int rng_mode, uint64_t seed,
+                    int resample_mode, int n_ranks, int rank, gpmdm_pf_t* out) {
+  return pf_create(m, T, 1, P, rng_mode, seed, resample_mode, n_ranks, rank, out);
+}
+
+int gpmdm_bank_create(gpmdm_model_t m, const double* T, int64_t n_filters, int64_t P, uint64_t seed,
+                      int resample_mode, gpmdm_pf_t* out) {
+  return pf_create(m, T, n_filters, P, GPMDM_RNG_PHILOX, seed, resample_mode, 1, 0, out);
+}
+
+int gpmdm_pf_shape(gpmdm_pf_t pf, int64_t* n_filters, int64_t* P) {
+  CHECK(pf, "null handle");
+  if (n_filters) *n_filters = pf->F;
+  if (P) *P = pf->Pf;
+  return GPMDM_OK;
+}
+
 int gpmdm_pf_destroy(gpmdm_pf_t pf) {
   delete pf;
   return GPMDM_OK;
@@ -518,8 +511,9 @@ int gpmdm_pf_destroy(gpmdm_pf_t pf) {
 static ResampleArgs resample_args(gpmdm_pf* pf) {
   const gpmdm_model* m = pf->m;
   ResampleArgs ra{};
-  ra.P = pf->P;
-  ra.nb = pf->nb;
+  ra.P = pf->Pf;
+  ra.nb = pf->nbf;
+  ra.F = pf->F;
   ra.C = m->C;
   ra.d = m->d;
   ra.systematic = pf->resample_mode == GPMDM_RESAMPLE_SYSTEMATIC;
@@ -543,8 +537,9 @@ static ResampleArgs resample_args(gpmdm_pf* pf) {
 
 static NormArgs norm_args(gpmdm_pf* pf) {
   NormArgs na{};
-  na.P = pf->P;
-  na.nb = pf->nb;
+  na.P = pf->Pf;
+  na.nb = pf->nbf;
+  na.F = pf->F;
   na.ll = pf->ll;
   na.gmax = pf->gmax;
   na.e = pf->e;
@@ -569,8 +564,8 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   HIPCHK(hipMemcpy(pf->X, states, sizeof(double) * P * m->d, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(pf->cls, c32.data(), sizeof(int) * P, hipMemcpyHostToDevice));
   HIPCHK(hipMemset(pf->ll, 0, sizeof(double) * P));
-  const unsigned long long neg = 0x000fffffffffffffull;   // ord_enc(-inf)
-  HIPCHK(hipMemcpy(pf->gmax, &neg, sizeof(neg), hipMemcpyHostToDevice));
+  const std::vector<unsigned long long> neg(pf->F, 0x000fffffffffffffull);   // ord_enc(-inf)
+  HIPCHK(hipMemcpy(pf->gmax, neg.data(), sizeof(unsigned long long) * pf->F, hipMemcpyHostToDevice));
   // read-outs of the initial state: ll = log_w = 0, w = 1/P (gpmdm_pf.py:102-104)
   launch_normalise(norm_args(pf), nullptr);
   ResampleArgs ra = resample_args(pf);
@@ -600,6 +595,8 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   pf->mark_begin(s, t0);
   SwitchArgs sa{};
   sa.P = pf->P;
+  sa.Pf = pf->Pf;
+  sa.F = pf->F;
   sa.C = C;
   sa.frame = pf->frame;
   sa.seed_lo = pf->seed_lo;
@@ -653,7 +650,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipSetDevice(m->device));
   const int C = m->C, d = m->d, D = m->D;
-  HIPCHK(hipMemcpyAsync(pf->z, zh, sizeof(double) * D, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(pf->z, zh, sizeof(double) * D * pf->F, hipMemcpyHostToDevice, s));
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
     CHECK(normals, "replay mode needs the dynamics normals");
     HIPCHK(hipMemcpyAsync(pf->normals, normals, sizeof(double) * pf->P * d, hipMemcpyHostToDevice, s));
@@ -692,6 +689,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     pf->mark_begin(s, t0);
     DynFinishArgs fa{};
     fa.n_out = nl;
+    fa.Pf = pf->Pf;
     fa.n_seg = C;
     fa.d = d;
     fa.frame = pf->frame;
@@ -744,6 +742,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     oa.mu = pf->muobs;
     oa.ld_mu = D;
     oa.z = pf->z;
+    oa.Pf = pf->Pf;
     oa.il2 = m->y_il2_dev;
     oa.ll_const = (double)((float)(0.5 * D) * (float)1.8378770351409912);
     oa.ll = pf->ll;
@@ -837,12 +836,16 @@ int gpmdm_pf_read(gpmdm_pf_t pf, double* post, double* mean, double* lik, void* 
   const gpmdm_model* m = pf->m;
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;
-  double buf[kMaxReadout + 1];
-  HIPCHK(hipMemcpyAsync(buf, pf->readout, sizeof(double) * (m->C + m->d + 1), hipMemcpyDeviceToHost, s));
+  const int nr = m->C + m->d + 1;
+  std::vector<double> buf((size_t)pf->F * nr);
+  HIPCHK(hipMemcpyAsync(buf.data(), pf->readout, sizeof(double) * buf.size(), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  if (post) std::memcpy(post, buf, sizeof(double) * m->C);
-  if (mean) std::memcpy(mean, buf + m->C, sizeof(double) * m->d);
-  if (lik) *lik = buf[m->C + m->d];
+  for (int f = 0; f < pf->F; ++f) {
+    const double* b = buf.data() + (size_t)f * nr;
+    if (post) std::memcpy(post + (size_t)f * m->C, b, sizeof(double) * m->C);
+    if (mean) std::memcpy(mean + (size_t)f * m->d, b + m->C, sizeof(double) * m->d);
+    if (lik) lik[f] = b[m->C + m->d];
+  }
   return GPMDM_OK;
 }
 
@@ -867,18 +870,19 @@ int gpmdm_pf_export(gpmdm_pf_t pf, double* states, int64_t* classes, double* ll,
   std::vector<double> l(P);
   HIPCHK(hipMemcpy(l.data(), pf->ll, sizeof(double) * P, hipMemcpyDeviceToHost));
   if (ll) std::memcpy(ll, l.data(), sizeof(double) * P);
-  unsigned long long gm = 0;
-  double S = 0;
-  HIPCHK(hipMemcpy(&gm, pf->gmax, sizeof(gm), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(&S, pf->total, sizeof(S), hipMemcpyDeviceToHost));
-  const unsigned long long v = (gm >> 63) ? (gm & 0x7fffffffffffffffull) : ~gm;
-  double M;
-  std::memcpy(&M, &v, sizeof(M));
-  if (log_w)
-    for (long long i = 0; i < P; ++i) log_w[i] = l[i] - M;
-  if (w) {
-    HIPCHK(hipMemcpy(w, pf->e, sizeof(double) * P, hipMemcpyDeviceToHost));
-    for (long long i = 0; i < P; ++i) w[i] /= S;
+  std::vector<unsigned long long> gm(pf->F);
+  std::vector<double> S(pf->F);
+  HIPCHK(hipMemcpy(gm.data(), pf->gmax, sizeof(unsigned long long) * pf->F, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(S.data(), pf->total, sizeof(double) * pf->F, hipMemcpyDeviceToHost));
+  if (w) HIPCHK(hipMemcpy(w, pf->e, sizeof(double) * P, hipMemcpyDeviceToHost));
+  for (int f = 0; f < pf->F; ++f) {
+    const unsigned long long v = (gm[f] >> 63) ? (gm[f] & 0x7fffffffffffffffull) : ~gm[f];
+    double M;
+    std::memcpy(&M, &v, sizeof(M));
+    for (long long i = f * pf->Pf; i < (f + 1) * pf->Pf; ++i) {
+      if (log_w) log_w[i] = l[i] - M;
+      if (w) w[i] /= S[f];
+    }
   }
   return GPMDM_OK;
 }

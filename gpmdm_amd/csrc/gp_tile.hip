@@ -87,7 +87,7 @@ __device__ __forceinline__ double exp2_64(double t, const double* tab) {
 //   bit 6: ablation -- no LDS A-fragment reads (A operands from registers)
 //   bit 7: ablation -- every block runs the full K range (no triangular schedule)
 template <int DI, bool DYN, int VAR = 0, int NW = 4>
-__global__ __launch_bounds__(64 * NW, (DI <= 8 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
+__global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
   constexpr int NT = 64 * NW;                                // threads
   constexpr int NB = 64 * NW;                                // columns per block
   constexpr int FS = NW * 1024;                              // fragment doubles per K-step

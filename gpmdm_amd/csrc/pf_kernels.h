@@ -8,16 +8,26 @@ namespace gpmdm {
 constexpr int kMaxClasses = 32;
 constexpr int kMaxReadout = kMaxClasses + 1 + kMaxD;
 
+// Filter banks: F independent filters of Pf particles each, stored filter-major
+// (particle g = f * Pf + p).  The Philox key of filter f is seed + f and the counters use
+// the in-filter index p, so filter f of a bank draws exactly what a single filter seeded
+// with seed + f draws.
+__device__ __forceinline__ uint2 filter_key(unsigned seed_lo, unsigned seed_hi, long long f) {
+  const unsigned long long k = (((unsigned long long)seed_hi << 32) | seed_lo) + (unsigned long long)f;
+  return make_uint2((unsigned)(k & 0xffffffffu), (unsigned)(k >> 32));
+}
+
 struct SwitchArgs {
-  long long P;
-  int C;
+  long long P;                    // all particles (F * Pf)
+  long long Pf;                   // particles per filter
+  int C, F;
   unsigned frame, seed_lo, seed_hi;
   const int* cls;                 // P   current classes
   int* cls_new;                   // P   switched classes
   const double* T;                // C x C Markov matrix (device)
   const double* E;                // P x C Exp(1) draws (replay) or nullptr (philox)
   int* blockcounts;               // nb x C
-  unsigned long long* gmax_reset; // reset of the normaliser's running max (or nullptr)
+  unsigned long long* gmax_reset; // F running maxima of the normaliser to reset (or nullptr)
 };
 
 struct ScanArgs {
@@ -45,6 +55,7 @@ struct GroupArgs {
 
 struct DynFinishArgs {
   long long n_out;                // rows produced by the tile kernel
+  long long Pf;                   // particles per filter (Philox key / counter split)
   int n_seg, d;
   unsigned frame, seed_lo, seed_hi;
   const int* seg_out_base;        // nullptr: single segment
@@ -70,7 +81,8 @@ struct ObsFinishArgs {
   long long ld_q;
   const double* mu;
   long long ld_mu;
-  const double* z;                // D (device)
+  const double* z;                // F x D (device): observation of each filter
+  long long Pf;                   // particles per filter (PF; predictive maps: unused)
   const double* il2;              // D  exp(y_log_lambdas)^-2 (device)
   double ll_const;                // 0.5 * D * ln(2 pi) in float32 (gpmdm_pf.py:5, 191)
   double* ll;                     // PF output (ll[ll_offset + o]) or nullptr
@@ -78,24 +90,25 @@ struct ObsFinishArgs {
   double* var_out;                // predictive map output n x D, or nullptr
 };
 
+// Normalisation and resampling run per filter: grid (nb, F), nb blocks of 256 per filter.
 struct NormArgs {
-  long long P;
-  int nb;
-  const double* ll;
-  unsigned long long* gmax;
+  long long P;                    // particles per filter
+  int nb, F;
+  const double* ll;               // F x P
+  unsigned long long* gmax;       // F
   double* e;                      // exp(ll - max)
   double* local;                  // block-local inclusive scan of e
-  double* blocksum;
-  double* blockoff;
-  double* total;                  // sum of e
-  double* cum;                    // normalised CDF
+  double* blocksum;               // F x nb
+  double* blockoff;               // F x nb
+  double* total;                  // F: sum of e
+  double* cum;                    // normalised CDF, F x P
 };
 
 struct ResampleArgs {
-  long long P;
-  int nb, C, d, systematic, identity;
+  long long P;                    // particles per filter
+  int nb, F, C, d, systematic, identity;
   unsigned frame, seed_lo, seed_hi;
-  const double* U;                // uniforms (replay) or nullptr
+  const double* U;                // uniforms (replay, single filter) or nullptr
   const double* cum;
   const double* ll;
   const double* e;
@@ -105,9 +118,9 @@ struct ResampleArgs {
   const double* X_src;
   int* cls_dst;
   double* X_dst;
-  int* ridx;
-  double* partials;               // nb x (C + 1 + d)
-  double* readout;                // C posterior, d mean, 1 likelihood sum
+  int* ridx;                      // in-filter source index of each slot
+  double* partials;               // F x nb x (C + 1 + d)
+  double* readout;                // per filter: C posterior, d mean, 1 likelihood sum
 };
 
 struct PackArgs {

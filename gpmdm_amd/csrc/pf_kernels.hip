@@ -22,11 +22,14 @@ __global__ __launch_bounds__(kB) void k_switch(SwitchArgs a) {
   __shared__ int hist[kMaxClasses];
   const int tid = threadIdx.x;
   if (tid < a.C) hist[tid] = 0;
-  if (blockIdx.x == 0 && tid == 0 && a.gmax_reset) *a.gmax_reset = ord_enc(-INFINITY);
-  __syncthreads();
   const long long p = (long long)blockIdx.x * kB + tid;
+  if (a.gmax_reset && p < a.F) a.gmax_reset[p] = ord_enc(-INFINITY);
+  __syncthreads();
   if (p < a.P) {
     const int c0 = a.cls[p];
+    const long long f = p / a.Pf;
+    const uint2 key = filter_key(a.seed_lo, a.seed_hi, f);
+    const unsigned pl = (unsigned)(p - f * a.Pf);
     int best = 0;
     double bestv = -INFINITY;
     for (int j = 0; j < a.C; j += 2) {
@@ -35,8 +38,7 @@ __global__ __launch_bounds__(kB) void k_switch(SwitchArgs a) {
         e0 = a.E[p * a.C + j];
         if (j + 1 < a.C) e1 = a.E[p * a.C + j + 1];
       } else {
-        const uint4 r = philox4x32_10(make_uint4((unsigned)p, a.frame, kStreamSwitch, (unsigned)(j >> 1)),
-                                      make_uint2(a.seed_lo, a.seed_hi));
+        const uint4 r = philox4x32_10(make_uint4(pl, a.frame, kStreamSwitch, (unsigned)(j >> 1)), key);
         e0 = -log(u01_oo(r.x, r.y));
         e1 = -log(u01_oo(r.z, r.w));
       }
@@ -183,8 +185,9 @@ __global__ __launch_bounds__(kB) void k_dyn_finish(DynFinishArgs a) {
       e0 = a.normals[pos * d + j];
       if (j + 1 < d) e1 = a.normals[pos * d + j + 1];
     } else {
-      const uint4 r = philox4x32_10(make_uint4((unsigned)p, a.frame, kStreamDyn, (unsigned)(j >> 1)),
-                                    make_uint2(a.seed_lo, a.seed_hi));
+      const long long f = p / a.Pf;
+      const uint4 r = philox4x32_10(make_uint4((unsigned)(p - f * a.Pf), a.frame, kStreamDyn, (unsigned)(j >> 1)),
+                                    filter_key(a.seed_lo, a.seed_hi, f));
       const double u1 = u01_oo(r.x, r.y), u2 = u01_co(r.z, r.w);
       const double rr = sqrt(-2.0 * log(u1));
       double sn, cs;
@@ -214,10 +217,11 @@ __global__ __launch_bounds__(kB) void k_obs_finish(ObsFinishArgs a) {
       for (int j = lane; j < a.D; j += 64) a.var_out[o * a.D + j] = vc * a.il2[j];
     } else {
       // ll = -1/2 sum[(z-mu)^2/var + log var] + sum(-log sqrt var) - D/2 ln(2pi)_f32
+      const double* z = a.z + ((a.ll_offset + o) / a.Pf) * a.D;
       double s1 = 0.0, s2 = 0.0;
       for (int j = lane; j < a.D; j += 64) {
         const double var = vc * a.il2[j];
-        const double t = a.z[j] - mu[j];
+        const double t = z[j] - mu[j];
         s1 += t * t / var + log(var);
         s2 += -log(sqrt(var));
       }
@@ -233,15 +237,16 @@ __global__ __launch_bounds__(kB) void k_obs_finish(ObsFinishArgs a) {
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(kB) void k_norm_max(NormArgs a) {
   __shared__ double s[kB / 64];
+  const long long f = blockIdx.y;
   const long long p = (long long)blockIdx.x * kB + threadIdx.x;
-  double v = p < a.P ? a.ll[p] : -INFINITY;
+  double v = p < a.P ? a.ll[f * a.P + p] : -INFINITY;
   v = wave_max(v);
   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
   __syncthreads();
   if (threadIdx.x == 0) {
     double m = s[0];
     for (int i = 1; i < kB / 64; ++i) m = fmax(m, s[i]);
-    atomicMax(a.gmax, ord_enc(m));
+    atomicMax(a.gmax + f, ord_enc(m));
   }
 }
 
@@ -249,10 +254,11 @@ __global__ __launch_bounds__(kB) void k_norm_max(NormArgs a) {
 __global__ __launch_bounds__(kB) void k_norm_exp_scan(NormArgs a) {
   __shared__ double wsum[kB / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long f = blockIdx.y;
   const long long p = (long long)blockIdx.x * kB + tid;
-  const double M = ord_dec(*a.gmax);
-  const double e = p < a.P ? exp(a.ll[p] - M) : 0.0;
-  if (p < a.P) a.e[p] = e;
+  const double M = ord_dec(a.gmax[f]);
+  const double e = p < a.P ? exp(a.ll[f * a.P + p] - M) : 0.0;
+  if (p < a.P) a.e[f * a.P + p] = e;
   double x = e;                               // wave inclusive scan
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -264,20 +270,23 @@ __global__ __launch_bounds__(kB) void k_norm_exp_scan(NormArgs a) {
   double base = 0.0;
   for (int v = 0; v < w; ++v) base += wsum[v];
   x += base;
-  if (p < a.P) a.local[p] = x;
-  if (tid == kB - 1) a.blocksum[blockIdx.x] = x;
+  if (p < a.P) a.local[f * a.P + p] = x;
+  if (tid == kB - 1) a.blocksum[f * a.nb + blockIdx.x] = x;
 }
 
-// One workgroup: exclusive scan of block sums, total S.
+// One workgroup per filter: exclusive scan of block sums, total S.
 __global__ __launch_bounds__(1024) void k_norm_total(NormArgs a) {
   __shared__ double part[1024];
   const int tid = threadIdx.x;
   const int nb = a.nb;
+  const long long f = blockIdx.x;
+  const double* blocksum = a.blocksum + f * nb;
+  double* blockoff = a.blockoff + f * nb;
   const int chunk = (nb + 1023) / 1024;
   double s = 0.0;
   for (int i = 0; i < chunk; ++i) {
     const int b = tid * chunk + i;
-    if (b < nb) s += a.blocksum[b];
+    if (b < nb) s += blocksum[b];
   }
   part[tid] = s;
   __syncthreads();
@@ -291,19 +300,20 @@ __global__ __launch_bounds__(1024) void k_norm_total(NormArgs a) {
   for (int i = 0; i < chunk; ++i) {
     const int b = tid * chunk + i;
     if (b < nb) {
-      a.blockoff[b] = run;
-      run += a.blocksum[b];
+      blockoff[b] = run;
+      run += blocksum[b];
     }
   }
-  if (tid == 1023) *a.total = part[1023];
+  if (tid == 1023) a.total[f] = part[1023];
 }
 
 __global__ __launch_bounds__(kB) void k_cdf(NormArgs a) {
+  const long long f = blockIdx.y;
   const long long p = (long long)blockIdx.x * kB + threadIdx.x;
   if (p >= a.P) return;
-  const double S = *a.total;
+  const double S = a.total[f];
   // torch: cumsum(w) / sum, last bucket forced to 1
-  a.cum[p] = p == a.P - 1 ? 1.0 : (a.blockoff[blockIdx.x] + a.local[p]) / S;
+  a.cum[f * a.P + p] = p == a.P - 1 ? 1.0 : (a.blockoff[f * a.nb + blockIdx.x] + a.local[f * a.P + p]) / S;
 }
 
 // One thread per output slot s: inverse-CDF search, gather, read-out partials.
@@ -311,11 +321,14 @@ __global__ __launch_bounds__(kB) void k_cdf(NormArgs a) {
 __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
   __shared__ double red[kB / 64][kMaxReadout];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const long long s = (long long)blockIdx.x * kB + tid;
+  const long long f = blockIdx.y;
+  const long long s = (long long)blockIdx.x * kB + tid;   // slot within filter f
+  const long long g0 = f * a.P;                            // filter f's first particle
+  const uint2 key = filter_key(a.seed_lo, a.seed_hi, f);
   const int C = a.C, d = a.d;
   const int nq = C + 1 + d;
   const bool act = s < a.P;
-  long long idx = 0;
+  long long idx = 0;                                       // source, within filter f
   int cnew = -1;
   double e2 = 0.0, wv = 0.0;
   if (act) {
@@ -328,42 +341,43 @@ __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
         if (a.U) {
           u0 = a.U[0];
         } else {
-          const uint4 r = philox4x32_10(make_uint4(0u, a.frame, kStreamSystematic, 0u), make_uint2(a.seed_lo, a.seed_hi));
+          const uint4 r = philox4x32_10(make_uint4(0u, a.frame, kStreamSystematic, 0u), key);
           u0 = u01_co(r.x, r.y);
         }
         u = ((double)s + u0) / (double)a.P;
       } else if (a.U) {
         u = a.U[s];
       } else {
-        const uint4 r = philox4x32_10(make_uint4((unsigned)s, a.frame, kStreamResample, 0u), make_uint2(a.seed_lo, a.seed_hi));
+        const uint4 r = philox4x32_10(make_uint4((unsigned)s, a.frame, kStreamResample, 0u), key);
         u = u01_co(r.x, r.y);
       }
+      const double* cum = a.cum + g0;
       long long lo = 0, hi = a.P;               // first index with cum >= u
       while (hi - lo > 0) {
         const long long mid = lo + (hi - lo) / 2;
-        if (a.cum[mid] < u) lo = mid + 1; else hi = mid;
+        if (cum[mid] < u) lo = mid + 1; else hi = mid;
       }
       idx = lo;
     }
-    cnew = a.cls_src[idx];
+    cnew = a.cls_src[g0 + idx];
     if (!a.identity) {
-      a.ridx[s] = (int)idx;
-      a.cls_dst[s] = cnew;
-      for (int j = 0; j < d; ++j) a.X_dst[s * d + j] = a.X_src[idx * d + j];
+      a.ridx[g0 + s] = (int)idx;
+      a.cls_dst[g0 + s] = cnew;
+      for (int j = 0; j < d; ++j) a.X_dst[(g0 + s) * d + j] = a.X_src[(g0 + idx) * d + j];
     }
     // read-outs: post-resample class/state at slot s, pre-resample ll/log_w at slot s
-    const double M = ord_dec(*a.gmax);
-    const double llv = a.ll[s];
+    const double M = ord_dec(a.gmax[f]);
+    const double llv = a.ll[g0 + s];
     const double lw = llv - M;
     e2 = exp((llv + lw) - M);                  // ll + log_w - max(ll + log_w); that max is M
-    wv = a.e[s] / *a.total;
+    wv = a.e[g0 + s] / a.total[f];
   }
   for (int k = 0; k < nq; ++k) {
     double v = 0.0;
     if (act) {
       if (k < C) v = (cnew == k) ? e2 : 0.0;
       else if (k == C) v = e2;
-      else v = a.X_src[idx * d + (k - C - 1)] * wv;
+      else v = a.X_src[(g0 + idx) * d + (k - C - 1)] * wv;
     }
     v = wave_sum(v);
     if (lane == 0) red[w][k] = v;
@@ -372,7 +386,7 @@ __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
   if (tid < nq) {
     double t = 0.0;
     for (int v = 0; v < kB / 64; ++v) t += red[v][tid];
-    a.partials[(long long)blockIdx.x * nq + tid] = t;
+    a.partials[(f * a.nb + blockIdx.x) * nq + tid] = t;
   }
 }
 
@@ -381,9 +395,12 @@ __global__ __launch_bounds__(256) void k_readout(ResampleArgs a) {
   __shared__ double tot[kMaxReadout];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nq = a.C + 1 + a.d;
+  const long long f = blockIdx.x;
+  const double* partials = a.partials + f * a.nb * nq;
+  double* readout = a.readout + f * (a.C + a.d + 1);
   for (int k = 0; k < nq; ++k) {
     double s = 0.0;
-    for (long long b = tid; b < a.nb; b += 256) s += a.partials[b * nq + k];
+    for (long long b = tid; b < a.nb; b += 256) s += partials[b * nq + k];
     s = wave_sum(s);
     if (lane == 0) red[w] = s;
     __syncthreads();
@@ -393,9 +410,9 @@ __global__ __launch_bounds__(256) void k_readout(ResampleArgs a) {
   if (tid == 0) {
     double cl = 0.0;
     for (int c = 0; c < a.C; ++c) cl += tot[c];
-    for (int c = 0; c < a.C; ++c) a.readout[c] = tot[c] / cl;   // class_probabilities
-    for (int j = 0; j < a.d; ++j) a.readout[a.C + j] = tot[a.C + 1 + j];  // current_state_mean
-    a.readout[a.C + a.d] = tot[a.C];                                       // log_likelihood()
+    for (int c = 0; c < a.C; ++c) readout[c] = tot[c] / cl;   // class_probabilities
+    for (int j = 0; j < a.d; ++j) readout[a.C + j] = tot[a.C + 1 + j];  // current_state_mean
+    readout[a.C + a.d] = tot[a.C];                                       // log_likelihood()
   }
 }
 
@@ -438,14 +455,15 @@ void launch_obs_finish(const ObsFinishArgs& a, hipStream_t s) {
   if (a.n_out > 0) hipLaunchKernelGGL(k_obs_finish, dim3(nblk(a.n_out, kB / 64)), dim3(kB), 0, s, a);
 }
 void launch_normalise(const NormArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_norm_max, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
-  hipLaunchKernelGGL(k_norm_exp_scan, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
-  hipLaunchKernelGGL(k_norm_total, dim3(1), dim3(1024), 0, s, a);
-  hipLaunchKernelGGL(k_cdf, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+  const dim3 g(nblk(a.P, kB), (unsigned)a.F);
+  hipLaunchKernelGGL(k_norm_max, g, dim3(kB), 0, s, a);
+  hipLaunchKernelGGL(k_norm_exp_scan, g, dim3(kB), 0, s, a);
+  hipLaunchKernelGGL(k_norm_total, dim3((unsigned)a.F), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(k_cdf, g, dim3(kB), 0, s, a);
 }
 void launch_resample(const ResampleArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_resample, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
-  hipLaunchKernelGGL(k_readout, dim3(1), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_resample, dim3(nblk(a.P, kB), (unsigned)a.F), dim3(kB), 0, s, a);
+  hipLaunchKernelGGL(k_readout, dim3((unsigned)a.F), dim3(256), 0, s, a);
 }
 void launch_pack(const PackArgs& a, hipStream_t s) {
   if (a.n > 0) hipLaunchKernelGGL(k_pack, dim3(nblk(a.n, kB)), dim3(kB), 0, s, a);

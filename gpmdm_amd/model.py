@@ -118,7 +118,10 @@ class GPMDM:
         self.class_aware_observations_list = [[] for _ in range(self.n_classes)]
         self.X = None
         self._handle = None
-        self._precompute_device = None   # None: CPU for N <= 4096, the model GPU above
+        # where _precompute_kernel_inverses runs: None = torch on the CPU for N <= 4096 (the
+        # reference's own arithmetic), the library's device factor (gpmdm_gp_factor:
+        # rocSOLVER potrf/trtri) above; or force "cpu" / "device"
+        self._precompute_device = None
         # waves per GP-tile workgroup (4 or 8; 0 = library default); env override for A/B runs
         self.tile_waves = int(os.environ.get("GPMDM_TILE_WAVES", "0"))
 
@@ -212,7 +215,10 @@ class GPMDM:
             raise NotImplementedError("the particle-filter path supports dyn_back_step=1 (as the "
                                       "reference PF does, gpmdm_pf.py:164)")
         N = self.X.shape[0]
-        dev = self._precompute_device or (torch.device("cpu") if N <= 4096 else self.device)
+        where = self._precompute_device or ("cpu" if N <= 4096 else "device")
+        if where == "device":
+            return self._precompute_on_device()
+        dev = torch.device("cpu")
         f64 = dict(dtype=torch.float64, device=dev)
         X = self.X.to(**f64)
         Y = torch.as_tensor(self.get_Y(), **f64)
@@ -245,6 +251,43 @@ class GPMDM:
                 dyn.append((xi.cpu().numpy().copy(), Rc.cpu().numpy().copy(), alpha.cpu().numpy().copy()))
             obs = (Ry.cpu().numpy().copy(), beta.cpu().numpy().copy())
         self._upload(obs, dyn)
+
+    def _precompute_on_device(self):
+        """The same factors through gpmdm_gp_factor (device Gram matrix, rocSOLVER potrf +
+        trtri, rocBLAS trmm), one GP block at a time."""
+        lib = _lib.load()
+        dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+
+        def factor(X, log_ls, lin_c2, a, b, c, B, what):
+            X = np.ascontiguousarray(X, dtype=np.float64)
+            B = np.ascontiguousarray(B, dtype=np.float64)
+            n, d = X.shape
+            ls = np.ascontiguousarray(np.exp(_to_np(log_ls)))
+            c2 = None if lin_c2 is None else np.ascontiguousarray(lin_c2, dtype=np.float64)
+            R = np.empty((n, n))
+            M = np.empty((n, B.shape[1]))
+            _lib.check(lib.gpmdm_gp_factor(dev_index, _lib.dptr(X), n, d, _lib.dptr(ls), _lib.dptr(c2),
+                                           a, b, c, _lib.dptr(B), B.shape[1], _lib.dptr(R), _lib.dptr(M)), what)
+            return R, M
+
+        X = self.X.numpy()
+        Y = np.asarray(self.get_Y(), dtype=np.float64)
+        sy2 = float(torch.exp(self.y_log_sigma_n)) ** 2
+        sx2 = float(torch.exp(self.x_log_sigma_n)) ** 2
+        Ry, beta = factor(X, self.y_log_lengthscales, None, sy2, self.sigma_n_num_Y ** 2, 0.0, Y, "K_y")
+        Xin, Xout, _ = self.get_Xin_Xout_matrices(X=self.X)
+        Xin, Xout = _to_np(Xin), _to_np(Xout)
+        c2 = _to_np(torch.exp(self.x_log_lin_coeff) ** 2)
+        dyn, off = [], 0
+        for c, n_c in enumerate(self._class_dynamics_rows()):
+            if n_c <= 0:
+                raise ValueError(f"class {c} has no dynamics pairs")
+            xi, xo = Xin[off:off + n_c], Xout[off:off + n_c]
+            off += n_c
+            Rc, alpha = factor(xi, self.x_log_lengthscales, c2, sx2, self.sigma_n_num_X ** 2, 1e-6, xo,
+                               f"K_x class {c}")
+            dyn.append((np.ascontiguousarray(xi), Rc, alpha))
+        self._upload((Ry, beta), dyn)
 
     def _upload(self, obs, dyn):
         lib = _lib.load()

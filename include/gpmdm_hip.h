@@ -99,6 +99,17 @@ int gpmdm_pf_create(gpmdm_model_t model, const double* T, int64_t P, int rng_mod
                     gpmdm_pf_t* out);
 int gpmdm_pf_destroy(gpmdm_pf_t pf);
 
+/* Filter bank: n_filters independent filters of P particles each sharing one model (the
+ * 39 trials test_gpmdm_pf.ipynb runs one after another).  Device
+ * (philox) draws, one rank.  Filter f draws exactly what a single filter created with
+ * seed + f draws, so its results are bit-identical to that filter's.  The handle works
+ * with every gpmdm_pf_* call below, with per-filter arrays stacked filter-major:
+ * states/classes (F*P) in init/export, z (F x D) in propagate, F x C / F x d / F in read.
+ * gpmdm_pf_shape reports (F, P) of any handle (F = 1 for gpmdm_pf_create). */
+int gpmdm_bank_create(gpmdm_model_t model, const double* T, int64_t n_filters, int64_t P,
+                      uint64_t seed, int resample_mode, gpmdm_pf_t* out);
+int gpmdm_pf_shape(gpmdm_pf_t pf, int64_t* n_filters, int64_t* P);
+
 /* _init_particles / reset()  (gpmdm_pf.py:87-115, 264-265): states P x d, classes P
  * (host).  Clears weights to 1/P and log-likelihoods to 0 as the reference does. */
 int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes);
@@ -152,6 +163,21 @@ int gpmdm_pf_export(gpmdm_pf_t pf, double* states, int64_t* classes, double* ll,
 #define GPMDM_N_STAGES 6
 int gpmdm_pf_enable_timing(gpmdm_pf_t pf, int enable);
 int gpmdm_pf_stage_times(gpmdm_pf_t pf, double* ms, int64_t* launches);
+
+/* Device-side GP factor: the recipe of _precompute_kernel_inverses
+ * (gpmdm.py:1284-1305) for one GP block -- the observation GP, or one class block of the
+ * dynamics GP (the reference's full masked matrix has exact zeros off the class blocks):
+ *   K = exp(-|x_i/l - x_j/l|^2) + diag_a I + diag_b I [+ [x_i,1] diag(lin_c2) [x_j,1]^T] + diag_c I
+ *   U = chol_upper(K) (rocSOLVER potrf), R = U^-1 (trtri), M = R R^T B (two rocBLAS trmm).
+ * X: n x d, lengthscales: d, lin_c2: d+1 (dynamics) or NULL (observations), B: n x k (k may
+ * be 0); outputs R (n x n, strictly-lower part zero) and M (n x k).  All host, row-major.
+ * The observation GP uses diag_a = sigma_n^2, diag_b = sigma_num^2, diag_c = 0
+ * (gpmdm.py:381-406); a dynamics block adds the linear kernel and diag_c = 1e-6
+ * (gpmdm.py:408-434, 1299-1305).  A K that is not positive definite is GPMDM_E_INVALID
+ * (the reference ignores cholesky_ex's info and continues with garbage). */
+int gpmdm_gp_factor(int device, const double* X, int64_t n, int32_t d, const double* lengthscales,
+                    const double* lin_c2, double diag_a, double diag_b, double diag_c,
+                    const double* B, int64_t k, double* R, double* M);
 
 /* Message of the last failed call on this thread ("" if none). */
 const char* gpmdm_last_error(void);
