@@ -152,12 +152,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if ndev and local >= ndev:          # rehearsal with more ranks than GPUs (never on a full node)
+        local %= ndev
+    backend = os.environ.get("GPMDM_BENCH_BACKEND", "nccl")
     dist = None
     group = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         group = dist.group.WORLD
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
@@ -204,6 +211,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     post = pf.class_probabilities().numpy()
+    dyn_rows = pf.dynamics_rows()
 
     N, D, d = model.X.shape[0], model.D, model.d
     P_local = P_total // world
@@ -239,6 +247,9 @@ def main():
                      "launch_ms": obs_launch_s * 1e3},
         "stages_ms_per_step": {k: v[0] / max(v[1], 1) for k, v in stages.items()},
         "posterior_last": [float(x) for x in post],
+        "dyn_rows_last": {"evaluated": dyn_rows, "particles": P_local,
+                          "note": "dynamics GP rows of the last step: one per distinct (ancestor, class) "
+                                  "key (bitwise-identical ancestor de-duplication, DESIGN.md §3)"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

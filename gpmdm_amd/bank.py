@@ -32,7 +32,8 @@ from .model import GPMDM
 
 class GPMDM_PF_Bank:
     def __init__(self, gpmdm: GPMDM, markov_switching_model, num_filters: int, num_particles: int, *,
-                 seed=None, resample: str = "multinomial", process_group=None, shard=None):
+                 seed=None, resample: str = "multinomial", process_group=None, shard=None,
+                 dedup: bool = True):
         self._gpmdm = gpmdm
         self._gpmdm.set_evaluation_mode()
         self._T = torch.as_tensor(markov_switching_model).type(torch.float64)
@@ -68,6 +69,7 @@ class GPMDM_PF_Bank:
                 _lib.GPMDM_RESAMPLE_MULTINOMIAL if resample == "multinomial" else _lib.GPMDM_RESAMPLE_SYSTEMATIC,
                 ctypes.byref(h)), "GPMDM_PF_Bank")
             self._h = h
+            _lib.check(_lib.load().gpmdm_pf_set_dedup(h, 1 if dedup else 0), "dedup")
             self._init_particles()
 
     def __del__(self):

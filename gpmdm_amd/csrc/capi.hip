@@ -192,11 +192,15 @@ struct gpmdm_pf {
   int n_ranks = 1, rank = 0, rng_mode = 0, resample_mode = 0, nb = 0, nbf = 0;
   unsigned seed_lo = 0, seed_hi = 0, frame = 0;
   bool initialised = false, switched = false, propagated = false;
+  bool dedup = true;                  // ancestor de-duplication of the dynamics GP
   // device state
   double *T = nullptr, *X = nullptr, *X_prop = nullptr, *ll = nullptr;
   int *cls = nullptr, *cls_new = nullptr, *perm = nullptr, *ridx = nullptr;
   int *blockcounts = nullptr, *blockoff = nullptr, *small = nullptr;   // small: class tables
   int *obs_tab = nullptr;
+  // ancestor de-duplication: owner/slot are C x P keyed by (class, ancestor)
+  unsigned* owner = nullptr;
+  int *slot = nullptr, *lflag = nullptr, *lblock = nullptr, *ltab = nullptr, *lperm = nullptr;
   double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *muobs = nullptr;
   int nparts_dyn_max = 0;
   double *z = nullptr, *E = nullptr, *normals = nullptr, *U = nullptr;
@@ -215,14 +219,21 @@ struct gpmdm_pf {
   int* seg_end() const { return small + 120; }
   int* seg_out() const { return small + 160; }
   int* seg_tiles() const { return small + 200; }
+  // leader segment tables (same shape as the full ones)
+  int* lseg_begin() const { return ltab; }
+  int* lseg_end() const { return ltab + 40; }
+  int* lseg_out() const { return ltab + 80; }
+  int* lseg_tiles() const { return ltab + 120; }
 
   ~gpmdm_pf() {
     double* ds[] = {T, X, X_prop, ll, qdyn, mudyn, qobs, muobs, z, E, normals, U,
                     e, local, blocksum, blockoffw, total, cum, partials, readout};
     for (double* p : ds) dfree(p);
-    int* is[] = {cls, cls_new, perm, ridx, blockcounts, blockoff, small, obs_tab};
+    int* is[] = {cls, cls_new, perm, ridx, blockcounts, blockoff, small, obs_tab,
+                 slot, lflag, lblock, ltab, lperm};
     for (int* p : is) dfree(p);
     dfree(gmax);
+    dfree(owner);
     for (auto& r : recs) { pool.push_back(r.a); pool.push_back(r.b); }
     for (auto ev : pool) (void)hipEventDestroy(ev);
   }
@@ -456,6 +467,12 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   ALLOC(blockoff, (long long)pf->nb * C);
   ALLOC(small, 256);
   ALLOC(obs_tab, 8);
+  ALLOC(owner, (long long)C * P);
+  ALLOC(slot, (long long)C * P);
+  ALLOC(lflag, P);
+  ALLOC(lblock, pf->nb);
+  ALLOC(ltab, 200);
+  ALLOC(lperm, P);
   ALLOC(qdyn, (long long)maxparts * nl);
   ALLOC(mudyn, nl * d);
   ALLOC(qobs, (long long)m->obs.n_parts() * nl);
@@ -563,6 +580,8 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   }
   HIPCHK(hipMemcpy(pf->X, states, sizeof(double) * P * m->d, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(pf->cls, c32.data(), sizeof(int) * P, hipMemcpyHostToDevice));
+  for (long long i = 0; i < P; ++i) c32[i] = (int)(i % pf->Pf);   // no shared ancestors yet
+  HIPCHK(hipMemcpy(pf->ridx, c32.data(), sizeof(int) * P, hipMemcpyHostToDevice));
   HIPCHK(hipMemset(pf->ll, 0, sizeof(double) * P));
   const std::vector<unsigned long long> neg(pf->F, 0x000fffffffffffffull);   // ord_enc(-inf)
   HIPCHK(hipMemcpy(pf->gmax, neg.data(), sizeof(unsigned long long) * pf->F, hipMemcpyHostToDevice));
@@ -593,6 +612,8 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   }
   hipEvent_t t0;
   pf->mark_begin(s, t0);
+  if (pf->dedup && pf->nloc > 0)
+    HIPCHK(hipMemsetAsync(pf->owner, 0xff, sizeof(unsigned) * C * pf->P, s));
   SwitchArgs sa{};
   sa.P = pf->P;
   sa.Pf = pf->Pf;
@@ -607,6 +628,12 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   sa.E = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->E : nullptr;
   sa.blockcounts = pf->blockcounts;
   sa.gmax_reset = pf->gmax;
+  if (pf->dedup && pf->nloc > 0) {
+    sa.anc = pf->ridx;
+    sa.owner = pf->owner;
+    sa.lo = pf->lo;
+    sa.hi = pf->hi;
+  }
   launch_switch(sa, s);
   ScanArgs sc{};
   sc.nb = pf->nb;
@@ -631,6 +658,30 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   ga.blockoff = pf->blockoff;
   ga.perm = pf->perm;
   launch_group(ga, s);
+  if (pf->dedup && pf->nloc > 0) {
+    LeadArgs la{};
+    la.P = pf->P;
+    la.Pf = pf->Pf;
+    la.lo = pf->lo;
+    la.hi = pf->hi;
+    la.nb = pf->nb;
+    la.C = C;
+    la.perm = pf->perm;
+    la.cls_new = pf->cls_new;
+    la.anc = pf->ridx;
+    la.owner = pf->owner;
+    la.seg_pos_begin = pf->seg_begin();
+    la.seg_pos_end = pf->seg_end();
+    la.lflag_scan = pf->lflag;
+    la.lblock = pf->lblock;
+    la.lseg_pos_begin = pf->lseg_begin();
+    la.lseg_pos_end = pf->lseg_end();
+    la.lseg_out_base = pf->lseg_out();
+    la.lseg_tile_start = pf->lseg_tiles();
+    la.lperm = pf->lperm;
+    la.slot = pf->slot;
+    launch_lead(la, s);
+  }
   pf->mark_end(s, GPMDM_STAGE_SWITCH, t0);
   HIPCHK(hipGetLastError());
   if (class_counts) {
@@ -672,11 +723,19 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
       tp.nw = m->dyn[c0].nw;
       tp.tiles_ub = (int)(cdiv(nl, kPT) + ns);
       tp.n_j_max = njm;
-      tp.seg_pos_begin = pf->seg_begin() + c0;
-      tp.seg_pos_end = pf->seg_end() + c0;
-      tp.seg_out_base = pf->seg_out() + c0;
-      tp.seg_tile_start = pf->seg_tiles() + c0;
-      tp.perm = pf->perm;
+      if (pf->dedup) {                  // one row per (ancestor, class) leader
+        tp.seg_pos_begin = pf->lseg_begin() + c0;
+        tp.seg_pos_end = pf->lseg_end() + c0;
+        tp.seg_out_base = pf->lseg_out() + c0;
+        tp.seg_tile_start = pf->lseg_tiles() + c0;
+        tp.perm = pf->lperm;
+      } else {
+        tp.seg_pos_begin = pf->seg_begin() + c0;
+        tp.seg_pos_end = pf->seg_end() + c0;
+        tp.seg_out_base = pf->seg_out() + c0;
+        tp.seg_tile_start = pf->seg_tiles() + c0;
+        tp.perm = pf->perm;
+      }
       tp.X = pf->X;
       fill_tile_common(tp, m, true);
       tp.qpart = pf->qdyn;
@@ -708,6 +767,11 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     for (int j = 0; j < d; ++j) fa.il2[j] = m->x_il2[j];
     fa.normals = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->normals : nullptr;
     fa.X_out = pf->X_prop;
+    if (pf->dedup) {
+      fa.slot = pf->slot;
+      fa.anc = pf->ridx;
+      fa.P = pf->P;
+    }
     launch_dyn_finish(fa, s);
     pf->mark_end(s, GPMDM_STAGE_DYN_FINISH, t0);
 
@@ -884,6 +948,28 @@ int gpmdm_pf_export(gpmdm_pf_t pf, double* states, int64_t* classes, double* ll,
       if (w) w[i] /= S[f];
     }
   }
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_set_dedup(gpmdm_pf_t pf, int enable) {
+  CHECK(pf, "null handle");
+  if (pf->switched) return fail(GPMDM_E_STATE, "set_dedup between switch and propagate");
+  pf->dedup = enable != 0;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_dyn_rows(gpmdm_pf_t pf, int64_t* rows, void* stream) {
+  CHECK(pf && rows, "null argument");
+  HIPCHK(hipSetDevice(pf->m->device));
+  const int C = pf->m->C;
+  int b[kMaxClasses], e[kMaxClasses];
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipMemcpyAsync(b, pf->dedup ? pf->lseg_begin() : pf->seg_begin(), sizeof(int) * C, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(e, pf->dedup ? pf->lseg_end() : pf->seg_end(), sizeof(int) * C, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  long long r = 0;
+  for (int c = 0; c < C; ++c) r += e[c] - b[c];
+  *rows = r;
   return GPMDM_OK;
 }
 

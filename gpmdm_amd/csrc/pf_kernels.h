@@ -28,6 +28,12 @@ struct SwitchArgs {
   const double* E;                // P x C Exp(1) draws (replay) or nullptr (philox)
   int* blockcounts;               // nb x C
   unsigned long long* gmax_reset; // F running maxima of the normaliser to reset (or nullptr)
+  // ancestor de-duplication (nullptr: off).  Particles of this rank's slice [lo, hi) that
+  // share a resampling ancestor and a new class have bit-identical dynamics-GP inputs; the
+  // smallest such particle index becomes the key's leader: owner[c * P + ancestor] = min p.
+  const int* anc;                 // P   in-filter ancestor index (resample source; identity after init)
+  unsigned* owner;                // C x P, preset to 0xffffffff
+  long long lo, hi;
 };
 
 struct ScanArgs {
@@ -53,6 +59,26 @@ struct GroupArgs {
   int* perm;                      // grouped position -> particle
 };
 
+// Leader compaction over the class-grouped positions (ancestor de-duplication).
+struct LeadArgs {
+  long long P, Pf, lo, hi;
+  int nb, C;
+  const int* perm;                // grouped position -> particle
+  const int* cls_new;
+  const int* anc;
+  const unsigned* owner;
+  const int* seg_pos_begin;       // [C] this rank's positions of class c (full grouping)
+  const int* seg_pos_end;
+  int* lflag_scan;                // P   block-local exclusive scan of the leader flags
+  int* lblock;                    // nb  leaders per block of positions
+  int* lseg_pos_begin;            // [C] leader rows of class c: [begin, end)
+  int* lseg_pos_end;
+  int* lseg_out_base;             // [C] (= begin: rows are their own output index)
+  int* lseg_tile_start;           // [C + 1]
+  int* lperm;                     // leader row -> particle
+  int* slot;                      // C x P: key -> leader row
+};
+
 struct DynFinishArgs {
   long long n_out;                // rows produced by the tile kernel
   long long Pf;                   // particles per filter (Philox key / counter split)
@@ -72,6 +98,10 @@ struct DynFinishArgs {
   const double* normals;          // grouped-position-major draws (replay) or nullptr
   double* X_out;                  // PF: propagated states (P x d, particle index)
   double* var_out;                // predictive map: n x d variances (PF: nullptr)
+  // ancestor de-duplication: the tile rows are leader rows, slot[c * P + g0 + anc[p]]
+  const int* slot;                // nullptr: row = output index o
+  const int* anc;
+  long long P;
 };
 
 struct ObsFinishArgs {
@@ -135,6 +165,7 @@ struct PackArgs {
 void launch_switch(const SwitchArgs& a, hipStream_t s);
 void launch_scan_counts(const ScanArgs& a, hipStream_t s);
 void launch_group(const GroupArgs& a, hipStream_t s);
+void launch_lead(const LeadArgs& a, hipStream_t s);
 void launch_dyn_finish(const DynFinishArgs& a, hipStream_t s);
 void launch_obs_finish(const ObsFinishArgs& a, hipStream_t s);
 void launch_normalise(const NormArgs& a, hipStream_t s);

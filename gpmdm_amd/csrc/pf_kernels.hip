@@ -23,6 +23,7 @@ __global__ __launch_bounds__(kB) void k_switch(SwitchArgs a) {
   const int tid = threadIdx.x;
   if (tid < a.C) hist[tid] = 0;
   const long long p = (long long)blockIdx.x * kB + tid;
+  long long dkey = -1;                              // de-duplication key (owner index)
   if (a.gmax_reset && p < a.F) a.gmax_reset[p] = ord_enc(-INFINITY);
   __syncthreads();
   if (p < a.P) {
@@ -52,6 +53,23 @@ __global__ __launch_bounds__(kB) void k_switch(SwitchArgs a) {
     }
     a.cls_new[p] = best;
     atomicAdd(&hist[best], 1);
+    if (a.owner && p >= a.lo && p < a.hi) dkey = (long long)best * a.P + f * a.Pf + a.anc[p];
+  }
+  if (a.owner) {
+    // Leader election: one atomicMin per distinct key per wave (its lowest lane = smallest
+    // p), so a collapsed cloud (every particle one ancestor) does not serialise P atomics
+    // on one address.
+    const int lane = tid & 63;
+    unsigned long long pending = __ballot(dkey >= 0);
+    while (pending) {
+      const int l0 = __ffsll((long long)pending) - 1;
+      const unsigned lo32 = __shfl((unsigned)(dkey & 0xffffffffll), l0);
+      const int hi32 = __shfl((int)(dkey >> 32), l0);
+      const long long k0 = ((long long)hi32 << 32) | lo32;
+      const unsigned long long same = __ballot(dkey == k0);
+      if (lane == l0) atomicMin(&a.owner[k0], (unsigned)p);
+      pending &= ~same;
+    }
   }
   __syncthreads();
   if (tid < a.C) a.blockcounts[(long long)blockIdx.x * a.C + tid] = hist[tid];
@@ -147,6 +165,101 @@ __global__ __launch_bounds__(kB) void k_group(GroupArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
+// Ancestor de-duplication of the dynamics GP.  After a resample, every
+// offspring of one ancestor holds a bit-identical copy of its state, and the dynamics GP
+// of (state, class) does not depend on anything else, so the tile kernel only needs one
+// row per distinct (ancestor, new class) key of this rank's slice: its leader (the
+// smallest particle index, k_switch's atomicMin).  Leaders are compacted in class-grouped
+// position order, so leader rows of class c are contiguous and the tile kernel's segment
+// tables keep their meaning.  Per-particle arithmetic is independent of which rows share a
+// tile, so the results are bitwise those of the undeduplicated path.
+__device__ __forceinline__ int lead_flag(const LeadArgs& a, long long pos) {
+  if (pos >= a.P) return 0;
+  const long long p = a.perm[pos];
+  if (p < a.lo || p >= a.hi) return 0;
+  const long long f = p / a.Pf;
+  return a.owner[(long long)a.cls_new[p] * a.P + f * a.Pf + a.anc[p]] == (unsigned)p;
+}
+
+// flag | block-local exclusive count << 1, and leaders per block
+__global__ __launch_bounds__(kB) void k_lead_flags(LeadArgs a) {
+  __shared__ int wc[kB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long pos = (long long)blockIdx.x * kB + tid;
+  const int lf = lead_flag(a, pos);
+  const unsigned long long m = __ballot(lf);
+  const int excl = __popcll(m & ((1ull << lane) - 1ull));
+  if (lane == 0) wc[w] = __popcll(m);
+  __syncthreads();
+  int base = 0;
+  for (int v = 0; v < w; ++v) base += wc[v];
+  if (pos < a.P) a.lflag_scan[pos] = ((base + excl) << 1) | lf;
+  if (tid == 0) {
+    int t = 0;
+    for (int v = 0; v < kB / 64; ++v) t += wc[v];
+    a.lblock[blockIdx.x] = t;
+  }
+}
+
+// One workgroup: lblock -> exclusive offsets (in place), then the leader segment tables.
+__global__ __launch_bounds__(1024) void k_lead_tables(LeadArgs a) {
+  __shared__ int part[1024];
+  __shared__ int total;
+  const int tid = threadIdx.x;
+  const int nb = a.nb;
+  const int chunk = (nb + 1023) / 1024;
+  int s = 0;
+  for (int i = 0; i < chunk; ++i) {
+    const int b = tid * chunk + i;
+    if (b < nb) s += a.lblock[b];
+  }
+  part[tid] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  int run = tid ? part[tid - 1] : 0;
+  for (int i = 0; i < chunk; ++i) {
+    const int b = tid * chunk + i;
+    if (b < nb) {
+      const int cnt = a.lblock[b];
+      a.lblock[b] = run;
+      run += cnt;
+    }
+  }
+  if (tid == 1023) total = part[1023];
+  __syncthreads();
+  if (tid == 0) {
+    auto row = [&](long long x) { return x >= a.P ? total : a.lblock[x / kB] + (a.lflag_scan[x] >> 1); };
+    int ts = 0;
+    for (int c = 0; c < a.C; ++c) {
+      const int b0 = row(a.seg_pos_begin[c]), e0 = row(a.seg_pos_end[c]);
+      a.lseg_pos_begin[c] = b0;
+      a.lseg_pos_end[c] = e0;
+      a.lseg_out_base[c] = b0;
+      a.lseg_tile_start[c] = ts;
+      ts += (e0 - b0 + kPT - 1) / kPT;
+    }
+    a.lseg_tile_start[a.C] = ts;
+  }
+}
+
+__global__ __launch_bounds__(kB) void k_lead_compact(LeadArgs a) {
+  const long long pos = (long long)blockIdx.x * kB + threadIdx.x;
+  if (pos >= a.P) return;
+  const int v = a.lflag_scan[pos];
+  if (!(v & 1)) return;
+  const long long p = a.perm[pos];
+  const int r = a.lblock[blockIdx.x] + (v >> 1);
+  const long long f = p / a.Pf;
+  a.lperm[r] = (int)p;
+  a.slot[(long long)a.cls_new[p] * a.P + f * a.Pf + a.anc[p]] = r;
+}
+
+// ---------------------------------------------------------------------------------
 // out index o -> class segment
 __device__ __forceinline__ int seg_of(const int* seg_out_base, int n_seg, int total, int o) {
   int c = 0;
@@ -162,9 +275,11 @@ __global__ __launch_bounds__(kB) void k_dyn_finish(DynFinishArgs a) {
   const int c = a.seg_out_base ? seg_of(a.seg_out_base, a.n_seg, (int)a.n_out, (int)o) : 0;
   const long long pos = (a.seg_pos_begin ? a.seg_pos_begin[c] : 0) + (o - (a.seg_out_base ? a.seg_out_base[c] : 0));
   const long long p = a.perm ? a.perm[pos] : pos;
+  long long r = o;                      // tile row holding this particle's GP outputs
+  if (a.slot) r = a.slot[(long long)c * a.P + (p / a.Pf) * a.Pf + a.anc[p]];
   double q = 0.0;
   const int np = a.n_parts[c];
-  for (int k = 0; k < np; ++k) q += a.qpart[(long long)k * a.ld_q + o];
+  for (int k = 0; k < np; ++k) q += a.qpart[(long long)k * a.ld_q + r];
   // k(x*, x*) of the dynamics kernel without noise: 1 + [x,1] diag(c^2) [x,1]^T (gpmdm.py:1100)
   const int d = a.d;
   double kd = 0.0;
@@ -195,8 +310,8 @@ __global__ __launch_bounds__(kB) void k_dyn_finish(DynFinishArgs a) {
       e0 = rr * cs;
       e1 = rr * sn;
     }
-    a.X_out[p * d + j] = e0 * sqrt(vc * a.il2[j]) + a.mu[o * a.ld_mu + j];
-    if (j + 1 < d) a.X_out[p * d + j + 1] = e1 * sqrt(vc * a.il2[j + 1]) + a.mu[o * a.ld_mu + j + 1];
+    a.X_out[p * d + j] = e0 * sqrt(vc * a.il2[j]) + a.mu[r * a.ld_mu + j];
+    if (j + 1 < d) a.X_out[p * d + j + 1] = e1 * sqrt(vc * a.il2[j + 1]) + a.mu[r * a.ld_mu + j + 1];
   }
 }
 
@@ -447,6 +562,11 @@ void launch_scan_counts(const ScanArgs& a, hipStream_t s) {
 }
 void launch_group(const GroupArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_group, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+}
+void launch_lead(const LeadArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_lead_flags, dim3((unsigned)a.nb), dim3(kB), 0, s, a);
+  hipLaunchKernelGGL(k_lead_tables, dim3(1), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(k_lead_compact, dim3((unsigned)a.nb), dim3(kB), 0, s, a);
 }
 void launch_dyn_finish(const DynFinishArgs& a, hipStream_t s) {
   if (a.n_out > 0) hipLaunchKernelGGL(k_dyn_finish, dim3(nblk(a.n_out, kB)), dim3(kB), 0, s, a);

@@ -10,7 +10,10 @@ every per-frame computation runs in the HIP library.  Extra keyword options:
 * ``seed``: Philox key (default: drawn from torch's generator);
 * ``resample='multinomial'`` (reference, gpmdm_pf.py:211) or ``'systematic'``;
 * ``process_group``: a ``torch.distributed`` group to shard particles over (one process
-  per GPU; one all-gather of the packed particle rows per frame).
+  per GPU; one all-gather of the packed particle rows per frame);
+* ``dedup`` (default True): evaluate the dynamics GP once per distinct (resampling
+  ancestor, new class) pair -- offspring of one ancestor hold bit-identical states -- and
+  share the result; bitwise identical to ``dedup=False`` (every particle evaluated).
 
 Reference quirks kept for parity: log variance counted twice in the
 log-likelihood, float32 ``ln 2pi``, non-recursive weights, read-outs pairing
@@ -31,7 +34,7 @@ from .model import GPMDM
 class GPMDM_PF:
     def __init__(self, gpmdm: GPMDM, markov_switching_model, num_particles: int, *,
                  rng: str = "torch", seed=None, resample: str = "multinomial", process_group=None,
-                 shard=None, exchange=None):
+                 shard=None, exchange=None, dedup: bool = True):
         self._gpmdm = gpmdm
         self._gpmdm.set_evaluation_mode()
         self._markov_switching_model = torch.as_tensor(markov_switching_model).type(self.dtype)
@@ -66,6 +69,7 @@ class GPMDM_PF:
             _lib.GPMDM_RESAMPLE_MULTINOMIAL if resample == "multinomial" else _lib.GPMDM_RESAMPLE_SYSTEMATIC,
             self._world, self._rank, ctypes.byref(h)), "GPMDM_PF")
         self._h = h
+        _lib.check(lib.gpmdm_pf_set_dedup(h, 1 if dedup else 0), "dedup")
         self._readout = None
         if self._world > 1:
             w, lo, hi = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
@@ -233,6 +237,13 @@ class GPMDM_PF:
         classes = np.ascontiguousarray(classes, dtype=np.int64).reshape(self._num_particles)
         _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "load_state")
         self._readout = None
+
+    def dynamics_rows(self) -> int:
+        """Rows the last dynamics-GP pass evaluated (distinct ancestor/class keys when
+        de-duplicating; this rank's particle count otherwise)."""
+        r = np.zeros(1, dtype=np.int64)
+        _lib.check(_lib.load().gpmdm_pf_dyn_rows(self._h, _lib.i64ptr(r), self._stream()), "dyn_rows")
+        return int(r[0])
 
     def enable_timing(self, on: bool = True):
         _lib.check(_lib.load().gpmdm_pf_enable_timing(self._h, 1 if on else 0))

@@ -164,6 +164,17 @@ int gpmdm_pf_export(gpmdm_pf_t pf, double* states, int64_t* classes, double* ll,
 int gpmdm_pf_enable_timing(gpmdm_pf_t pf, int enable);
 int gpmdm_pf_stage_times(gpmdm_pf_t pf, double* ms, int64_t* launches);
 
+/* Ancestor de-duplication of the dynamics GP (default on).  After a resample, offspring of
+ * one ancestor carry bit-identical states; the dynamics GP (gpmdm.py:1032-1068) of a
+ * (state, class) pair is evaluated once per distinct (ancestor, new class) key of the
+ * rank's slice and shared by its offspring.  Results are bitwise identical either way
+ * (per-particle arithmetic does not depend on tile membership); enable=0 evaluates every
+ * particle, as the reference does.  Must not be toggled between switch and propagate.
+ * gpmdm_pf_dyn_rows synchronises `stream` and returns the rows the last dynamics pass
+ * evaluated (distinct keys with de-duplication, the slice size without). */
+int gpmdm_pf_set_dedup(gpmdm_pf_t pf, int enable);
+int gpmdm_pf_dyn_rows(gpmdm_pf_t pf, int64_t* rows, void* stream);
+
 /* Device-side GP factor: the recipe of _precompute_kernel_inverses
  * (gpmdm.py:1284-1305) for one GP block -- the observation GP, or one class block of the
  * dynamics GP (the reference's full masked matrix has exact zeros off the class blocks):

@@ -52,6 +52,24 @@ def product_model(f):
         sigma_n_num_X=float(f["sigma_n_num_X"]), sigma_n_num_Y=float(f["sigma_n_num_Y"]))
 
 
+def synthetic_model(C, d, D, L, S=3, seed=9):
+    """A small random-hyperparameter GPMDM (C classes x S sequences x L frames), its Markov
+    matrix and the stacked observations Y (host arrays)."""
+    import torch
+    from gpmdm_amd import GPMDM, synthetic
+    data = synthetic.make_sequences(C=C, S=S, L=L, D=D, d=d, seed=seed)
+    rng = np.random.RandomState(seed + 1)
+    N = C * S * L
+    X = rng.randn(N, d)
+    lp = dict(y_log_lengthscales=np.log(rng.uniform(1.0, 2.5, d)), y_log_lambdas=np.log(rng.uniform(0.5, 2, D)),
+              y_log_sigma_n=np.log(0.15), x_log_lengthscales=np.log(rng.uniform(1.0, 2.5, d)),
+              x_log_lambdas=np.log(rng.uniform(0.5, 2, d)), x_log_sigma_n=np.log(0.12),
+              x_log_lin_coeff=np.log(rng.uniform(0.2, 0.8, d + 1)))
+    m = GPMDM.from_arrays(X, data.sequences, **lp)
+    Y = np.concatenate([y for c in data.sequences for y in c]).astype(np.float64)
+    return m, torch.tensor(synthetic.markov_matrix(C)), Y
+
+
 def nrel(a, b):
     """max |a - b| / max |b| (normwise relative error)."""
     a = np.asarray(a, dtype=np.float64)
