@@ -46,7 +46,7 @@ constexpr double kLog2eX64 = 92.33248261689366;   // 64 / ln 2, as in gp_tile.hi
 // the accumulators by MFMA.  Hf[((J kh_n + kh) nw + w) 256 + 4 l + nt] =
 //   H[row = 4 kh + (l >> 4)][col = nb J + 16 (nw nt + w) + (l & 15)].
 struct GpImage {
-  int n_rows = 0, n_m = 0, n_j = 0, n_wc = 0, nw = 4;
+  int n_rows = 0, n_m = 0, n_j = 0, n_wc = 0, nw = 4, coff = 0;
   double* Xs = nullptr;   // n_rows x d, inputs / lengthscales
   double* Xsq = nullptr;  // n_rows
   double* Hf = nullptr;   // dynamics only
@@ -68,9 +68,10 @@ struct GpImage {
     s.n_m = n_m;
     s.n_j = n_j;
     s.n_wc = n_wc;
+    s.coff = coff;
     return s;
   }
-  int n_parts() const { return (int)cdiv(n_rows, 64 * nw); }   // column blocks holding R columns
+  int n_parts() const { return (int)cdiv(n_rows + coff, 64 * nw); }   // blocks holding R columns
 };
 
 int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const double* ls,
@@ -80,7 +81,9 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
   g.n_rows = n_rows;
   g.n_m = n_m;
   g.n_wc = (int)cdiv(n_rows + n_m, kWC);
-  g.n_j = (int)cdiv(n_rows + n_m, nb);
+  g.coff = col_offset(n_rows + n_m, nb);
+  g.n_j = (int)cdiv(n_rows + n_m + g.coff, nb);
+  const int coff = g.coff;
   std::vector<double> xs((size_t)n_rows * d), xsq(n_rows, 0.0);
   for (long long i = 0; i < n_rows; ++i) {
     double s = 0.0;
@@ -96,10 +99,10 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
   TRY(dalloc(&g.Xsq, xsq.size()));
   HIPCHK(hipMemcpy(g.Xsq, xsq.data(), xsq.size() * sizeof(double), hipMemcpyHostToDevice));
   long long total = 0;
-  for (int J = 0; J < g.n_j; ++J) total += (long long)ksteps(block_kmax(J, n_rows, nb)) * fs;
+  for (int J = 0; J < g.n_j; ++J) total += (long long)ksteps(block_kmax(J, n_rows, nb, coff)) * fs;
   TRY(dalloc(&g.Bf, (size_t)total));
   auto val = [&](long long row, long long col) -> double {
-    if (row >= n_rows) return 0.0;
+    if (row >= n_rows || col < 0) return 0.0;
     if (col < n_rows) return row <= col ? R[row * n_rows + col] : 0.0;   // upper triangle of R
     const long long j = col - n_rows;
     return j < n_m ? M[row * n_m + j] : 0.0;
@@ -122,8 +125,8 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
           for (int l = 0; l < 64; ++l)
             for (int nt = 0; nt < 4; ++nt) {
               const int row = 4 * kh + (l >> 4);
-              const long long col = (long long)J * nb + 16 * (nw * nt + w) + (l & 15);
-              if (row <= d && col < n_cols)
+              const long long col = (long long)J * nb + 16 * (nw * nt + w) + (l & 15) - coff;
+              if (row <= d && col >= 0 && col < n_cols)
                 hf[(((size_t)J * kh_n + kh) * nw + w) * 256 + 4 * l + nt] = H[row * n_cols + col];
             }
     TRY(dalloc(&g.Hf, hf.size()));
@@ -132,7 +135,7 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
   long long off = 0;
   std::vector<double> buf;
   for (int J = 0; J < g.n_j; ++J) {
-    const int nks = ksteps(block_kmax(J, n_rows, nb));
+    const int nks = ksteps(block_kmax(J, n_rows, nb, coff));
     buf.assign((size_t)nks * fs, 0.0);
     for (int ks = 0; ks < nks; ++ks)
       for (int w = 0; w < nw; ++w) {
@@ -141,7 +144,7 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
           for (int v = 0; v < 16; ++v) {
             const int kk = v >> 2, nt = v & 3;
             const long long row = (long long)ks * kBK + kk * 4 + (l >> 4);
-            const long long col = (long long)J * nb + 16 * (nw * nt + w) + (l & 15);
+            const long long col = (long long)J * nb + 16 * (nw * nt + w) + (l & 15) - coff;
             dst[(v >> 1) * 128 + 2 * l + (v & 1)] = val(row, col);
           }
       }

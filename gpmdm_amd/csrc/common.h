@@ -31,6 +31,7 @@ struct SegDesc {                  // one GP: the observation GP, or the class-c 
   int n_m;                        // mean columns (D or d)
   int n_j;                        // column blocks of 256
   int n_wc;                       // wave-columns (64 wide) holding real columns
+  int coff;                       // front padding of the column space (see col_offset)
 };
 
 struct TileParams {
@@ -53,10 +54,18 @@ struct TileParams {
 };
 
 // Column-block geometry shared by the host (fragment layout) and the kernel.
-// A block of nw waves spans nb = 64*nw columns; its K range ends at min(n_rows, (J+1)*nb).
-__host__ __device__ inline int block_kmax(int J, int n_rows, int nb) {
-  const int hi = (J + 1) * nb;
+// Columns are [R (n_rows) | M (n_m)].  The column space is padded at the FRONT by coff
+// (a multiple of 16) so that the partial block is block 0, whose triangular K range is a
+// single K-step, instead of a last block that needs every training row for a handful of
+// mean columns.  Block J spans virtual columns [J nb, (J+1) nb) = real columns
+// [J nb - coff, (J+1) nb - coff); its K range ends at min(n_rows, (J+1) nb - coff).
+__host__ __device__ inline int block_kmax(int J, int n_rows, int nb, int coff) {
+  const int hi = (J + 1) * nb - coff;
   return hi < n_rows ? hi : n_rows;
+}
+__host__ __device__ inline int col_offset(int n_cols, int nb) {
+  const int r = n_cols % nb;
+  return r ? ((nb - r) / 16) * 16 : 0;
 }
 __host__ __device__ inline int ksteps(int kmax) { return (kmax + kBK - 1) / kBK; }
 // Dynamics linear kernel: K=4 MFMA sub-steps covering the d+1 rows of H.

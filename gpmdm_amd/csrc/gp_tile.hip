@@ -56,6 +56,74 @@ __constant__ double kExp2Tab[64] = {
     1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951
 };
 
+// 2^(j/256), j = 0..255 (correctly rounded).
+__constant__ double kExp2Tab256[256] = {
+    1.0, 1.0027112750502025, 1.0054299011128027, 1.0081558981184175,
+    1.0108892860517005, 1.0136300849514894, 1.016378314910953, 1.019133996077738,
+    1.0218971486541166, 1.0246677928971357, 1.0274459491187637, 1.030231637686041,
+    1.0330248790212284, 1.0358256936019572, 1.0386341019613787, 1.041450124688316,
+    1.0442737824274138, 1.0471050958792898, 1.0499440858006872, 1.0527907730046264,
+    1.0556451783605572, 1.0585073227945128, 1.061377227289262, 1.0642549128844645,
+    1.0671404006768237, 1.0700337118202419, 1.0729348675259756, 1.075843889062791,
+    1.0787607977571199, 1.0816856149932152, 1.0846183622133092, 1.0875590609177697,
+    1.0905077326652577, 1.0934643990728858, 1.0964290818163769, 1.099401802630222,
+    1.102382583307841, 1.1053714457017412, 1.1083684117236787, 1.1113735033448175,
+    1.1143867425958924, 1.1174081515673693, 1.1204377524096067, 1.12347556733302,
+    1.1265216186082418, 1.129575928566288, 1.1326385195987192, 1.1357094141578055,
+    1.1387886347566916, 1.1418762039695616, 1.1449721444318042, 1.148076478840179,
+    1.1511892299529827, 1.154310420590216, 1.1574400736337511, 1.1605782120274988,
+    1.1637248587775775, 1.1668800369524817, 1.1700437696832502, 1.1732160801636373,
+    1.1763969916502812, 1.1795865274628758, 1.182784710984341, 1.1859915656609938,
+    1.189207115002721, 1.1924313825831512, 1.1956643920398273, 1.1989061670743806,
+    1.202156731452703, 1.2054161090051239, 1.2086843236265816, 1.2119613992768012,
+    1.215247359980469, 1.2185422298274085, 1.2218460329727576, 1.2251587936371455,
+    1.22848053610687, 1.2318112847340759, 1.2351510639369334, 1.2384998981998165,
+    1.241857812073484, 1.245224830175258, 1.2486009771892048, 1.2519862778663162,
+    1.255380757024691, 1.2587844395497165, 1.2621973503942507, 1.2656195145788063,
+    1.2690509571917332, 1.2724917033894028, 1.275941778396392, 1.2794012075056693,
+    1.2828700160787783, 1.2863482295460256, 1.2898358734066657, 1.2933329732290895,
+    1.2968395546510096, 1.3003556433796506, 1.3038812651919358, 1.3074164459346773,
+    1.3109612115247644, 1.3145155879493546, 1.318079601266064, 1.3216532776031575,
+    1.3252366431597413, 1.3288297242059544, 1.3324325470831615, 1.3360451382041458,
+    1.339667524053303, 1.3432997311868353, 1.3469417862329458, 1.3505937158920345,
+    1.3542555469368927, 1.3579273062129011, 1.3616090206382248, 1.365300717204012,
+    1.3690024229745905, 1.3727141650876684, 1.3764359707545302, 1.380167867260238,
+    1.383909881963832, 1.387662042298529, 1.3914243757719262, 1.3951969099662003,
+    1.3989796725383112, 1.4027726912202048, 1.4065759938190154, 1.4103896082172707,
+    1.4142135623730951, 1.4180478843204152, 1.4218926021691656, 1.4257477441054942,
+    1.42961333839197, 1.433489413367789, 1.4373759974489824, 1.4412731191286257,
+    1.4451808069770467, 1.449099089642035, 1.4530279958490526, 1.4569675544014438,
+    1.460917794180647, 1.4648787441464057, 1.4688504333369818, 1.4728328908693675,
+    1.4768261459394993, 1.4808302278224719, 1.4848451658727524, 1.488870989524397,
+    1.4929077282912648, 1.4969554117672355, 1.5010140696264256, 1.5050837316234065,
+    1.5091644275934228, 1.5132561874526098, 1.5173590411982147, 1.5214730189088146,
+    1.5255981507445384, 1.529734466947287, 1.533881997840956, 1.5380407738316568,
+    1.5422108254079407, 1.5463921831410214, 1.550584877685, 1.5547889397770887,
+    1.559004400237837, 1.5632312899713576, 1.567469639965553, 1.5717194812923414,
+    1.5759808451078865, 1.5802537626528246, 1.5845382652524937, 1.588834384317164,
+    1.593142151342267, 1.597461597908627, 1.6017927556826934, 1.606135656416771,
+    1.6104903319492543, 1.6148568142048607, 1.6192351351948637, 1.6236253270173289,
+    1.6280274218573478, 1.632441451987275, 1.6368674497669644, 1.6413054476440063,
+    1.645755478153965, 1.6502175739206177, 1.6546917676561943, 1.6591780921616162,
+    1.6636765803267364, 1.6681872651305825, 1.6727101796415966, 1.6772453570178785,
+    1.681792830507429, 1.6863526334483934, 1.6909247992693053, 1.6955093614893326,
+    1.7001063537185235, 1.7047158096580513, 1.709337763100463, 1.713972247929926,
+    1.718619298122478, 1.723278947746274, 1.7279512309618377, 1.732636182022311,
+    1.7373338352737062, 1.7420442251551564, 1.746767386199169, 1.7515033530318782,
+    1.7562521603732995, 1.761013843037584, 1.7657884359332727, 1.7705759740635547,
+    1.7753764925265212, 1.7801900265154245, 1.785016611318935, 1.789856282321401,
+    1.7947090750031072, 1.7995750249405351, 1.804454167806624, 1.809346539371032,
+    1.8142521755003989, 1.8191711121586085, 1.8241033854070534, 1.8290490314048973,
+    1.8340080864093424, 1.8389805867758937, 1.843966568958626, 1.8489660695104508,
+    1.8539791250833855, 1.8590057724288205, 1.864046048397789, 1.8690999899412386,
+    1.8741676341103, 1.8792490180565602, 1.8843441790323345, 1.8894531543909392,
+    1.8945759815869656, 1.8997126981765553, 1.9048633418176741, 1.9100279502703899,
+    1.9152065613971474, 1.9203992131630474, 1.925605943636125, 1.930826790987627,
+    1.9360617934922943, 1.9413109895286405, 1.9465744175792332, 1.9518521162309783,
+    1.9571441241754002, 1.9624504802089273, 1.9677712232331759, 1.9731063922552343,
+    1.978456026387951, 1.9838201648502194, 1.9891988469672663, 1.9945921121709402
+};
+
 // The kernel value is exp(x), x = -(|a|^2 + |b|^2) + 2 a.b (expansion form of
 // gpmdm.py:508-515).  Every term arrives pre-multiplied by 64/ln2 (particle side in the
 // kernel prologue, |b|^2 on the host), so the fma chain yields t = 64 x / ln2 directly and
@@ -77,6 +145,52 @@ __device__ __forceinline__ double exp2_64(double t, const double* tab) {
   return ldexp(fma(tj, p, tj), ni >> 6);
 }
 
+// exp(x) for t = x 256 / ln 2 <= ~0 (the kernel-value exponent, pre-scaled like exp2_64).
+// Fewer and cheaper VALU ops than exp2_64 (FP64 VALU and FP64 MFMA share the SIMD's issue,
+// tools/microbench/mix_probe.hip): no v_rndne/v_cvt/v_ldexp.
+//   t >= -1022*256 (clamp: below that exp(x) < 2^-1022 and the result is 2^-1022-ish,
+//     negligible next to the unit diagonal instead of an exact 0);
+//   s = t + 1.5*2^52 rounds t to the nearest integer n, whose two's complement sits in the
+//     low word of s; f = t - (s - 1.5*2^52), |f| <= 1/2 (exact);
+//   2^(f/256) - 1 by a degree-4 Taylor polynomial (truncation < 4e-17);
+//   2^(n/256) = table[n & 255] * 2^(n >> 8), the power of two added to the exponent field.
+constexpr double kLog2eX256 = 4.0 * kLog2eX64;      // 256 / ln 2 (exactly 4x: rows arrive x64-scaled)
+constexpr double kExpC1 = 0.0027076061740622863;   // (ln2/256)^k / k!
+constexpr double kExpC2 = 3.6655655969101062e-06;
+constexpr double kExpC3 = 3.3083026805413713e-09;
+constexpr double kExpC4 = 2.239395190875157e-12;
+
+__device__ __forceinline__ double exp2_256(double t, const double* tab) {
+  t = fmax(t, -261632.0);
+  const double s = t + 6755399441055744.0;
+  const int ni = __double2loint(s);
+  const double f = t - (s - 6755399441055744.0);
+  double p = fma(f, kExpC4, kExpC3);
+  p = fma(p, f, kExpC2);
+  p = fma(p, f, kExpC1);
+  p *= f;
+  const double tj = tab[ni & 255];
+  const double r = fma(tj, p, tj);
+  return __hiloint2double(__double2hiint(r) + ((ni >> 8) << 20), __double2loint(r));
+}
+
+// exp2_64 without v_rndne/v_cvt/v_ldexp: the 64-entry table (lanes hitting one entry are
+// LDS broadcasts) with the magic-number rounding and exponent-field insertion of exp2_256.
+__device__ __forceinline__ double exp2_64m(double t, const double* tab) {
+  t = fmax(t, -65408.0);                                    // -1022 * 64
+  const double s = t + 6755399441055744.0;
+  const int ni = __double2loint(s);
+  const double f = t - (s - 6755399441055744.0);
+  double p = fma(f, 1.2417843701716925e-12, 5.732851688640402e-10);
+  p = fma(p, f, 2.1173137155464776e-07);
+  p = fma(p, f, 5.86490495505617e-05);
+  p = fma(p, f, 0.010830424696249145);
+  p *= f;
+  const double tj = tab[ni & 63];
+  const double r = fma(tj, p, tj);
+  return __hiloint2double(__double2hiint(r) + ((ni >> 6) << 20), __double2loint(r));
+}
+
 // VAR: experiment switches for tools/microbench/tile_bench.hip (production uses 0).
 //   bit 0: no tile retirement (every real tile runs to the block's last K-step)
 //   bit 1: ablation -- replace the kernel-value generation by a cheap stand-in
@@ -86,6 +200,8 @@ __device__ __forceinline__ double exp2_64(double t, const double* tab) {
 //   bit 5: ablation -- no B loads (B operands stay in registers)
 //   bit 6: ablation -- no LDS A-fragment reads (A operands from registers)
 //   bit 7: ablation -- every block runs the full K range (no triangular schedule)
+//   bit 8: exp2_256 (256-entry table, no rndne/cvt/ldexp) instead of exp2_64
+//   bit 9: exp2_64m (64-entry table, no rndne/cvt/ldexp)
 template <int DI, bool DYN, int VAR = 0, int NW = 4>
 __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
   constexpr int NT = 64 * NW;                                // threads
@@ -97,7 +213,9 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   constexpr int RPT = (NRV + NT - 1) / NT;                   // row values per thread
   __shared__ double As[2][kBK][kLDA];
   __shared__ double RX[2][kBK][RW];
-  __shared__ double tab[64];
+  constexpr bool E256 = (VAR & 256) != 0;
+  constexpr double kScale = E256 ? kLog2eX256 : kLog2eX64;
+  __shared__ double tab[E256 ? 256 : 64];
   __shared__ double qred[NW][kPT];
 
   const int tid = threadIdx.x;
@@ -121,8 +239,13 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   const int n_rows = prm.seg[c].n_rows;
   const int n_m = prm.seg[c].n_m;
   const int n_cols = n_rows + n_m;
+  const int coff = prm.seg[c].coff;
 
-  if (tid < 64) tab[tid] = kExp2Tab[tid];
+  if constexpr (E256) {
+    for (int i = tid; i < 256; i += NT) tab[i] = kExp2Tab256[i];
+  } else {
+    if (tid < 64) tab[tid] = kExp2Tab[tid];
+  }
 
   const int seg_begin = prm.seg_pos_begin[c];
   const int pos0 = seg_begin + (t - prm.seg_tile_start[c]) * kPT;
@@ -141,12 +264,12 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     const double x = prm.X[(long long)prow * DI + j];
     const double xs = x / prm.ls[j];
     asq = fma(xs, xs, asq);
-    a2[j] = (2.0 * kLog2eX64) * xs;
+    a2[j] = (2.0 * kScale) * xs;
   }
-  asq *= kLog2eX64;                                        // |x / l|^2 (64 / ln 2)
+  asq *= kScale;                                           // |x / l|^2 (64 / ln 2)
 
   // ---- K ranges ------------------------------------------------------------------
-  const int nks = (VAR & 128) ? ksteps(n_rows) : ksteps(block_kmax(J, n_rows, NB));
+  const int nks = (VAR & 128) ? ksteps(n_rows) : ksteps(block_kmax(J, n_rows, NB, coff));
   // this wave's tiles: columns NB*J + 16(NW t + w) .. +15.  T1 = real tiles, kend[t] = the
   // K-step where tile t retires (R tile: past its last column's diagonal; tiles holding
   // mean columns: all rows).  kend is non-decreasing in t.
@@ -154,8 +277,8 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   int kend[4];
 #pragma unroll
   for (int tt = 0; tt < 4; ++tt) {
-    const int c0 = J * NB + 16 * (NW * tt + w);
-    const bool real = c0 < n_cols;
+    const int c0 = J * NB + 16 * (NW * tt + w) - coff;   // front-padding tiles: c0 < 0
+    const bool real = c0 >= 0 && c0 < n_cols;
     if (real) T1 = tt + 1;
     const int hi = c0 + 16;
     int ke = (hi <= n_rows) ? ksteps(hi) : ksteps(n_rows);
@@ -163,7 +286,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     kend[tt] = real ? (ke < nks ? ke : nks) : 0;
   }
   long long boff = 0;                                       // fragments of blocks < J
-  for (int jj = 0; jj < J; ++jj) boff += (long long)ksteps(block_kmax(jj, n_rows, NB)) * FS;
+  for (int jj = 0; jj < J; ++jj) boff += (long long)ksteps(block_kmax(jj, n_rows, NB, coff)) * FS;
   const double* __restrict__ Bw = Bf + boff + w * 1024 + lane * 2;
   // last K-step this wave multiplies (kend is non-decreasing over the real tiles; no
   // runtime indexing of kend[], which would put it in scratch)
@@ -183,7 +306,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
         const int r = idx / RW, f = idx - (idx / RW) * RW;
         int i = ks * kBK + r;
         i = i < last_row ? i : last_row;
-        v = f < DI ? Xs[(long long)i * DI + f] : Xsq[i];
+        v = f < DI ? Xs[(long long)i * DI + f] : (E256 ? 4.0 * Xsq[i] : Xsq[i]);
       }
       rr[k] = v;
     }
@@ -215,6 +338,8 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       }
       double val;
       if constexpr (VAR & 2) val = fma(x, 1e-3, 1.0);
+      else if constexpr (E256) val = exp2_256(x, tab);
+      else if constexpr ((VAR & 512) != 0) val = exp2_64m(x, tab);
       else val = exp2_64(x, tab);
       v[s] = i < n_rows ? val : 0.0;
     }
@@ -377,7 +502,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
 
   // ---- epilogue --------------------------------------------------------------------
   // C/D layout of v_mfma_f64_16x16x4_f64: lane l, reg r -> row (l>>4) + 4r, col l&15.
-  const bool has_r = J * NB < n_rows;
+  const bool has_r = J * NB - coff < n_rows;
   if (has_r) {
     double qs[4][4];
 #pragma unroll
@@ -388,7 +513,8 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
           const double x = acc[mt][nt][r];
-          if (J * NB + 16 * (NW * nt + w) + li < n_rows) s = fma(x, x, s);
+          const int col = J * NB + 16 * (NW * nt + w) + li - coff;
+          if (col >= 0 && col < n_rows) s = fma(x, x, s);
         }
         s += __shfl_xor(s, 1);
         s += __shfl_xor(s, 2);
@@ -403,10 +529,10 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
         for (int r = 0; r < 4; ++r) qred[w][mt * 16 + lk + 4 * r] = qs[mt][r];
     }
   }
-  if ((J + 1) * NB > n_rows) {                                // mean columns
+  if ((J + 1) * NB - coff > n_rows) {                         // mean columns
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
-      const int jm = J * NB + 16 * (NW * nt + w) + li - n_rows;
+      const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
       if (jm >= 0 && jm < n_m) {
 #pragma unroll
         for (int mt = 0; mt < 4; ++mt)

@@ -45,9 +45,10 @@ int main(int argc, char** argv) {
   TileParams pp[2];
   for (int v = 0; v < 2; ++v) {
     const int nw = v == 0 ? 4 : 8, nb = 64 * nw;
-    const int n_j = (N + D + nb - 1) / nb;
+    const int coff = getenv("TB_NO_COFF") ? 0 : col_offset(N + D, nb);
+    const int n_j = (N + D + coff + nb - 1) / nb;
     long long total = 0;
-    for (int J = 0; J < n_j; ++J) total += (long long)ksteps(block_kmax(J, N, nb)) * nw * 1024;
+    for (int J = 0; J < n_j; ++J) total += (long long)ksteps(block_kmax(J, N, nb, coff)) * nw * 1024;
     std::vector<double> hB(total);
     for (auto& x : hB) x = 0.01 * nd(rng);
     double* B;
@@ -56,7 +57,7 @@ int main(int argc, char** argv) {
     TileParams& p = pp[v];
     p = TileParams{};
     p.seg[0].Xs = Xs; p.seg[0].Xsq = Xsq; p.seg[0].Bf = B;
-    p.seg[0].n_rows = N; p.seg[0].n_m = D; p.seg[0].n_j = n_j; p.seg[0].n_wc = (N + D + 63) / 64;
+    p.seg[0].n_rows = N; p.seg[0].n_m = D; p.seg[0].n_j = n_j; p.seg[0].n_wc = (N + D + 63) / 64; p.seg[0].coff = coff;
     p.n_seg = 1; p.tiles_ub = ntiles; p.n_j_max = n_j; p.nw = nw;
     p.seg_pos_begin = tab; p.seg_pos_end = tab + 1; p.seg_out_base = tab + 2; p.seg_tile_start = tab + 3;
     p.X = X;
@@ -69,9 +70,9 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   typedef void (*L)(const TileParams&, hipStream_t);
   struct V { L fn; int pi; const char* name; };
-  V vars[] = {{launch_var<0, 4>, 0, "NW4 production"}, {launch_var<0, 8>, 1, "NW8 production"},
-              {launch_var<16, 4>, 0, "NW4 no gen"}, {launch_var<16, 8>, 1, "NW8 no gen"},
-              {launch_var<8, 8>, 1, "NW8 no barrier (ablation)"}};
+  V vars[] = {{launch_var<0, 4>, 0, "NW4 production"}, {launch_var<256, 4>, 0, "NW4 exp2_256"},
+              {launch_var<16, 4>, 0, "NW4 no gen"}, {launch_var<512, 4>, 0, "NW4 exp2_64m"},
+              {launch_var<2, 4>, 0, "NW4 cheap stand-in exp"}};
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
   std::vector<std::vector<float>> t(NV);
   for (int v = 0; v < NV; ++v) vars[v].fn(pp[vars[v].pi], s);
