@@ -70,9 +70,9 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   typedef void (*L)(const TileParams&, hipStream_t);
   struct V { L fn; int pi; const char* name; };
-  V vars[] = {{launch_var<0, 4>, 0, "NW4 production"}, {launch_var<256, 4>, 0, "NW4 exp2_256"},
-              {launch_var<16, 4>, 0, "NW4 no gen"}, {launch_var<512, 4>, 0, "NW4 exp2_64m"},
-              {launch_var<2, 4>, 0, "NW4 cheap stand-in exp"}};
+  V vars[] = {{launch_var<0, 4>, 0, "NW4 production"}, {launch_var<0, 8>, 1, "NW8 production"},
+              {launch_var<16, 4>, 0, "NW4 no gen"}, {launch_var<16, 8>, 1, "NW8 no gen"},
+              {launch_var<2, 8>, 1, "NW8 cheap stand-in exp"}};
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
   std::vector<std::vector<float>> t(NV);
   for (int v = 0; v < NV; ++v) vars[v].fn(pp[vars[v].pi], s);
