@@ -25,7 +25,7 @@ _i64p = POINTER(c_int64)
 
 class ModelDesc(ctypes.Structure):
     _fields_ = [
-        ("N", c_int64), ("D", c_int32), ("d", c_int32), ("C", c_int32), ("tile_waves", c_int32),
+        ("N", c_int64), ("D", c_int32), ("d", c_int32), ("C", c_int32), ("tile_shape", c_int32),
         ("X", _dp), ("obs_R", _dp), ("obs_beta", _dp),
         ("y_lengthscales", _dp), ("y_inv_lambda2", _dp),
         ("Nc", _i64p), ("Xin", POINTER(_dp)), ("dyn_R", POINTER(_dp)), ("dyn_alpha", POINTER(_dp)),

@@ -32,21 +32,23 @@ constexpr double kLog2eX64 = 92.33248261689366;   // 64 / ln 2, as in gp_tile.hi
 // One GP's device image: scaled inputs (+ squared norms), raw inputs, and B = [R | M] in
 // MFMA-fragment order.
 //
-// Fragment layout (consumed by gp_tile.hip): column block J (nb = 64*nw columns) stores
-// ksteps(block_kmax(J)) K-steps; each K-step holds nw waves x 1024 doubles, and inside a
-// wave's 1024 doubles the value v = 2q + e of lane l sits at q*128 + 2l + e, where
-// v = kk*4 + nt is the B operand of MFMA sub-step kk (K=4) for column tile nt of wave w,
+// Fragment layout (consumed by gp_tile.hip), for a tile shape (nw waves, each owning ntw
+// column tiles of 16; nb = 16 ntw nw columns per block): column block J stores
+// ksteps(block_kmax(J)) K-steps; each K-step holds nw waves x 256 ntw doubles, and inside a
+// wave's share the value v = 2q + e of lane l sits at q*128 + 2l + e, where
+// v = kk*ntw + nt is the B operand of MFMA sub-step kk (K=4) for column tile nt of wave w,
 // whose 16 columns are interleaved with the other waves' tiles:
 //   B[row = 16 ks + 4 kk + (l >> 4)][col = nb J + 16 (nw nt + w) + (l & 15)].
-// A lane's 16 values are therefore 8 x 16-byte loads, each wave-instruction reading one
+// A lane's 4 ntw values are therefore 16-byte loads, each wave-instruction reading one
 // contiguous 1 KiB.  Rows below the diagonal of R are never stored (triangular skip).
 //
 // Dynamics images also carry H = (X~ C^2)^T B ((d+1) x cols, X~ = [Xin, 1], C^2 the linear
 // kernel's coefficients, gpmdm.py:493-506): the linear kernel's share of K* B, seeded into
-// the accumulators by MFMA.  Hf[((J kh_n + kh) nw + w) 256 + 4 l + nt] =
+// the accumulators by MFMA.  Hf[((J kh_n + kh) nw + w) 64 ntw + ntw l + nt] =
 //   H[row = 4 kh + (l >> 4)][col = nb J + 16 (nw nt + w) + (l & 15)].
 struct GpImage {
-  int n_rows = 0, n_m = 0, n_j = 0, n_wc = 0, nw = 4, coff = 0;
+  int n_rows = 0, n_m = 0, n_j = 0, coff = 0;
+  TileGeo geo = kGeo64x256;
   double* Xs = nullptr;   // n_rows x d, inputs / lengthscales
   double* Xsq = nullptr;  // n_rows
   double* Hf = nullptr;   // dynamics only
@@ -67,20 +69,19 @@ struct GpImage {
     s.n_rows = n_rows;
     s.n_m = n_m;
     s.n_j = n_j;
-    s.n_wc = n_wc;
     s.coff = coff;
     return s;
   }
-  int n_parts() const { return (int)cdiv(n_rows + coff, 64 * nw); }   // blocks holding R columns
+  int n_parts() const { return (int)cdiv(n_rows + coff, geo.nb()); }   // blocks holding R columns
+  int tiles(long long n) const { return (int)cdiv(n, geo.pt()); }
 };
 
 int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const double* ls,
-                const double* lin_c2, const double* R, const double* M, int nw) {
-  const int nb = 64 * nw, fs = nw * 1024;
-  g.nw = nw;
+                const double* lin_c2, const double* R, const double* M, TileGeo geo) {
+  const int nw = geo.nw, ntw = geo.ntw, nb = geo.nb(), fs = geo.fs(), ws = 256 * ntw;
+  g.geo = geo;
   g.n_rows = n_rows;
   g.n_m = n_m;
-  g.n_wc = (int)cdiv(n_rows + n_m, kWC);
   g.coff = col_offset(n_rows + n_m, nb);
   g.n_j = (int)cdiv(n_rows + n_m + g.coff, nb);
   const int coff = g.coff;
@@ -118,16 +119,16 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
         H[(size_t)d * n_cols + col] += lin_c2[d] * b;
       }
     const int kh_n = lin_substeps(d);
-    std::vector<double> hf((size_t)g.n_j * kh_n * nw * 256, 0.0);
+    std::vector<double> hf((size_t)g.n_j * kh_n * nw * 64 * ntw, 0.0);
     for (int J = 0; J < g.n_j; ++J)
       for (int kh = 0; kh < kh_n; ++kh)
         for (int w = 0; w < nw; ++w)
           for (int l = 0; l < 64; ++l)
-            for (int nt = 0; nt < 4; ++nt) {
+            for (int nt = 0; nt < ntw; ++nt) {
               const int row = 4 * kh + (l >> 4);
               const long long col = (long long)J * nb + 16 * (nw * nt + w) + (l & 15) - coff;
               if (row <= d && col >= 0 && col < n_cols)
-                hf[(((size_t)J * kh_n + kh) * nw + w) * 256 + 4 * l + nt] = H[row * n_cols + col];
+                hf[(((size_t)J * kh_n + kh) * nw + w) * 64 * ntw + ntw * l + nt] = H[row * n_cols + col];
             }
     TRY(dalloc(&g.Hf, hf.size()));
     HIPCHK(hipMemcpy(g.Hf, hf.data(), hf.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -139,10 +140,10 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
     buf.assign((size_t)nks * fs, 0.0);
     for (int ks = 0; ks < nks; ++ks)
       for (int w = 0; w < nw; ++w) {
-        double* dst = buf.data() + ((size_t)ks * nw + w) * 1024;
+        double* dst = buf.data() + ((size_t)ks * nw + w) * ws;
         for (int l = 0; l < 64; ++l)
-          for (int v = 0; v < 16; ++v) {
-            const int kk = v >> 2, nt = v & 3;
+          for (int v = 0; v < 4 * ntw; ++v) {
+            const int kk = v / ntw, nt = v % ntw;
             const long long row = (long long)ks * kBK + kk * 4 + (l >> 4);
             const long long col = (long long)J * nb + 16 * (nw * nt + w) + (l & 15) - coff;
             dst[(v >> 1) * 128 + 2 * l + (v & 1)] = val(row, col);
@@ -290,10 +291,20 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
   m->x_ls.assign(desc->x_lengthscales, desc->x_lengthscales + d);
   m->x_lin_c2.assign(desc->x_lin_coeff2, desc->x_lin_coeff2 + d + 1);
   m->x_il2.assign(desc->x_inv_lambda2, desc->x_inv_lambda2 + d);
-  const int nw = desc->tile_waves == 0 ? kDefaultNW : desc->tile_waves;
-  if (nw != 4 && nw != 8) { delete m; return fail(GPMDM_E_INVALID, "tile_waves must be 0, 4 or 8"); }
+  // tile shapes: the observation GP defaults to 32x512 (half the kernel-value generation per
+  // MFMA of 64x256, tools/microbench/tile_bench.hip); the dynamics GPs use 64-particle tiles
+  // (their class-grouped tile starts are computed on the device in 64s, pf_kernels.hip)
+  // (above d = 12 the 32x512 shape's registers spill: 64x256 there)
+  TileGeo obs_geo = d <= 12 ? kGeo32x512 : kGeo64x256, dyn_geo = kGeo64x256;
+  switch (desc->tile_shape) {
+    case GPMDM_TILE_DEFAULT: break;
+    case GPMDM_TILE_64x256: obs_geo = kGeo64x256; break;
+    case GPMDM_TILE_64x512: obs_geo = dyn_geo = kGeo64x512; break;
+    case GPMDM_TILE_32x512: obs_geo = kGeo32x512; break;
+    default: delete m; return fail(GPMDM_E_INVALID, "tile_shape must be one of GPMDM_TILE_*");
+  }
   int rc = build_image(m->obs, (int)m->N, d, m->D, desc->X, desc->y_lengthscales, nullptr,
-                       desc->obs_R, desc->obs_beta, nw);
+                       desc->obs_R, desc->obs_beta, obs_geo);
   if (rc) { delete m; return rc; }
   m->dyn.resize(m->C);
   for (int c = 0; c < m->C; ++c) {
@@ -303,7 +314,7 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
     }
     rc = build_image(m->dyn[c], (int)desc->Nc[c], d, d, desc->Xin[c], desc->x_lengthscales,
                      m->x_lin_c2.data(),
-                     desc->dyn_R[c], desc->dyn_alpha[c], nw);
+                     desc->dyn_R[c], desc->dyn_alpha[c], dyn_geo);
     if (rc) { delete m; return rc; }
   }
   rc = dalloc(&m->y_il2_dev, m->D);
@@ -338,13 +349,13 @@ int gpmdm_predict_obs(gpmdm_model_t m, const double* Xs, int64_t n, double* mu, 
   HIPCHK(hipSetDevice(m->device));
   const int nparts = m->obs.n_parts();
   TRY(m->ensure_q((size_t)nparts * n));
-  const int tab[5] = {0, (int)n, 0, 0, (int)cdiv(n, kPT)};
+  const int tab[5] = {0, (int)n, 0, 0, m->obs.tiles(n)};
   HIPCHK(hipMemcpyAsync(m->tab, tab, sizeof(tab), hipMemcpyHostToDevice, s));
   TileParams tp{};
   tp.seg[0] = m->obs.seg();
   tp.n_seg = 1;
-  tp.nw = m->obs.nw;
-  tp.tiles_ub = (int)cdiv(n, kPT);
+  tp.geo = m->obs.geo;
+  tp.tiles_ub = m->obs.tiles(n);
   tp.n_j_max = m->obs.n_j;
   tp.seg_pos_begin = m->tab + 0;
   tp.seg_pos_end = m->tab + 1;
@@ -384,13 +395,13 @@ int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, doubl
   const GpImage& g = m->dyn[c];
   const int nparts = g.n_parts();
   TRY(m->ensure_q((size_t)nparts * n));
-  const int tab[5] = {0, (int)n, 0, 0, (int)cdiv(n, kPT)};
+  const int tab[5] = {0, (int)n, 0, 0, g.tiles(n)};
   HIPCHK(hipMemcpyAsync(m->tab, tab, sizeof(tab), hipMemcpyHostToDevice, s));
   TileParams tp{};
   tp.seg[0] = g.seg();
   tp.n_seg = 1;
-  tp.nw = g.nw;
-  tp.tiles_ub = (int)cdiv(n, kPT);
+  tp.geo = g.geo;
+  tp.tiles_ub = g.tiles(n);
   tp.n_j_max = g.n_j;
   tp.seg_pos_begin = m->tab + 0;
   tp.seg_pos_end = m->tab + 1;
@@ -496,7 +507,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   ALLOC(partials, F * pf->nbf * (C + 1 + d));
   ALLOC(readout, F * (C + d + 1));
 #undef ALLOC
-  const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, kPT)};
+  const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, m->obs.tiles(pf->nloc)};
   if (hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(pf->T, T, sizeof(double) * C * C, hipMemcpyHostToDevice) != hipSuccess) {
     delete pf;
@@ -723,7 +734,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
         njm = std::max(njm, m->dyn[c0 + k].n_j);
       }
       tp.n_seg = ns;
-      tp.nw = m->dyn[c0].nw;
+      tp.geo = m->dyn[c0].geo;           // 64-particle tiles (device-side tile starts)
       tp.tiles_ub = (int)(cdiv(nl, kPT) + ns);
       tp.n_j_max = njm;
       if (pf->dedup) {                  // one row per (ancestor, class) leader
@@ -783,8 +794,8 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     TileParams tp{};
     tp.seg[0] = m->obs.seg();
     tp.n_seg = 1;
-    tp.nw = m->obs.nw;
-    tp.tiles_ub = (int)cdiv(nl, kPT);
+    tp.geo = m->obs.geo;
+    tp.tiles_ub = m->obs.tiles(nl);
     tp.n_j_max = m->obs.n_j;
     tp.seg_pos_begin = pf->obs_tab + 0;
     tp.seg_pos_end = pf->obs_tab + 1;

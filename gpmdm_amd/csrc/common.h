@@ -10,17 +10,27 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------------
 // Fused GP tile geometry (see gp_tile.hip and DESIGN.md §3).
-//   one workgroup = NW waves = 64 particles x 64*NW columns of V = K* . B, where K*
+//   one workgroup = NW waves = 16 MT particles x 16 NTW NW columns of V = K* . B, where K*
 //   (particles x training rows) is generated on the fly and B = [R | M] is the extended
-//   weight matrix stored in MFMA-fragment order (each wave owns 4 tiles of 16 columns).
+//   weight matrix stored in MFMA-fragment order (each wave owns MT x NTW tiles of 16 x 16).
+//   Shapes: 64x256 (NW 4, MT 4, NTW 4; the dynamics GPs), 64x512 (8, 4, 4) and 32x512
+//   (4, 2, 8; the observation GP default).
 // ---------------------------------------------------------------------------------
-constexpr int kPT = 64;           // particles per tile (MFMA M)
-constexpr int kWC = 64;           // columns per wave
+constexpr int kPT = 64;           // particles per tile of the 64-row shapes (dynamics GPs)
 constexpr int kBK = 16;           // training rows per K-step (4 x K=4 MFMA sub-steps)
-constexpr int kLDA = kPT + 16;    // LDS row stride (doubles): rows k, k+1 land 32 banks apart
-constexpr int kDefaultNW = 4;     // waves per workgroup unless the model asks otherwise
 constexpr int kMaxSeg = 8;        // segments (classes) per launch
 constexpr int kMaxD = 32;         // latent dimension limit
+
+// Tile shapes selectable per model (gpmdm_model_desc.tile_shape).
+struct TileGeo {
+  int nw, mt, ntw;
+  __host__ __device__ int pt() const { return 16 * mt; }          // particles per tile
+  __host__ __device__ int nb() const { return 16 * ntw * nw; }    // columns per block
+  __host__ __device__ int fs() const { return nw * 256 * ntw; }   // fragment doubles per K-step
+};
+constexpr TileGeo kGeo64x256{4, 4, 4};
+constexpr TileGeo kGeo64x512{8, 4, 4};
+constexpr TileGeo kGeo32x512{4, 2, 8};
 
 struct SegDesc {                  // one GP: the observation GP, or the class-c dynamics GP
   const double* Xs;               // n_rows x d : training inputs / lengthscales
@@ -29,8 +39,7 @@ struct SegDesc {                  // one GP: the observation GP, or the class-c 
   const double* Bf;               // B = [triu(R) | M] in fragment order (see capi.hip)
   int n_rows;                     // training rows = R columns
   int n_m;                        // mean columns (D or d)
-  int n_j;                        // column blocks of 256
-  int n_wc;                       // wave-columns (64 wide) holding real columns
+  int n_j;                        // column blocks
   int coff;                       // front padding of the column space (see col_offset)
 };
 
@@ -39,7 +48,7 @@ struct TileParams {
   int n_seg;
   int tiles_ub;                   // grid = n_j_max * tiles_ub workgroups
   int n_j_max;
-  int nw;                         // waves per workgroup (4 or 8): fragment layout of B
+  TileGeo geo;                    // tile shape: fragment layout of B, particles per tile
   const int* seg_pos_begin;       // [n_seg]   first position (device)
   const int* seg_pos_end;         // [n_seg]
   const int* seg_out_base;        // [n_seg]   output row of the first position

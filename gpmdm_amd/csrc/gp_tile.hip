@@ -1,578 +1,11 @@
-// Fused GP predictive tile for gfx950: kernel-row generation + FP64 MFMA contraction.
-//
-// Replaces, for a tile of 64 particles x 256 columns:
-//   observation GP  (gpmdm.py:955-959)  Ky* = exp(-|x*-X|^2/l^2),
-//                   mean = Ky*^T beta, var-quadratic form = Ky*^T Ky^-1 Ky*
-//   dynamics GP     (gpmdm.py:1061-1065) Kx* = RBF + linear kernel over the class-c rows,
-//                   mean = Kx*^T alpha_c, quadratic form = Kx*^T A_c Kx*
-// The linear kernel (gpmdm.py:493-506) is rank d+1: k_lin(p, i) = x~_p^T C^2 x~_i with
-// x~ = [x, 1], so its contribution to V = K* B is x~_p^T H with H = (X~ C^2)^T B, a
-// (d+1)-row matrix precomputed on the host.  It is added to the accumulators after the K
-// loop by ceil((d+1)/4) extra MFMA sub-steps, and the K loop generates only the RBF part
-// (the same code as the observation GP).
-// With K^-1 = R R^T (R = U^-1 from the reference's own Cholesky recipe, gpmdm.py:1286-1289)
-// the quadratic form is |R^T k|^2.  R is upper triangular, so column block J only needs
-// training rows [0, (J+1)*256), and each wave stops at its own 64 columns: about half the
-// dense FLOPs.  B = [R | M] carries the mean weights M (beta or alpha_c) as extra columns,
-// so one pass produces both.
-//
-// Workgroup = 4 waves; wave w owns the four 16-column tiles at columns
-// 256J + 16(4t + w), t = 0..3 (interleaved, so all waves reach nearly the same K), for all
-// 64 particles (4 x 4 tiles of v_mfma_f64_16x16x4_f64, 128 accumulator VGPRs).  A tile of R
-// columns retires once K passes its diagonal: the K loop runs in phases with tiles
-// [T0, T1) active, so no MFMA multiplies the zero triangle and no wave idles while its
-// siblings (and the barrier) wait.  Per K-step of 16 training rows:
-//   * K* tile (64 x 16) generated once per workgroup: each thread makes 4 values
-//     (expansion-form distance as gpmdm.py:508-515, table-driven fp64 exp), stored to a
-//     double-buffered LDS image that all 4 waves read as A fragments;
-//   * B fragments stream from HBM/L2 straight into VGPRs (8 x 16 B per lane, one K-step
-//     ahead): B is stored in fragment order, so no LDS round trip and no re-layout;
-//   * one barrier per K-step.  Two workgroups per CU overlap each other's barriers.
-// Workgroups are ordered heavy-first (column block J descending), which both balances the
-// triangular work and makes concurrent workgroups share a B panel in each XCD's L2.
-#include <type_traits>
-
+// Dispatch of the fused GP tile kernel (gp_tile.h) on the latent dimension.  The kernels
+// are instantiated in gp_tile_d*.hip.
 #include "common.h"
 
 namespace gpmdm {
 
-// 2^(j/64), j = 0..63 (correctly rounded).
-__constant__ double kExp2Tab[64] = {
-    1.0, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
-    1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
-    1.0905077326652577, 1.102382583307841, 1.1143867425958924, 1.1265216186082418,
-    1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
-    1.189207115002721, 1.202156731452703, 1.215247359980469, 1.22848053610687,
-    1.241857812073484, 1.255380757024691, 1.2690509571917332, 1.2828700160787783,
-    1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.339667524053303,
-    1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
-    1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
-    1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
-    1.5422108254079407, 1.559004400237837, 1.5759808451078865, 1.593142151342267,
-    1.6104903319492543, 1.6280274218573478, 1.645755478153965, 1.6636765803267364,
-    1.681792830507429, 1.7001063537185235, 1.718619298122478, 1.7373338352737062,
-    1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
-    1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
-    1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951
-};
-
-// 2^(j/256), j = 0..255 (correctly rounded).
-__constant__ double kExp2Tab256[256] = {
-    1.0, 1.0027112750502025, 1.0054299011128027, 1.0081558981184175,
-    1.0108892860517005, 1.0136300849514894, 1.016378314910953, 1.019133996077738,
-    1.0218971486541166, 1.0246677928971357, 1.0274459491187637, 1.030231637686041,
-    1.0330248790212284, 1.0358256936019572, 1.0386341019613787, 1.041450124688316,
-    1.0442737824274138, 1.0471050958792898, 1.0499440858006872, 1.0527907730046264,
-    1.0556451783605572, 1.0585073227945128, 1.061377227289262, 1.0642549128844645,
-    1.0671404006768237, 1.0700337118202419, 1.0729348675259756, 1.075843889062791,
-    1.0787607977571199, 1.0816856149932152, 1.0846183622133092, 1.0875590609177697,
-    1.0905077326652577, 1.0934643990728858, 1.0964290818163769, 1.099401802630222,
-    1.102382583307841, 1.1053714457017412, 1.1083684117236787, 1.1113735033448175,
-    1.1143867425958924, 1.1174081515673693, 1.1204377524096067, 1.12347556733302,
-    1.1265216186082418, 1.129575928566288, 1.1326385195987192, 1.1357094141578055,
-    1.1387886347566916, 1.1418762039695616, 1.1449721444318042, 1.148076478840179,
-    1.1511892299529827, 1.154310420590216, 1.1574400736337511, 1.1605782120274988,
-    1.1637248587775775, 1.1668800369524817, 1.1700437696832502, 1.1732160801636373,
-    1.1763969916502812, 1.1795865274628758, 1.182784710984341, 1.1859915656609938,
-    1.189207115002721, 1.1924313825831512, 1.1956643920398273, 1.1989061670743806,
-    1.202156731452703, 1.2054161090051239, 1.2086843236265816, 1.2119613992768012,
-    1.215247359980469, 1.2185422298274085, 1.2218460329727576, 1.2251587936371455,
-    1.22848053610687, 1.2318112847340759, 1.2351510639369334, 1.2384998981998165,
-    1.241857812073484, 1.245224830175258, 1.2486009771892048, 1.2519862778663162,
-    1.255380757024691, 1.2587844395497165, 1.2621973503942507, 1.2656195145788063,
-    1.2690509571917332, 1.2724917033894028, 1.275941778396392, 1.2794012075056693,
-    1.2828700160787783, 1.2863482295460256, 1.2898358734066657, 1.2933329732290895,
-    1.2968395546510096, 1.3003556433796506, 1.3038812651919358, 1.3074164459346773,
-    1.3109612115247644, 1.3145155879493546, 1.318079601266064, 1.3216532776031575,
-    1.3252366431597413, 1.3288297242059544, 1.3324325470831615, 1.3360451382041458,
-    1.339667524053303, 1.3432997311868353, 1.3469417862329458, 1.3505937158920345,
-    1.3542555469368927, 1.3579273062129011, 1.3616090206382248, 1.365300717204012,
-    1.3690024229745905, 1.3727141650876684, 1.3764359707545302, 1.380167867260238,
-    1.383909881963832, 1.387662042298529, 1.3914243757719262, 1.3951969099662003,
-    1.3989796725383112, 1.4027726912202048, 1.4065759938190154, 1.4103896082172707,
-    1.4142135623730951, 1.4180478843204152, 1.4218926021691656, 1.4257477441054942,
-    1.42961333839197, 1.433489413367789, 1.4373759974489824, 1.4412731191286257,
-    1.4451808069770467, 1.449099089642035, 1.4530279958490526, 1.4569675544014438,
-    1.460917794180647, 1.4648787441464057, 1.4688504333369818, 1.4728328908693675,
-    1.4768261459394993, 1.4808302278224719, 1.4848451658727524, 1.488870989524397,
-    1.4929077282912648, 1.4969554117672355, 1.5010140696264256, 1.5050837316234065,
-    1.5091644275934228, 1.5132561874526098, 1.5173590411982147, 1.5214730189088146,
-    1.5255981507445384, 1.529734466947287, 1.533881997840956, 1.5380407738316568,
-    1.5422108254079407, 1.5463921831410214, 1.550584877685, 1.5547889397770887,
-    1.559004400237837, 1.5632312899713576, 1.567469639965553, 1.5717194812923414,
-    1.5759808451078865, 1.5802537626528246, 1.5845382652524937, 1.588834384317164,
-    1.593142151342267, 1.597461597908627, 1.6017927556826934, 1.606135656416771,
-    1.6104903319492543, 1.6148568142048607, 1.6192351351948637, 1.6236253270173289,
-    1.6280274218573478, 1.632441451987275, 1.6368674497669644, 1.6413054476440063,
-    1.645755478153965, 1.6502175739206177, 1.6546917676561943, 1.6591780921616162,
-    1.6636765803267364, 1.6681872651305825, 1.6727101796415966, 1.6772453570178785,
-    1.681792830507429, 1.6863526334483934, 1.6909247992693053, 1.6955093614893326,
-    1.7001063537185235, 1.7047158096580513, 1.709337763100463, 1.713972247929926,
-    1.718619298122478, 1.723278947746274, 1.7279512309618377, 1.732636182022311,
-    1.7373338352737062, 1.7420442251551564, 1.746767386199169, 1.7515033530318782,
-    1.7562521603732995, 1.761013843037584, 1.7657884359332727, 1.7705759740635547,
-    1.7753764925265212, 1.7801900265154245, 1.785016611318935, 1.789856282321401,
-    1.7947090750031072, 1.7995750249405351, 1.804454167806624, 1.809346539371032,
-    1.8142521755003989, 1.8191711121586085, 1.8241033854070534, 1.8290490314048973,
-    1.8340080864093424, 1.8389805867758937, 1.843966568958626, 1.8489660695104508,
-    1.8539791250833855, 1.8590057724288205, 1.864046048397789, 1.8690999899412386,
-    1.8741676341103, 1.8792490180565602, 1.8843441790323345, 1.8894531543909392,
-    1.8945759815869656, 1.8997126981765553, 1.9048633418176741, 1.9100279502703899,
-    1.9152065613971474, 1.9203992131630474, 1.925605943636125, 1.930826790987627,
-    1.9360617934922943, 1.9413109895286405, 1.9465744175792332, 1.9518521162309783,
-    1.9571441241754002, 1.9624504802089273, 1.9677712232331759, 1.9731063922552343,
-    1.978456026387951, 1.9838201648502194, 1.9891988469672663, 1.9945921121709402
-};
-
-// The kernel value is exp(x), x = -(|a|^2 + |b|^2) + 2 a.b (expansion form of
-// gpmdm.py:508-515).  Every term arrives pre-multiplied by 64/ln2 (particle side in the
-// kernel prologue, |b|^2 on the host), so the fma chain yields t = 64 x / ln2 directly and
-// exp(x) = 2^(t/64): n = rint(t), f = t - n (exact, Sterbenz), 2^(f/64) - 1 by a degree-5
-// polynomial in f (|f| <= 1/2, truncation < 2^-55), table 2^(j/64), ldexp.  No clamp is
-// needed: v_cvt_i32_f64 saturates and ldexp underflows to 0 exactly like exp().
-constexpr double kLog2eX64 = 92.33248261689366;   // 64 / ln 2 (host and device)
-
-__device__ __forceinline__ double exp2_64(double t, const double* tab) {
-  const double n = __builtin_rint(t);
-  const double f = t - n;
-  double p = fma(f, 1.2417843701716925e-12, 5.732851688640402e-10);
-  p = fma(p, f, 2.1173137155464776e-07);
-  p = fma(p, f, 5.86490495505617e-05);
-  p = fma(p, f, 0.010830424696249145);
-  p *= f;                                                          // 2^(f/64) - 1
-  const int ni = (int)n;
-  const double tj = tab[ni & 63];
-  return ldexp(fma(tj, p, tj), ni >> 6);
-}
-
-// exp(x) for t = x 256 / ln 2 <= ~0 (the kernel-value exponent, pre-scaled like exp2_64).
-// Fewer and cheaper VALU ops than exp2_64 (FP64 VALU and FP64 MFMA share the SIMD's issue,
-// tools/microbench/mix_probe.hip): no v_rndne/v_cvt/v_ldexp.
-//   t >= -1022*256 (clamp: below that exp(x) < 2^-1022 and the result is 2^-1022-ish,
-//     negligible next to the unit diagonal instead of an exact 0);
-//   s = t + 1.5*2^52 rounds t to the nearest integer n, whose two's complement sits in the
-//     low word of s; f = t - (s - 1.5*2^52), |f| <= 1/2 (exact);
-//   2^(f/256) - 1 by a degree-4 Taylor polynomial (truncation < 4e-17);
-//   2^(n/256) = table[n & 255] * 2^(n >> 8), the power of two added to the exponent field.
-constexpr double kLog2eX256 = 4.0 * kLog2eX64;      // 256 / ln 2 (exactly 4x: rows arrive x64-scaled)
-constexpr double kExpC1 = 0.0027076061740622863;   // (ln2/256)^k / k!
-constexpr double kExpC2 = 3.6655655969101062e-06;
-constexpr double kExpC3 = 3.3083026805413713e-09;
-constexpr double kExpC4 = 2.239395190875157e-12;
-
-__device__ __forceinline__ double exp2_256(double t, const double* tab) {
-  t = fmax(t, -261632.0);
-  const double s = t + 6755399441055744.0;
-  const int ni = __double2loint(s);
-  const double f = t - (s - 6755399441055744.0);
-  double p = fma(f, kExpC4, kExpC3);
-  p = fma(p, f, kExpC2);
-  p = fma(p, f, kExpC1);
-  p *= f;
-  const double tj = tab[ni & 255];
-  const double r = fma(tj, p, tj);
-  return __hiloint2double(__double2hiint(r) + ((ni >> 8) << 20), __double2loint(r));
-}
-
-// exp2_64 without v_rndne/v_cvt/v_ldexp: the 64-entry table (lanes hitting one entry are
-// LDS broadcasts) with the magic-number rounding and exponent-field insertion of exp2_256.
-__device__ __forceinline__ double exp2_64m(double t, const double* tab) {
-  t = fmax(t, -65408.0);                                    // -1022 * 64
-  const double s = t + 6755399441055744.0;
-  const int ni = __double2loint(s);
-  const double f = t - (s - 6755399441055744.0);
-  double p = fma(f, 1.2417843701716925e-12, 5.732851688640402e-10);
-  p = fma(p, f, 2.1173137155464776e-07);
-  p = fma(p, f, 5.86490495505617e-05);
-  p = fma(p, f, 0.010830424696249145);
-  p *= f;
-  const double tj = tab[ni & 63];
-  const double r = fma(tj, p, tj);
-  return __hiloint2double(__double2hiint(r) + ((ni >> 6) << 20), __double2loint(r));
-}
-
-// VAR: experiment switches for tools/microbench/tile_bench.hip (production uses 0).
-//   bit 0: no tile retirement (every real tile runs to the block's last K-step)
-//   bit 1: ablation -- replace the kernel-value generation by a cheap stand-in
-//   bit 2: ablation -- generation reads no training rows (constant row)
-//   bit 3: ablation -- no barrier in the K loop (wrong results; timing only)
-//   bit 4: ablation -- no generation and no A stores at all (MFMA + B stream bound)
-//   bit 5: ablation -- no B loads (B operands stay in registers)
-//   bit 6: ablation -- no LDS A-fragment reads (A operands from registers)
-//   bit 7: ablation -- every block runs the full K range (no triangular schedule)
-//   bit 8: exp2_256 (256-entry table, no rndne/cvt/ldexp) instead of exp2_64
-//   bit 9: exp2_64m (64-entry table, no rndne/cvt/ldexp)
-template <int DI, bool DYN, int VAR = 0, int NW = 4>
-__global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
-  constexpr int NT = 64 * NW;                                // threads
-  constexpr int NB = 64 * NW;                                // columns per block
-  constexpr int FS = NW * 1024;                              // fragment doubles per K-step
-  constexpr int GV = kBK / NW;                               // K* values per thread per K-step
-  constexpr int RW = DI + 1;                                 // row record: Xs[DI], |Xs|^2
-  constexpr int NRV = kBK * RW;                              // row values per K-step
-  constexpr int RPT = (NRV + NT - 1) / NT;                   // row values per thread
-  __shared__ double As[2][kBK][kLDA];
-  __shared__ double RX[2][kBK][RW];
-  constexpr bool E256 = (VAR & 256) != 0;
-  constexpr double kScale = E256 ? kLog2eX256 : kLog2eX64;
-  __shared__ double tab[E256 ? 256 : 64];
-  __shared__ double qred[NW][kPT];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int b = blockIdx.x;
-  const int J = prm.n_j_max - 1 - b / prm.tiles_ub;
-  // tile index within this launch's segments (a launch may cover classes c0..c0+7)
-  const int t = b - (b / prm.tiles_ub) * prm.tiles_ub + prm.seg_tile_start[0];
-
-  int c = -1;
-  for (int s = 0; s < prm.n_seg; ++s)
-    if (t >= prm.seg_tile_start[s] && t < prm.seg_tile_start[s + 1]) c = s;
-  c = __builtin_amdgcn_readfirstlane(c);
-  if (c < 0) return;
-  const int n_j = prm.seg[c].n_j;
-  if (J >= n_j) return;
-  const double* __restrict__ Xs = prm.seg[c].Xs;
-  const double* __restrict__ Xsq = prm.seg[c].Xsq;
-  const double* __restrict__ Bf = prm.seg[c].Bf;
-  const int n_rows = prm.seg[c].n_rows;
-  const int n_m = prm.seg[c].n_m;
-  const int n_cols = n_rows + n_m;
-  const int coff = prm.seg[c].coff;
-
-  if constexpr (E256) {
-    for (int i = tid; i < 256; i += NT) tab[i] = kExp2Tab256[i];
-  } else {
-    if (tid < 64) tab[tid] = kExp2Tab[tid];
-  }
-
-  const int seg_begin = prm.seg_pos_begin[c];
-  const int pos0 = seg_begin + (t - prm.seg_tile_start[c]) * kPT;
-  const int pos_end = prm.seg_pos_end[c];
-  const int out_base = prm.seg_out_base[c] - seg_begin;   // out = out_base + pos
-
-  // ---- this thread's particle (generation role: particle m, rows w + 4s) ----------
-  const int m = lane;
-  int pos = pos0 + m;
-  if (pos >= pos_end) pos = pos0;                          // clamp (results unused)
-  const int prow = prm.perm ? prm.perm[pos] : pos;
-  double a2[DI];                                           // 2 (x / l) (64 / ln 2)
-  double asq = 0.0;
-#pragma unroll
-  for (int j = 0; j < DI; ++j) {
-    const double x = prm.X[(long long)prow * DI + j];
-    const double xs = x / prm.ls[j];
-    asq = fma(xs, xs, asq);
-    a2[j] = (2.0 * kScale) * xs;
-  }
-  asq *= kScale;                                           // |x / l|^2 (64 / ln 2)
-
-  // ---- K ranges ------------------------------------------------------------------
-  const int nks = (VAR & 128) ? ksteps(n_rows) : ksteps(block_kmax(J, n_rows, NB, coff));
-  // this wave's tiles: columns NB*J + 16(NW t + w) .. +15.  T1 = real tiles, kend[t] = the
-  // K-step where tile t retires (R tile: past its last column's diagonal; tiles holding
-  // mean columns: all rows).  kend is non-decreasing in t.
-  int T1 = 0;
-  int kend[4];
-#pragma unroll
-  for (int tt = 0; tt < 4; ++tt) {
-    const int c0 = J * NB + 16 * (NW * tt + w) - coff;   // front-padding tiles: c0 < 0
-    const bool real = c0 >= 0 && c0 < n_cols;
-    if (real) T1 = tt + 1;
-    const int hi = c0 + 16;
-    int ke = (hi <= n_rows) ? ksteps(hi) : ksteps(n_rows);
-    if constexpr (VAR & 129) ke = nks;
-    kend[tt] = real ? (ke < nks ? ke : nks) : 0;
-  }
-  long long boff = 0;                                       // fragments of blocks < J
-  for (int jj = 0; jj < J; ++jj) boff += (long long)ksteps(block_kmax(jj, n_rows, NB, coff)) * FS;
-  const double* __restrict__ Bw = Bf + boff + w * 1024 + lane * 2;
-  // last K-step this wave multiplies (kend is non-decreasing over the real tiles; no
-  // runtime indexing of kend[], which would put it in scratch)
-  const int kmaxw = max(max(kend[0], kend[1]), max(kend[2], kend[3]));
-  const int ks_last = (kmaxw > 0 ? kmaxw : 1) - 1;
-
-  // Training rows of a K-step are staged through an LDS ring (RX) one step ahead with
-  // vector loads, so generation reads them as LDS broadcasts: no scalar loads whose
-  // lgkmcnt(0) waits would serialise with the A-fragment reads.
-  const int last_row = n_rows - 1;
-  auto load_rows = [&](int ks, double (&rr)[RPT]) {
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int idx = tid + NT * k;
-      double v = 0.0;
-      if (idx < NRV) {
-        const int r = idx / RW, f = idx - (idx / RW) * RW;
-        int i = ks * kBK + r;
-        i = i < last_row ? i : last_row;
-        v = f < DI ? Xs[(long long)i * DI + f] : (E256 ? 4.0 * Xsq[i] : Xsq[i]);
-      }
-      rr[k] = v;
-    }
-  };
-  auto store_rows = [&](int buf, const double (&rr)[RPT]) {
-#pragma unroll
-    for (int k = 0; k < RPT; ++k) {
-      const int idx = tid + NT * k;
-      if (idx < NRV) (&RX[buf][0][0])[idx] = rr[k];
-    }
-  };
-  // Branch-free generation (rows past n_rows are zeroed after the fact).
-  auto gen = [&](int ks, double (&v)[GV]) {
-    const int rb = ks & 1;
-#pragma unroll
-    for (int s = 0; s < GV; ++s) {
-      const int r = w + NW * s;
-      const int i = ks * kBK + r;                          // wave-uniform training row
-      const double* row = &RX[rb][r][0];
-      double x;
-      if constexpr (VAR & 4) {
-        x = -(asq + 0.5 * i);
-#pragma unroll
-        for (int j = 0; j < DI; ++j) x = fma(a2[j], 0.25 * j, x);
-      } else {
-        x = -(asq + row[DI]);
-#pragma unroll
-        for (int j = 0; j < DI; ++j) x = fma(a2[j], row[j], x);
-      }
-      double val;
-      if constexpr (VAR & 2) val = fma(x, 1e-3, 1.0);
-      else if constexpr (E256) val = exp2_256(x, tab);
-      else if constexpr ((VAR & 512) != 0) val = exp2_64m(x, tab);
-      else val = exp2_64(x, tab);
-      v[s] = i < n_rows ? val : 0.0;
-    }
-  };
-  // B fragments: one register set, refilled sub-step by sub-step for the next K-step right
-  // after the MFMAs that consumed it (so the prefetch needs no second set of registers).
-  // The address is clamped to the wave's last K-step so no branch guards the loads.
-  auto loadB_part = [&](int ks, int kk, double (&bb)[16]) {
-    if constexpr (VAR & 32) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bb[kk * 4 + q] = bb[kk * 4 + q] * 0.999 + 1e-3 * (ks & 1);
-      return;
-    }
-    const double* src = Bw + (long long)(ks < ks_last ? ks : ks_last) * FS + kk * 256;
-    const double2 x0 = *reinterpret_cast<const double2*>(src);
-    const double2 x1 = *reinterpret_cast<const double2*>(src + 128);
-    bb[kk * 4 + 0] = x0.x;
-    bb[kk * 4 + 1] = x0.y;
-    bb[kk * 4 + 2] = x1.x;
-    bb[kk * 4 + 3] = x1.y;
-  };
-  auto store = [&](int buf, const double (&v)[GV]) {
-#pragma unroll
-    for (int s = 0; s < GV; ++s) As[buf][w + NW * s][m] = v[s];
-  };
-
-  const int li = lane & 15, lk = lane >> 4;
-  d4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
-
-  // One K-step with tiles [T0, T1) active: generate K*(ks+1) and stage rows(ks+2), then per
-  // sub-step kk: A fragments from LDS, MFMAs, refill B(ks+1) for kk.  (Generating for
-  // ks+1 = nks is harmless: clamped rows, stored to a buffer never read again.)
-  auto full_step = [&](auto t0c, auto t1c, int ks, double (&bb)[16]) {
-    constexpr int T0 = decltype(t0c)::value, T1c = decltype(t1c)::value;
-    const int buf = ks & 1;
-    double v[GV];
-    double rr[RPT];
-    if constexpr (!(VAR & 16)) {
-      load_rows(ks + 2, rr);
-      gen(ks + 1, v);
-    }
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      double af[4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        if constexpr (VAR & 64) af[mt] = asq + mt + kk + buf;
-        else af[mt] = As[buf][kk * 4 + lk][mt * 16 + li];
-      }
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int nt = T0; nt < T1c; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bb[kk * 4 + nt], acc[mt][nt], 0, 0, 0);
-      loadB_part(ks + 1, kk, bb);
-    }
-    if constexpr (!(VAR & 16)) {
-      store(buf ^ 1, v);
-      store_rows(buf, rr);
-    }
-    if constexpr (!(VAR & 8)) __syncthreads();
-  };
-
-  double bb[16];
-  if constexpr (VAR & 32) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) bb[q] = 1e-3 * q + lane;
-  }
-  {
-    double rr[RPT];
-    load_rows(0, rr);
-    store_rows(0, rr);
-    load_rows(1, rr);
-    store_rows(1, rr);
-  }
-  __syncthreads();                                           // table + rows of steps 0, 1
-  {
-    double v[GV];
-    gen(0, v);
-    store(0, v);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) loadB_part(0, kk, bb);
-  }
-  __syncthreads();
-
-  int ks = 0;
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  using I4 = std::integral_constant<int, 4>;
-  // K-steps [ks, e) with tiles [T0, T1) active
-  auto run_phase = [&](auto t0c, auto t1c, int e) {
-    for (; ks < e; ++ks) full_step(t0c, t1c, ks, bb);
-  };
-  switch (T1) {
-    case 4:
-      run_phase(I0{}, I4{}, kend[0]);
-      run_phase(I1{}, I4{}, kend[1]);
-      run_phase(I2{}, I4{}, kend[2]);
-      run_phase(I3{}, I4{}, kend[3]);
-      break;
-    case 3:
-      run_phase(I0{}, I3{}, kend[0]);
-      run_phase(I1{}, I3{}, kend[1]);
-      run_phase(I2{}, I3{}, kend[2]);
-      break;
-    case 2:
-      run_phase(I0{}, I2{}, kend[0]);
-      run_phase(I1{}, I2{}, kend[1]);
-      break;
-    case 1:
-      run_phase(I0{}, I1{}, kend[0]);
-      break;
-    default:
-      break;
-  }
-  // the rest of the block's K range (other waves' tiles): generate only
-  for (; ks < nks; ++ks) {
-    double v[GV];
-    double rr[RPT];
-    load_rows(ks + 2, rr);
-    gen(ks + 1, v);
-    store((ks + 1) & 1, v);
-    store_rows(ks & 1, rr);
-    __syncthreads();
-  }
-
-  if constexpr (DYN) {
-    // Linear-kernel share: acc += X~ H for this block.  A fragment: lane l holds
-    // x~[particle mt*16 + (l&15)][4 kh + (l>>4)]; B fragment: Hf[J][kh][w][l][nt].
-    constexpr int KH = (DI + 1 + 3) / 4;
-    const double* __restrict__ Hw = prm.seg[c].Hf + ((long long)J * KH * NW + w) * 256 + lane * 4;
-    int prw[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      int pp = pos0 + mt * 16 + li;
-      if (pp >= pos_end) pp = pos0;
-      prw[mt] = prm.perm ? prm.perm[pp] : pp;
-    }
-#pragma unroll
-    for (int kh = 0; kh < KH; ++kh) {
-      const int k = 4 * kh + lk;
-      const double2 h0 = *reinterpret_cast<const double2*>(Hw + (long long)kh * NW * 256);
-      const double2 h1 = *reinterpret_cast<const double2*>(Hw + (long long)kh * NW * 256 + 2);
-      const double hb[4] = {h0.x, h0.y, h1.x, h1.y};
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const double xa = k < DI ? prm.X[(long long)prw[mt] * DI + (k < DI ? k : 0)] : (k == DI ? 1.0 : 0.0);
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa, hb[nt], acc[mt][nt], 0, 0, 0);
-      }
-    }
-  }
-
-  // ---- epilogue --------------------------------------------------------------------
-  // C/D layout of v_mfma_f64_16x16x4_f64: lane l, reg r -> row (l>>4) + 4r, col l&15.
-  const bool has_r = J * NB - coff < n_rows;
-  if (has_r) {
-    double qs[4][4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double s = 0.0;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-          const double x = acc[mt][nt][r];
-          const int col = J * NB + 16 * (NW * nt + w) + li - coff;
-          if (col >= 0 && col < n_rows) s = fma(x, x, s);
-        }
-        s += __shfl_xor(s, 1);
-        s += __shfl_xor(s, 2);
-        s += __shfl_xor(s, 4);
-        s += __shfl_xor(s, 8);
-        qs[mt][r] = s;
-      }
-    if (li == 0) {
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) qred[w][mt * 16 + lk + 4 * r] = qs[mt][r];
-    }
-  }
-  if ((J + 1) * NB - coff > n_rows) {                         // mean columns
-#pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
-      if (jm >= 0 && jm < n_m) {
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int p = pos0 + mt * 16 + lk + 4 * r;
-            if (p < pos_end) prm.mu[(long long)(out_base + p) * prm.ld_mu + jm] = acc[mt][nt][r];
-          }
-      }
-    }
-  }
-  if (has_r) {
-    __syncthreads();
-    if (tid < kPT) {
-      const int p = pos0 + tid;
-      if (p < pos_end) {
-        double q = 0.0;
-#pragma unroll
-        for (int ww = 0; ww < NW; ++ww) q += qred[ww][tid];
-        prm.qpart[(long long)J * prm.ld_q + out_base + p] = q;
-      }
-    }
-  }
-}
-
 template <int DI>
-static void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
-  const dim3 grid((unsigned)(p.n_j_max * p.tiles_ub));
-  if (p.nw == 8) {
-    if (dyn)
-      hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 8>), grid, dim3(512), 0, stream, p);
-    else
-      hipLaunchKernelGGL((k_gp_tile<DI, false, 0, 8>), grid, dim3(512), 0, stream, p);
-  } else {
-    if (dyn)
-      hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4>), grid, dim3(256), 0, stream, p);
-    else
-      hipLaunchKernelGGL((k_gp_tile<DI, false, 0, 4>), grid, dim3(256), 0, stream, p);
-  }
-}
+void launch_d(const TileParams& p, bool dyn, hipStream_t stream);
 
 void launch_gp_tile(const TileParams& p, int d, bool dyn, hipStream_t stream) {
   if (p.n_j_max <= 0 || p.tiles_ub <= 0) return;

@@ -122,8 +122,9 @@ class GPMDM:
         # reference's own arithmetic), the library's device factor (gpmdm_gp_factor:
         # rocSOLVER potrf/trtri) above; or force "cpu" / "device"
         self._precompute_device = None
-        # waves per GP-tile workgroup (4 or 8; 0 = library default); env override for A/B runs
-        self.tile_waves = int(os.environ.get("GPMDM_TILE_WAVES", "0"))
+        # GP-tile workgroup shape (include/gpmdm_hip.h GPMDM_TILE_*: 0 default, 1 64x256,
+        # 2 64x512, 3 32x512); env override for A/B runs
+        self.tile_shape = int(os.environ.get("GPMDM_TILE_SHAPE", "0"))
 
     # ---- reference API: data registry (gpmdm.py:239-309) -------------------------
     def set_evaluation_mode(self):
@@ -302,7 +303,7 @@ class GPMDM:
         Ry, beta = obs
         desc = _lib.ModelDesc()
         desc.N, desc.D, desc.d, desc.C = self.X.shape[0], D, d, C
-        desc.tile_waves = self.tile_waves
+        desc.tile_shape = self.tile_shape
         desc.X = arr(self.X.numpy())
         desc.obs_R = arr(Ry)
         desc.obs_beta = arr(beta)

@@ -55,12 +55,21 @@ typedef struct gpmdm_pf* gpmdm_pf_t;
  *   dyn_R[c]   Nc x Nc upper-triangular U_c^-1 of the class-c block of K_x (gpmdm.py:1299-1305)
  *   dyn_alpha[c] Nc x d  A_c Xout_c  (mean weights of map_x_dynamics_for_class, gpmdm.py:1064)
  */
+/* GP-tile workgroup shapes (particles x columns of K* B per workgroup).  The default runs
+ * the observation GP as 32x512 and the dynamics GPs as 64x256; 64x512 applies to both. */
+enum {
+  GPMDM_TILE_DEFAULT = 0,
+  GPMDM_TILE_64x256 = 1,
+  GPMDM_TILE_64x512 = 2,
+  GPMDM_TILE_32x512 = 3
+};
+
 typedef struct gpmdm_model_desc {
   int64_t N;                     /* training latents (rows of X, Y) */
   int32_t D;                     /* observation dimension */
   int32_t d;                     /* latent dimension (<= 32) */
   int32_t C;                     /* classes */
-  int32_t tile_waves;            /* waves per GP-tile workgroup: 0 = default (4), 4 or 8 */
+  int32_t tile_shape;            /* GPMDM_TILE_*: GP-tile workgroup shape (0 = default) */
   const double* X;               /* N x d latents (particle initialisation is host-side) */
   const double* obs_R;           /* N x N */
   const double* obs_beta;        /* N x D */

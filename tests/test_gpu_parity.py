@@ -290,3 +290,52 @@ def test_config3_and_config5_shapes_vs_oracle(C, d, D, L):
     assert nrel(st["w"], r.w) < 1e-5
     assert np.max(np.abs(pf.class_probabilities().numpy() - r.posterior)) < 1e-6
     assert nrel(pf.current_state_mean().numpy(), r.mean) < 1e-6
+
+
+@pytest.mark.parametrize("shape", [1, 2, 3])
+@pytest.mark.parametrize("d,D", [(3, 62), (16, 40)])
+def test_tile_shapes_vs_oracle(shape, d, D, monkeypatch):
+    """Every GP-tile workgroup shape (GPMDM_TILE_64x256 / 64x512 / 32x512, forced through
+    GPMDM_TILE_SHAPE) on a ragged model: N = 2 x 3 x 157 rows (not a multiple of any block
+    width), query counts not multiples of the 32- or 64-particle tiles.  Predictive maps and
+    one resynced filter step against the oracle; the 32x512 shape at d=16 (beyond the
+    default's d <= 12 cut, registers spill) must still be exact."""
+    from gpmdm_amd import GPMDM, GPMDM_PF, synthetic
+    from oracle import gpmdm_oracle as O
+    monkeypatch.setenv("GPMDM_TILE_SHAPE", str(shape))
+    C, L = 2, 157
+    data = synthetic.make_sequences(C=C, S=3, L=L, D=D, d=d, seed=21)
+    rng = np.random.RandomState(22)
+    N = C * 3 * L
+    X = rng.randn(N, d)
+    lp = dict(y_log_lengthscales=np.log(rng.uniform(1.0, 2.5, d)), y_log_lambdas=np.log(rng.uniform(0.5, 2, D)),
+              y_log_sigma_n=np.log(0.1), x_log_lengthscales=np.log(rng.uniform(1.0, 2.5, d)),
+              x_log_lambdas=np.log(rng.uniform(0.5, 2, d)), x_log_sigma_n=np.log(0.1),
+              x_log_lin_coeff=np.log(rng.uniform(0.2, 0.8, d + 1)))
+    m = GPMDM.from_arrays(X, data.sequences, **lp)
+    assert m.tile_shape == shape
+    om = O.OracleModel(X=X, Y=np.concatenate([y for c in data.sequences for y in c]).astype(np.float64),
+                       seq_lengths=[[L] * 3] * C, **lp).precompute()
+    for n in (1, 33, 1000):
+        xs = X[rng.randint(0, N, n)] + 0.1 * rng.randn(n, d)
+        mu, var = m.map_x_to_y(torch.tensor(xs))
+        omu, ovar = om.map_x_to_y(xs)
+        assert nrel(mu.numpy(), omu) < 1e-8 and nrel(var.numpy(), ovar) < 1e-7, n
+        for c in range(C):
+            mu, var = m.map_x_dynamics_for_class(torch.tensor(xs), c)
+            omu, ovar = om.map_x_dynamics_for_class(xs, c)
+            assert nrel(mu.numpy(), omu) < 1e-8 and nrel(var.numpy(), ovar) < 1e-6, (n, c)
+    P = 1001
+    T = synthetic.markov_matrix(C)
+    pf = GPMDM_PF(m, torch.tensor(T), P, rng="torch")
+    st0 = pf.export_state()
+    E = rng.exponential(size=(P, C))
+    nrm = rng.randn(P, d)
+    u = rng.rand(P)
+    z = data.sequences[0][0][5].astype(np.float64)
+    pf.update_with_draws(z, E, nrm, u)
+    r = O.step(om, T, st0["states"], st0["classes"], z, E, nrm, u)
+    st = pf.export_state()
+    assert np.array_equal(st["classes"], r.classes)
+    assert nrel(st["states"], r.states) < 1e-6
+    assert nrel(st["w"], r.w) < 1e-5

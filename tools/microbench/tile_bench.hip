@@ -8,15 +8,15 @@
 #include <random>
 #include <vector>
 
-#include "../../gpmdm_amd/csrc/gp_tile.hip"
+#include "../../gpmdm_amd/csrc/gp_tile.h"
 
 using namespace gpmdm;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
-template <int VAR, int NW>
+template <int VAR, int NW, int MT = 4, int NTW = 4>
 void launch_var(const TileParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((k_gp_tile<3, false, VAR, NW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, p);
+  hipLaunchKernelGGL((k_gp_tile<3, false, VAR, NW, MT, NTW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, p);
 }
 
 int main(int argc, char** argv) {
@@ -32,23 +32,27 @@ int main(int argc, char** argv) {
   }
   for (auto& v : hX) v = 2.0 * nd(rng);
   double *Xs, *Xsq, *X, *q, *mu;
-  int* tab;
   CK(hipMalloc(&Xs, N * d * 8)); CK(hipMalloc(&Xsq, N * 8));
-  CK(hipMalloc(&X, (size_t)P * d * 8)); CK(hipMalloc(&q, (size_t)P * 16 * 8)); CK(hipMalloc(&mu, (size_t)P * D * 8));
-  CK(hipMalloc(&tab, 64));
-  CK(hipMemcpy(Xs, hXs.data(), N * d * 8, hipMemcpyHostToDevice));
+  CK(hipMalloc(&X, (size_t)P * d * 8)); CK(hipMalloc(&q, (size_t)P * 32 * 8)); CK(hipMalloc(&mu, (size_t)P * D * 8));
+    CK(hipMemcpy(Xs, hXs.data(), N * d * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(Xsq, hXsq.data(), N * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(X, hX.data(), (size_t)P * d * 8, hipMemcpyHostToDevice));
-  const int ntiles = (P + kPT - 1) / kPT;
-  int ht[5] = {0, P, 0, 0, ntiles};
-  CK(hipMemcpy(tab, ht, sizeof(ht), hipMemcpyHostToDevice));
-  TileParams pp[2];
-  for (int v = 0; v < 2; ++v) {
-    const int nw = v == 0 ? 4 : 8, nb = 64 * nw;
+  // geometries: {waves, particle tiles MT, column tiles per wave NTW}
+  struct Geo { int nw, mt, ntw; };
+  const Geo geos[] = {{4, 4, 4}, {8, 2, 8}, {4, 2, 8}, {8, 2, 4}};
+  const int NGEO = sizeof(geos) / sizeof(geos[0]);
+  TileParams pp[NGEO];
+  int* tabs;
+  CK(hipMalloc(&tabs, NGEO * 8 * sizeof(int)));
+  for (int v = 0; v < NGEO; ++v) {
+    const int nw = geos[v].nw, pt = 16 * geos[v].mt, nb = 16 * geos[v].ntw * nw, fs = nw * 256 * geos[v].ntw;
+    const int ntiles = (P + pt - 1) / pt;
+    int ht[5] = {0, P, 0, 0, ntiles};
+    CK(hipMemcpy(tabs + 8 * v, ht, sizeof(ht), hipMemcpyHostToDevice));
     const int coff = getenv("TB_NO_COFF") ? 0 : col_offset(N + D, nb);
     const int n_j = (N + D + coff + nb - 1) / nb;
     long long total = 0;
-    for (int J = 0; J < n_j; ++J) total += (long long)ksteps(block_kmax(J, N, nb, coff)) * nw * 1024;
+    for (int J = 0; J < n_j; ++J) total += (long long)ksteps(block_kmax(J, N, nb, coff)) * fs;
     std::vector<double> hB(total);
     for (auto& x : hB) x = 0.01 * nd(rng);
     double* B;
@@ -57,8 +61,9 @@ int main(int argc, char** argv) {
     TileParams& p = pp[v];
     p = TileParams{};
     p.seg[0].Xs = Xs; p.seg[0].Xsq = Xsq; p.seg[0].Bf = B;
-    p.seg[0].n_rows = N; p.seg[0].n_m = D; p.seg[0].n_j = n_j; p.seg[0].n_wc = (N + D + 63) / 64; p.seg[0].coff = coff;
-    p.n_seg = 1; p.tiles_ub = ntiles; p.n_j_max = n_j; p.nw = nw;
+    p.seg[0].n_rows = N; p.seg[0].n_m = D; p.seg[0].n_j = n_j; p.seg[0].coff = coff;
+    p.n_seg = 1; p.tiles_ub = ntiles; p.n_j_max = n_j; p.geo = TileGeo{nw, geos[v].mt, geos[v].ntw};
+    int* tab = tabs + 8 * v;
     p.seg_pos_begin = tab; p.seg_pos_end = tab + 1; p.seg_out_base = tab + 2; p.seg_tile_start = tab + 3;
     p.X = X;
     for (int j = 0; j < d; ++j) p.ls[j] = 1.0;
@@ -70,9 +75,10 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   typedef void (*L)(const TileParams&, hipStream_t);
   struct V { L fn; int pi; const char* name; };
-  V vars[] = {{launch_var<0, 4>, 0, "NW4 production"}, {launch_var<0, 8>, 1, "NW8 production"},
-              {launch_var<16, 4>, 0, "NW4 no gen"}, {launch_var<16, 8>, 1, "NW8 no gen"},
-              {launch_var<2, 8>, 1, "NW8 cheap stand-in exp"}};
+  V vars[] = {{launch_var<0, 4>, 0, "NW4 64x256 production"}, {launch_var<0, 4, 2, 8>, 2, "NW4 32x512"},
+              {launch_var<0, 8, 2, 8>, 1, "NW8 32x1024"}, {launch_var<0, 8, 2, 4>, 3, "NW8 32x512"},
+              {launch_var<256, 4, 2, 8>, 2, "NW4 32x512 exp2_256"}, {launch_var<512, 4, 2, 8>, 2, "NW4 32x512 exp2_64m"},
+              {launch_var<16, 8, 2, 8>, 1, "NW8 32x1024 no gen"}};
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
   std::vector<std::vector<float>> t(NV);
   for (int v = 0; v < NV; ++v) vars[v].fn(pp[vars[v].pi], s);
