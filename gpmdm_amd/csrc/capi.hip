@@ -167,6 +167,8 @@ struct gpmdm_model {
   GpImage obs;
   std::vector<GpImage> dyn;
   double* y_il2_dev = nullptr;
+  double* y_lam2_dev = nullptr;   // 1 / il2 = exp(y_log_lambdas)^2
+  double sum_log_il2 = 0.0;
   // predictive-map scratch
   int* tab = nullptr;                 // 5 ints: begin, end, out_base, tile_start[2]
   double* qscratch = nullptr;
@@ -176,6 +178,7 @@ struct gpmdm_model {
     obs.release();
     for (auto& g : dyn) g.release();
     dfree(y_il2_dev);
+    dfree(y_lam2_dev);
     dfree(tab);
     dfree(qscratch);
   }
@@ -205,7 +208,7 @@ struct gpmdm_pf {
   // ancestor de-duplication: owner/slot are C x P keyed by (class, ancestor)
   unsigned* owner = nullptr;
   int *slot = nullptr, *lflag = nullptr, *lblock = nullptr, *ltab = nullptr, *lperm = nullptr;
-  double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *muobs = nullptr;
+  double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *sobs = nullptr;
   int nparts_dyn_max = 0;
   double *z = nullptr, *E = nullptr, *normals = nullptr, *U = nullptr;
   unsigned long long* gmax = nullptr;
@@ -230,7 +233,7 @@ struct gpmdm_pf {
   int* lseg_tiles() const { return ltab + 120; }
 
   ~gpmdm_pf() {
-    double* ds[] = {T, X, X_prop, ll, qdyn, mudyn, qobs, muobs, z, E, normals, U,
+    double* ds[] = {T, X, X_prop, ll, qdyn, mudyn, qobs, sobs, z, E, normals, U,
                     e, local, blocksum, blockoffw, total, cum, partials, readout};
     for (double* p : ds) dfree(p);
     int* is[] = {cls, cls_new, perm, ridx, blockcounts, blockoff, small, obs_tab,
@@ -322,6 +325,19 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
   if (hipMemcpy(m->y_il2_dev, m->y_il2.data(), m->D * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
     delete m;
     return fail(GPMDM_E_HIP, "upload y_inv_lambda2");
+  }
+  {
+    std::vector<double> lam2(m->D);
+    for (int j = 0; j < m->D; ++j) {
+      lam2[j] = 1.0 / m->y_il2[j];
+      m->sum_log_il2 += std::log(m->y_il2[j]);
+    }
+    rc = dalloc(&m->y_lam2_dev, m->D);
+    if (rc) { delete m; return rc; }
+    if (hipMemcpy(m->y_lam2_dev, lam2.data(), m->D * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+      delete m;
+      return fail(GPMDM_E_HIP, "upload lambda^2");
+    }
   }
   rc = dalloc(&m->tab, 8);
   if (rc) { delete m; return rc; }
@@ -490,7 +506,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   ALLOC(qdyn, (long long)maxparts * nl);
   ALLOC(mudyn, nl * d);
   ALLOC(qobs, (long long)m->obs.n_parts() * nl);
-  ALLOC(muobs, nl * D);
+  ALLOC(sobs, (long long)m->obs.n_j * nl);   // fused likelihood partials (no mean stored)
   ALLOC(z, F * D);
   if (rng_mode == GPMDM_RNG_REPLAY) {
     ALLOC(E, P * C);
@@ -806,8 +822,10 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     fill_tile_common(tp, m, false);
     tp.qpart = pf->qobs;
     tp.ld_q = nl;
-    tp.mu = pf->muobs;
-    tp.ld_mu = D;
+    tp.spart = pf->sobs;
+    tp.z = pf->z;
+    tp.lam2 = m->y_lam2_dev;
+    tp.Pf = pf->Pf;
     launch_gp_tile(tp, d, false, s);
     pf->mark_end(s, GPMDM_STAGE_OBS_GEMM, t0);
     pf->mark_begin(s, t0);
@@ -817,8 +835,10 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     oa.D = D;
     oa.qpart = pf->qobs;
     oa.ld_q = nl;
-    oa.mu = pf->muobs;
-    oa.ld_mu = D;
+    oa.spart = pf->sobs;
+    oa.jm0 = (m->obs.n_rows + m->obs.coff) / m->obs.geo.nb();   // first block with mean columns
+    oa.n_j = m->obs.n_j;
+    oa.sum_log_il2 = m->sum_log_il2;
     oa.z = pf->z;
     oa.Pf = pf->Pf;
     oa.il2 = m->y_il2_dev;

@@ -58,8 +58,15 @@ struct TileParams {
   double ls[kMaxD];               // RBF lengthscales
   double* qpart;                  // [J][ld_q]: partial sums of (R^T k)^2 per column block
   long long ld_q;
-  double* mu;                     // [out][ld_mu] mean columns
+  double* mu;                     // [out][ld_mu] mean columns (predictive maps)
   long long ld_mu;
+  // Fused likelihood (particle filter, observation GP): instead of storing the mean, blocks
+  // holding mean columns write spart[J][out] = sum_j (z_j - mu_j)^2 lam2_j over their mean
+  // columns (z = the observation of the particle's filter, pos / Pf).
+  double* spart;                  // nullptr: store mu
+  const double* z;                // F x n_m
+  const double* lam2;             // n_m: exp(y_log_lambdas)^2 = 1 / il2
+  long long Pf;                   // particles per filter
 };
 
 // Column-block geometry shared by the host (fragment layout) and the kernel.

@@ -203,6 +203,8 @@ __device__ __forceinline__ double exp2_64m(double t, const double* tab) {
 //   bit 7: ablation -- every block runs the full K range (no triangular schedule)
 //   bit 8: exp2_256 (256-entry table, no rndne/cvt/ldexp) instead of exp2_64
 //   bit 9: exp2_64m (64-entry table, no rndne/cvt/ldexp)
+//   bit 10: A/B -- conditional row staging (only the NRV record threads load and store)
+//   bit 11: A/B -- no vmcnt(0) drain after the prologue
 //
 // Geometry: NW waves; each wave owns MT x NTW tiles of 16 x 16 (16 MT particles x 16 NTW
 // columns), so a workgroup covers PT = 16 MT particles x NB = 16 NTW NW columns.  K* costs
@@ -235,11 +237,12 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   constexpr int NRV = kBK * RW;                              // row values per K-step
   constexpr int RPT = (NRV + NT - 1) / NT;                   // row values per thread
   __shared__ double As[2][kBK][LDA];
-  __shared__ double RX[2][kBK][RW];
+  __shared__ double RX[2][RPT * NT];                          // row records, then padding
   constexpr bool E256 = (VAR & 256) != 0;
   constexpr double kScale = E256 ? kLog2eX256 : kLog2eX64;
   __shared__ double tab[E256 ? 256 : 64];
   __shared__ double qred[NW][PT];
+  __shared__ double sred[NW][PT];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -323,25 +326,30 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   // vector loads, so generation reads them as LDS broadcasts: no scalar loads whose
   // lgkmcnt(0) waits would serialise with the A-fragment reads.
   const int last_row = n_rows - 1;
+  // Branch-free: threads past the record count load a clamped (valid) address and store it
+  // to a padding slot, so no exec-mask branch splits the K-step (the compiler otherwise
+  // sinks the load into the conditional store and waits for it with vmcnt(0)).
   auto load_rows = [&](int ks, double (&rr)[RPT]) {
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-      const int idx = tid + NT * k;
-      double v = 0.0;
-      if (idx < NRV) {
-        const int r = idx / RW, f = idx - (idx / RW) * RW;
-        int i = ks * kBK + r;
-        i = i < last_row ? i : last_row;
-        v = f < DI ? Xs[(long long)i * DI + f] : (E256 ? 4.0 * Xsq[i] : Xsq[i]);
-      }
-      rr[k] = v;
+      int idx = tid + NT * k;
+      idx = idx < NRV ? idx : NRV - 1;
+      const int r = idx / RW, f = idx - (idx / RW) * RW;
+      int i = ks * kBK + r;
+      i = i < last_row ? i : last_row;
+      const double* src = f < DI ? Xs + ((long long)i * DI + f) : Xsq + i;
+      const double v = *src;
+      rr[k] = (E256 && f == DI) ? 4.0 * v : v;
     }
   };
   auto store_rows = [&](int buf, const double (&rr)[RPT]) {
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-      const int idx = tid + NT * k;
-      if (idx < NRV) (&RX[buf][0][0])[idx] = rr[k];
+      if constexpr (VAR & 1024) {
+        if (tid + NT * k < NRV) RX[buf][tid + NT * k] = rr[k];
+      } else {
+        RX[buf][tid + NT * k] = rr[k];                      // unconditional (padding slots)
+      }
     }
   };
   // Branch-free generation (rows past n_rows are zeroed after the fact).
@@ -351,7 +359,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     for (int s = 0; s < GV; ++s) {
       const int r = g + NG * s;
       const int i = ks * kBK + r;                          // training row
-      const double* row = &RX[rb][r][0];
+      const double* row = &RX[rb][r * RW];
       double x;
       if constexpr (VAR & 4) {
         x = -(asq + 0.5 * i);
@@ -453,6 +461,10 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) loadB_part(0, kk, bb);
   }
+  // Drain the prologue's loads (vmcnt(0)) so that the K loop's entry carries no pending
+  // loads: otherwise the waitcnt pass merges the prologue's issue order into the loop
+  // header and waits for every in-flight B fragment at sub-step 0 of each K-step.
+  if constexpr (!(VAR & 2048)) __builtin_amdgcn_s_waitcnt(0x0F70);
   __syncthreads();
 
   int ks = 0;
@@ -539,7 +551,9 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
         for (int r = 0; r < 4; ++r) qred[w][mt * 16 + lk + 4 * r] = qs[mt][r];
     }
   }
-  if ((J + 1) * NB - coff > n_rows) {                         // mean columns
+  const bool has_m = (J + 1) * NB - coff > n_rows;            // block holds mean columns
+  const bool fused = prm.spart != nullptr;
+  if (has_m && !fused) {
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
@@ -554,15 +568,59 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       }
     }
   }
-  if (has_r) {
+  if (has_m && fused) {
+    // sum_j (z_j - mu_j)^2 lam2_j over this block's mean columns (gpmdm_pf.py:188-192 with
+    // var_j = vc / lam2_j factored out; k_obs_ll finishes the likelihood)
+    double ss[MT][4];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ss[mt][r] = 0.0;
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+      const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
+      if (jm >= 0 && jm < n_m) {
+        const double lam = prm.lam2[jm];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            int p = pos0 + mt * 16 + lk + 4 * r;
+            p = p < pos_end ? p : pos0;
+            const double t = prm.z[(p / prm.Pf) * n_m + jm] - acc[mt][nt][r];
+            ss[mt][r] = fma(t * t, lam, ss[mt][r]);
+          }
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double s = ss[mt][r];
+        s += __shfl_xor(s, 1);
+        s += __shfl_xor(s, 2);
+        s += __shfl_xor(s, 4);
+        s += __shfl_xor(s, 8);
+        if (li == 0) sred[w][mt * 16 + lk + 4 * r] = s;
+      }
+  }
+  if (has_r || (has_m && fused)) {
     __syncthreads();
     if (tid < PT) {
       const int p = pos0 + tid;
       if (p < pos_end) {
-        double q = 0.0;
+        if (has_r) {
+          double q = 0.0;
 #pragma unroll
-        for (int ww = 0; ww < NW; ++ww) q += qred[ww][tid];
-        prm.qpart[(long long)J * prm.ld_q + out_base + p] = q;
+          for (int ww = 0; ww < NW; ++ww) q += qred[ww][tid];
+          prm.qpart[(long long)J * prm.ld_q + out_base + p] = q;
+        }
+        if (has_m && fused) {
+          double sm = 0.0;
+#pragma unroll
+          for (int ww = 0; ww < NW; ++ww) sm += sred[ww][tid];
+          prm.spart[(long long)J * prm.ld_q + out_base + p] = sm;
+        }
       }
     }
   }

@@ -118,6 +118,10 @@ struct ObsFinishArgs {
   double* ll;                     // PF output (ll[ll_offset + o]) or nullptr
   long long ll_offset;
   double* var_out;                // predictive map output n x D, or nullptr
+  // fused mode (the tile kernel wrote spart instead of mu): ll from q and S partials
+  const double* spart;            // [J][ld_q] for J in [jm0, n_j), or nullptr
+  int jm0, n_j;
+  double sum_log_il2;             // sum_j log il2_j
 };
 
 // Normalisation and resampling run per filter: grid (nb, F), nb blocks of 256 per filter.

@@ -5,6 +5,7 @@
 //   k_group         stable class grouping (the order of gpmdm_pf.py:158-161)
 //   k_dyn_finish    variance + sample mu + sqrt(var) eps   gpmdm.py:1062-1067, gpmdm_pf.py:167-168
 //   k_obs_finish    variance + Gaussian log-likelihood      gpmdm.py:958-961, gpmdm_pf.py:188-192
+//   k_obs_ll        the same from the tile kernel's fused partial sums (filter path)
 //   k_norm_*        log_w = ll - max, w = exp / sum          gpmdm_pf.py:200-204
 //   k_cdf/k_resample  torch.multinomial(w, P, True) inverse CDF + gathers  gpmdm_pf.py:206-213
 //                   and the read-out partial sums            gpmdm_pf.py:224-262, 302-312
@@ -349,6 +350,22 @@ __global__ __launch_bounds__(kB) void k_obs_finish(ObsFinishArgs a) {
   (void)smax;
 }
 
+// Fused form of k_obs_finish for the filter (one thread per particle): the tile kernel
+// left S = sum_j (z_j - mu_j)^2 lam2_j in spart, and with var_j = vc il2_j
+//   ll = -1/2 sum_j[(z_j - mu_j)^2 / var_j + log var_j] + sum_j(-log sqrt var_j) - D/2 ln(2pi)_f32
+//      = -1/2 S / vc - D log vc - sum_j log il2_j - D/2 ln(2pi)_f32
+// (the reference's double count of log var kept, gpmdm_pf.py:188-192).
+__global__ __launch_bounds__(kB) void k_obs_ll(ObsFinishArgs a) {
+  const long long o = (long long)blockIdx.x * kB + threadIdx.x;
+  if (o >= a.n_out) return;
+  double q = 0.0;
+  for (int k = 0; k < a.n_parts; ++k) q += a.qpart[(long long)k * a.ld_q + o];
+  double S = 0.0;
+  for (int k = a.jm0; k < a.n_j; ++k) S += a.spart[(long long)k * a.ld_q + o];
+  const double vc = 1.0 - q;                           // k(x*,x*) = 1 (gpmdm.py:991)
+  a.ll[a.ll_offset + o] = -0.5 * S / vc - a.D * log(vc) - a.sum_log_il2 - a.ll_const;
+}
+
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(kB) void k_norm_max(NormArgs a) {
   __shared__ double s[kB / 64];
@@ -572,7 +589,11 @@ void launch_dyn_finish(const DynFinishArgs& a, hipStream_t s) {
   if (a.n_out > 0) hipLaunchKernelGGL(k_dyn_finish, dim3(nblk(a.n_out, kB)), dim3(kB), 0, s, a);
 }
 void launch_obs_finish(const ObsFinishArgs& a, hipStream_t s) {
-  if (a.n_out > 0) hipLaunchKernelGGL(k_obs_finish, dim3(nblk(a.n_out, kB / 64)), dim3(kB), 0, s, a);
+  if (a.n_out <= 0) return;
+  if (a.spart)
+    hipLaunchKernelGGL(k_obs_ll, dim3(nblk(a.n_out, kB)), dim3(kB), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_obs_finish, dim3(nblk(a.n_out, kB / 64)), dim3(kB), 0, s, a);
 }
 void launch_normalise(const NormArgs& a, hipStream_t s) {
   const dim3 g(nblk(a.P, kB), (unsigned)a.F);

@@ -39,7 +39,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(X, hX.data(), (size_t)P * d * 8, hipMemcpyHostToDevice));
   // geometries: {waves, particle tiles MT, column tiles per wave NTW}
   struct Geo { int nw, mt, ntw; };
-  const Geo geos[] = {{4, 4, 4}, {8, 2, 8}, {4, 2, 8}, {8, 2, 4}};
+  const Geo geos[] = {{4, 4, 4}, {8, 4, 4}, {4, 2, 8}};
   const int NGEO = sizeof(geos) / sizeof(geos[0]);
   TileParams pp[NGEO];
   int* tabs;
@@ -75,10 +75,9 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   typedef void (*L)(const TileParams&, hipStream_t);
   struct V { L fn; int pi; const char* name; };
-  V vars[] = {{launch_var<0, 4>, 0, "NW4 64x256 production"}, {launch_var<0, 4, 2, 8>, 2, "NW4 32x512"},
-              {launch_var<0, 8, 2, 8>, 1, "NW8 32x1024"}, {launch_var<0, 8, 2, 4>, 3, "NW8 32x512"},
-              {launch_var<256, 4, 2, 8>, 2, "NW4 32x512 exp2_256"}, {launch_var<512, 4, 2, 8>, 2, "NW4 32x512 exp2_64m"},
-              {launch_var<16, 8, 2, 8>, 1, "NW8 32x1024 no gen"}};
+  V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512 now"}, {launch_var<1024 | 2048, 4, 2, 8>, 2, "32x512 cond rows, no drain"},
+              {launch_var<1024, 4, 2, 8>, 2, "32x512 cond rows, drain"}, {launch_var<2048, 4, 2, 8>, 2, "32x512 uncond rows, no drain"},
+              {launch_var<0, 4>, 0, "64x256 now"}, {launch_var<1024 | 2048, 4>, 0, "64x256 cond rows, no drain"}};
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
   std::vector<std::vector<float>> t(NV);
   for (int v = 0; v < NV; ++v) vars[v].fn(pp[vars[v].pi], s);
