@@ -297,8 +297,9 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
   // tile shapes: the observation GP defaults to 32x512 (half the kernel-value generation per
   // MFMA of 64x256, tools/microbench/tile_bench.hip); the dynamics GPs use 64-particle tiles
   // (their class-grouped tile starts are computed on the device in 64s, pf_kernels.hip)
-  // (above d = 12 the 32x512 shape's registers spill: 64x256 there)
-  TileGeo obs_geo = d <= 12 ? kGeo32x512 : kGeo64x256, dyn_geo = kGeo64x256;
+  // (above d = 12 the 32x512 shape's registers spill; 64x512 (8 waves) is the best of the
+  // others there: config 5, d = 16, 0.79 of FP64 peak vs 0.70 for 64x256)
+  TileGeo obs_geo = d <= 12 ? kGeo32x512 : kGeo64x512, dyn_geo = kGeo64x256;
   switch (desc->tile_shape) {
     case GPMDM_TILE_DEFAULT: break;
     case GPMDM_TILE_64x256: obs_geo = kGeo64x256; break;

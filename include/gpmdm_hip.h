@@ -56,7 +56,8 @@ typedef struct gpmdm_pf* gpmdm_pf_t;
  *   dyn_alpha[c] Nc x d  A_c Xout_c  (mean weights of map_x_dynamics_for_class, gpmdm.py:1064)
  */
 /* GP-tile workgroup shapes (particles x columns of K* B per workgroup).  The default runs
- * the observation GP as 32x512 and the dynamics GPs as 64x256; 64x512 applies to both. */
+ * the observation GP as 32x512 (d <= 12) or 64x512 (d > 12) and the dynamics GPs as
+ * 64x256; an explicit 64x512 applies to both. */
 enum {
   GPMDM_TILE_DEFAULT = 0,
   GPMDM_TILE_64x256 = 1,
