@@ -85,7 +85,8 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
   g.coff = col_offset(n_rows + n_m, nb);
   g.n_j = (int)cdiv(n_rows + n_m + g.coff, nb);
   const int coff = g.coff;
-  std::vector<double> xs((size_t)n_rows * d), xsq(n_rows, 0.0);
+  const int cap = row_cap(n_rows);   // padded rows (gp_tile.h: padding rows generate K* = 0)
+  std::vector<double> xs((size_t)cap * d, 0.0), xsq(cap, kPadSq);
   for (long long i = 0; i < n_rows; ++i) {
     double s = 0.0;
     for (int j = 0; j < d; ++j) {

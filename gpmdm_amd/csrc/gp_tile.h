@@ -205,6 +205,8 @@ __device__ __forceinline__ double exp2_64m(double t, const double* tab) {
 //   bit 9: exp2_64m (64-entry table, no rndne/cvt/ldexp)
 //   bit 10: A/B -- conditional row staging (only the NRV record threads load and store)
 //   bit 11: A/B -- no vmcnt(0) drain after the prologue
+//   bit 12: generation split across the sub-steps + sched_group_barrier MFMA/VALU interleave
+//   bit 13: generation split across the sub-steps (no sched_group_barrier)
 //
 // Geometry: NW waves; each wave owns MT x NTW tiles of 16 x 16 (16 MT particles x 16 NTW
 // columns), so a workgroup covers PT = 16 MT particles x NB = 16 NTW NW columns.  K* costs
@@ -325,7 +327,6 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   // Training rows of a K-step are staged through an LDS ring (RX) one step ahead with
   // vector loads, so generation reads them as LDS broadcasts: no scalar loads whose
   // lgkmcnt(0) waits would serialise with the A-fragment reads.
-  const int last_row = n_rows - 1;
   // Branch-free: threads past the record count load a clamped (valid) address and store it
   // to a padding slot, so no exec-mask branch splits the K-step (the compiler otherwise
   // sinks the load into the conditional store and waits for it with vmcnt(0)).
@@ -336,7 +337,6 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       idx = idx < NRV ? idx : NRV - 1;
       const int r = idx / RW, f = idx - (idx / RW) * RW;
       int i = ks * kBK + r;
-      i = i < last_row ? i : last_row;
       const double* src = f < DI ? Xs + ((long long)i * DI + f) : Xsq + i;
       const double v = *src;
       rr[k] = (E256 && f == DI) ? 4.0 * v : v;
@@ -352,31 +352,35 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       }
     }
   };
-  // Branch-free generation (rows past n_rows are zeroed after the fact).
-  auto gen = [&](int ks, double (&v)[GV]) {
+  // Branch-free generation.  The row arrays are padded to row_cap(n_rows) rows with
+  // |Xs|^2 = kPadSq, so the exponent of a padding row is ~ -1e300 and its kernel value is
+  // exactly 0 (v_cvt_i32_f64 saturates, ldexp underflows): no masking per value.
+  auto gen_one = [&](int ks, int s) -> double {
     const int rb = ks & 1;
+    const int r = g + NG * s;
+    const int i = ks * kBK + r;                            // training row
+    const double* row = &RX[rb][r * RW];
+    double x;
+    if constexpr (VAR & 4) {
+      x = -(asq + 0.5 * i);
 #pragma unroll
-    for (int s = 0; s < GV; ++s) {
-      const int r = g + NG * s;
-      const int i = ks * kBK + r;                          // training row
-      const double* row = &RX[rb][r * RW];
-      double x;
-      if constexpr (VAR & 4) {
-        x = -(asq + 0.5 * i);
+      for (int j = 0; j < DI; ++j) x = fma(a2[j], 0.25 * j, x);
+    } else {
+      x = -(asq + row[DI]);
 #pragma unroll
-        for (int j = 0; j < DI; ++j) x = fma(a2[j], 0.25 * j, x);
-      } else {
-        x = -(asq + row[DI]);
-#pragma unroll
-        for (int j = 0; j < DI; ++j) x = fma(a2[j], row[j], x);
-      }
-      double val;
-      if constexpr (VAR & 2) val = fma(x, 1e-3, 1.0);
-      else if constexpr (E256) val = exp2_256(x, tab);
-      else if constexpr ((VAR & 512) != 0) val = exp2_64m(x, tab);
-      else val = exp2_64(x, tab);
-      v[s] = i < n_rows ? val : 0.0;
+      for (int j = 0; j < DI; ++j) x = fma(a2[j], row[j], x);
     }
+    double val;
+    if constexpr (VAR & 2) val = fma(x, 1e-3, 1.0);
+    else if constexpr (E256) val = exp2_256(x, tab);
+    else if constexpr ((VAR & 512) != 0) val = exp2_64m(x, tab);
+    else val = exp2_64(x, tab);
+    (void)i;
+    return val;                                            // padding rows: exactly 0
+  };
+  auto gen = [&](int ks, double (&v)[GV]) {
+#pragma unroll
+    for (int s = 0; s < GV; ++s) v[s] = gen_one(ks, s);
   };
   // B fragments: one register set, refilled sub-step by sub-step for the next K-step right
   // after the MFMAs that consumed it (so the prefetch needs no second set of registers).
@@ -410,6 +414,11 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   // One K-step with tiles [T0, T1) active: generate K*(ks+1) and stage rows(ks+2), then per
   // sub-step kk: A fragments from LDS, MFMAs, refill B(ks+1) for kk.  (Generating for
   // ks+1 = nks is harmless: clamped rows, stored to a buffer never read again.)
+  // VAR 4096/8192 (A/B): the K* values of step ks+1 are generated between the sub-steps'
+  // MFMAs (value s after sub-step s*4/GV) instead of in one block; 4096 also pins an
+  // MFMA/VALU interleave with sched_group_barrier so the generation's dependent chain
+  // hides under the MFMA pipe.
+  constexpr bool SPLIT = (VAR & (4096 | 8192)) != 0;
   auto full_step = [&](auto t0c, auto t1c, int ks, double (&bb)[4 * NTW]) {
     constexpr int T0 = decltype(t0c)::value, T1c = decltype(t1c)::value;
     const int buf = ks & 1;
@@ -417,7 +426,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     double rr[RPT];
     if constexpr (!(VAR & 16)) {
       load_rows(ks + 2, rr);
-      gen(ks + 1, v);
+      if constexpr (!SPLIT) gen(ks + 1, v);
     }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
@@ -432,6 +441,22 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
 #pragma unroll
         for (int nt = T0; nt < T1c; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bb[kk * NTW + nt], acc[mt][nt], 0, 0, 0);
+      if constexpr (SPLIT && !(VAR & 16)) {
+        constexpr int PER = 4 / GV > 0 ? 4 / GV : 1;
+        if (kk % PER == 0) {
+#pragma unroll
+          for (int s = 0; s < GV; ++s)
+            if (s == kk / PER) v[s] = gen_one(ks + 1, s);
+        }
+      }
+      if constexpr ((VAR & 4096) != 0) {
+        constexpr int NM = MT * (T1c - T0);
+#pragma unroll
+        for (int q = 0; q < NM; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // 2 VALU
+        }
+      }
       loadB_part(ks + 1, kk, bb);
     }
     if constexpr (!(VAR & 16)) {

@@ -24,7 +24,8 @@ int main(int argc, char** argv) {
   const int P = argc > 1 ? atoi(argv[1]) : 100000;
   std::mt19937_64 rng(1);
   std::normal_distribution<double> nd(0.0, 1.0);
-  std::vector<double> hXs(N * d), hXsq(N), hX((size_t)P * d);
+  const int cap = row_cap(N);   // padded like capi.hip::build_image
+  std::vector<double> hXs((size_t)cap * d, 0.0), hXsq(cap, kPadSq), hX((size_t)P * d);
   for (int i = 0; i < N; ++i) {
     double s = 0;
     for (int j = 0; j < d; ++j) { hXs[i * d + j] = 2.0 * nd(rng); s += hXs[i * d + j] * hXs[i * d + j]; }
@@ -32,10 +33,10 @@ int main(int argc, char** argv) {
   }
   for (auto& v : hX) v = 2.0 * nd(rng);
   double *Xs, *Xsq, *X, *q, *mu;
-  CK(hipMalloc(&Xs, N * d * 8)); CK(hipMalloc(&Xsq, N * 8));
+  CK(hipMalloc(&Xs, cap * d * 8)); CK(hipMalloc(&Xsq, cap * 8));
   CK(hipMalloc(&X, (size_t)P * d * 8)); CK(hipMalloc(&q, (size_t)P * 32 * 8)); CK(hipMalloc(&mu, (size_t)P * D * 8));
-    CK(hipMemcpy(Xs, hXs.data(), N * d * 8, hipMemcpyHostToDevice));
-  CK(hipMemcpy(Xsq, hXsq.data(), N * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(Xs, hXs.data(), cap * d * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(Xsq, hXsq.data(), cap * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(X, hX.data(), (size_t)P * d * 8, hipMemcpyHostToDevice));
   // geometries: {waves, particle tiles MT, column tiles per wave NTW}
   struct Geo { int nw, mt, ntw; };
@@ -75,9 +76,8 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   typedef void (*L)(const TileParams&, hipStream_t);
   struct V { L fn; int pi; const char* name; };
-  V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512 now"}, {launch_var<1024 | 2048, 4, 2, 8>, 2, "32x512 cond rows, no drain"},
-              {launch_var<1024, 4, 2, 8>, 2, "32x512 cond rows, drain"}, {launch_var<2048, 4, 2, 8>, 2, "32x512 uncond rows, no drain"},
-              {launch_var<0, 4>, 0, "64x256 now"}, {launch_var<1024 | 2048, 4>, 0, "64x256 cond rows, no drain"}};
+  V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512 production"}, {launch_var<16, 4, 2, 8>, 2, "32x512 no gen"},
+              {launch_var<0, 4>, 0, "64x256 production"}, {launch_var<0, 8>, 1, "64x512 production"}};
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
   std::vector<std::vector<float>> t(NV);
   for (int v = 0; v < NV; ++v) vars[v].fn(pp[vars[v].pi], s);
