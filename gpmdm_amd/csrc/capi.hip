@@ -299,11 +299,13 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
   // MFMA of 64x256, tools/microbench/tile_bench.hip); the dynamics GPs use 64-particle tiles
   // (their class-grouped tile starts are computed on the device in 64s, pf_kernels.hip)
   // (above d = 12 the 32x512 shape's registers spill; 64x512 (8 waves) is the best of the
-  // others there: config 5, d = 16, 0.79 of FP64 peak vs 0.70 for 64x256)
-  TileGeo obs_geo = d <= 12 ? kGeo32x512 : kGeo64x512, dyn_geo = kGeo64x256;
+  // others there: config 5, d = 16, 0.79 of FP64 peak vs 0.70 for 64x256).  The dynamics
+  // GPs run few rows (ancestor de-duplication) against short triangular blocks: their time
+  // is the K loop of the heaviest blocks, which 32-particle tiles halve (32x256).
+  TileGeo obs_geo = d <= 12 ? kGeo32x512 : kGeo64x512, dyn_geo = kGeo32x256;
   switch (desc->tile_shape) {
     case GPMDM_TILE_DEFAULT: break;
-    case GPMDM_TILE_64x256: obs_geo = kGeo64x256; break;
+    case GPMDM_TILE_64x256: obs_geo = dyn_geo = kGeo64x256; break;
     case GPMDM_TILE_64x512: obs_geo = dyn_geo = kGeo64x512; break;
     case GPMDM_TILE_32x512: obs_geo = kGeo32x512; break;
     default: delete m; return fail(GPMDM_E_INVALID, "tile_shape must be one of GPMDM_TILE_*");
@@ -670,6 +672,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   ScanArgs sc{};
   sc.nb = pf->nb;
   sc.C = C;
+  sc.pt = m->dyn[0].geo.pt();
   sc.lo = pf->lo;
   sc.hi = pf->hi;
   sc.blockcounts = pf->blockcounts;
@@ -698,6 +701,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
     la.hi = pf->hi;
     la.nb = pf->nb;
     la.C = C;
+    la.pt = m->dyn[0].geo.pt();
     la.perm = pf->perm;
     la.cls_new = pf->cls_new;
     la.anc = pf->ridx;
@@ -752,8 +756,8 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
         njm = std::max(njm, m->dyn[c0 + k].n_j);
       }
       tp.n_seg = ns;
-      tp.geo = m->dyn[c0].geo;           // 64-particle tiles (device-side tile starts)
-      tp.tiles_ub = (int)(cdiv(nl, kPT) + ns);
+      tp.geo = m->dyn[c0].geo;           // tile starts computed on the device in units of pt
+      tp.tiles_ub = (int)(cdiv(nl, tp.geo.pt()) + ns);
       tp.n_j_max = njm;
       if (pf->dedup) {                  // one row per (ancestor, class) leader
         tp.seg_pos_begin = pf->lseg_begin() + c0;

@@ -655,9 +655,11 @@ template <int DI>
 void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
   const dim3 grid((unsigned)(p.n_j_max * p.tiles_ub));
   const TileGeo g = p.geo;
-  if (dyn) {   // dynamics GPs: 64-particle tiles only (class tile starts are in 64s)
+  if (dyn) {
     if (g.nw == 8)
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 8>), grid, dim3(512), 0, stream, p);
+    else if (g.mt == 2)
+      hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 2, 4>), grid, dim3(256), 0, stream, p);
     else
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4>), grid, dim3(256), 0, stream, p);
   } else if (g.mt == 2) {

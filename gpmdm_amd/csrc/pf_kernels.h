@@ -38,6 +38,7 @@ struct SwitchArgs {
 
 struct ScanArgs {
   int nb, C;
+  int pt;                         // particles per dynamics-GP tile (seg_tile_start unit)
   long long lo, hi;               // this rank's particle slice
   const int* blockcounts;
   const int* cls_new;
@@ -63,6 +64,7 @@ struct GroupArgs {
 struct LeadArgs {
   long long P, Pf, lo, hi;
   int nb, C;
+  int pt;                         // particles per dynamics-GP tile
   const int* perm;                // grouped position -> particle
   const int* cls_new;
   const int* anc;

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(1024) void k_scan_counts(ScanArgs a) {
       a.seg_out_base[c] = ob;
       a.seg_tile_start[c] = ts;
       ob += e0 - b0;
-      ts += (e0 - b0 + kPT - 1) / kPT;
+      ts += (e0 - b0 + a.pt - 1) / a.pt;
       cs += tot[c];
     }
     a.class_start[a.C] = cs;
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(1024) void k_lead_tables(LeadArgs a) {
       a.lseg_pos_end[c] = e0;
       a.lseg_out_base[c] = b0;
       a.lseg_tile_start[c] = ts;
-      ts += (e0 - b0 + kPT - 1) / kPT;
+      ts += (e0 - b0 + a.pt - 1) / a.pt;
     }
     a.lseg_tile_start[a.C] = ts;
   }
