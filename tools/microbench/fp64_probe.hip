@@ -99,7 +99,7 @@ static float time_kernel(F launch, int reps = 5) {
   return best;
 }
 
-int main() {
+int main(int argc, char** argv) {
   hipDeviceProp_t prop; CK(hipGetDeviceProperties(&prop, 0));
   int ncu = prop.multiProcessorCount;
   printf("device %s CUs %d clock %d kHz\n", prop.gcnArchName, ncu, prop.clockRate);
@@ -165,6 +165,21 @@ int main() {
     float ms = time_kernel([&] { k_exp_rate<<<blocks, 256>>>(dout, iters, 1.0); });
     double n = (double)blocks * 256 * iters * 4;
     printf("exp(double) waves/CU=%d : %.3f ms  %.2f Gexp/s\n", wpc, ms, n / ms / 1e6);
+  }
+  // Sustained rate (argv[1] = seconds, e.g. 0.5): one long launch at 8 waves/CU, so power
+  // management has settled on its clock -- the practical ceiling for a multi-ms kernel.
+  if (argc > 1) {
+    const double secs = atof(argv[1]);
+    const int blocks = ncu * 2;
+    const int long_iters = (int)(iters * secs / 0.87e-3);
+    hipEvent_t a0, a1; CK(hipEventCreate(&a0)); CK(hipEventCreate(&a1));
+    CK(hipEventRecord(a0));
+    k_mfma_rate<8><<<blocks, 256>>>(dout, long_iters, 1.0);
+    CK(hipEventRecord(a1));
+    CK(hipEventSynchronize(a1));
+    float ms; CK(hipEventElapsedTime(&ms, a0, a1));
+    const double flops = (double)blocks * 4 * long_iters * 8 * 2.0 * 16 * 16 * 4;
+    printf("sustained mfma_f64 16x16x4 waves/CU=8, one %.0f ms launch: %.2f TFLOP/s\n", ms, flops / ms / 1e9);
   }
   return 0;
 }
