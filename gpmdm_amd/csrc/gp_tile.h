@@ -207,6 +207,7 @@ __device__ __forceinline__ double exp2_64m(double t, const double* tab) {
 //   bit 11: A/B -- no vmcnt(0) drain after the prologue
 //   bit 12: generation split across the sub-steps + sched_group_barrier MFMA/VALU interleave
 //   bit 13: generation split across the sub-steps (no sched_group_barrier)
+//   bit 14: A/B -- B fragments by flat global loads instead of buffer loads
 //
 // Geometry: NW waves; each wave owns MT x NTW tiles of 16 x 16 (16 MT particles x 16 NTW
 // columns), so a workgroup covers PT = 16 MT particles x NB = 16 NTW NW columns.  K* costs
@@ -316,7 +317,12 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   }
   long long boff = 0;                                       // fragments of blocks < J
   for (int jj = 0; jj < J; ++jj) boff += (long long)ksteps(block_kmax(jj, n_rows, NB, coff)) * FS;
-  const double* __restrict__ Bw = Bf + boff + w * WS + lane * 2;
+  // B addressing: a buffer resource on this wave's share of block J (SGPRs), a per-lane
+  // byte offset (VGPR, constant) and a wave-uniform K-step offset (SGPR), so the K loop
+  // spends no VALU on 64-bit address arithmetic.
+  const double* __restrict__ Bw = Bf + boff + w * WS;
+  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc((void*)Bw, (short)0, 0x7fffffff, 0x00020000);
+  const unsigned lane_off = (unsigned)lane * 16u;
   // last K-step this wave multiplies (kend is non-decreasing over the real tiles; no
   // runtime indexing of kend[], which would put it in scratch)
   int kmaxw = 0;
@@ -391,12 +397,24 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       for (int q = 0; q < NTW; ++q) bb[kk * NTW + q] = bb[kk * NTW + q] * 0.999 + 1e-3 * (ks & 1);
       return;
     }
-    const double* src = Bw + (long long)(ks < ks_last ? ks : ks_last) * FS + kk * (64 * NTW);
+    const int kc = ks < ks_last ? ks : ks_last;
+    if constexpr ((VAR & 16384) != 0) {          // A/B: flat global loads (64-bit VGPR addresses)
+      const double* src = Bw + (long long)kc * FS + kk * (64 * NTW) + lane * 2;
+#pragma unroll
+      for (int h = 0; h < NTW / 2; ++h) {
+        const double2 x = *reinterpret_cast<const double2*>(src + 128 * h);
+        bb[kk * NTW + 2 * h + 0] = x.x;
+        bb[kk * NTW + 2 * h + 1] = x.y;
+      }
+      return;
+    }
 #pragma unroll
     for (int h = 0; h < NTW / 2; ++h) {
-      const double2 x = *reinterpret_cast<const double2*>(src + 128 * h);
-      bb[kk * NTW + 2 * h + 0] = x.x;
-      bb[kk * NTW + 2 * h + 1] = x.y;
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      const int soff = (kc * FS + kk * (64 * NTW) + 128 * h) * 8;     // bytes, wave-uniform
+      const v4u x = __builtin_amdgcn_raw_buffer_load_b128(brsrc, lane_off, soff, 0);
+      bb[kk * NTW + 2 * h + 0] = __builtin_bit_cast(double, (unsigned long long)x.x | ((unsigned long long)x.y << 32));
+      bb[kk * NTW + 2 * h + 1] = __builtin_bit_cast(double, (unsigned long long)x.z | ((unsigned long long)x.w << 32));
     }
   };
   auto store = [&](int buf, const double (&v)[GV]) {
@@ -550,24 +568,99 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   // ---- epilogue --------------------------------------------------------------------
   // C/D layout of v_mfma_f64_16x16x4_f64: lane l, reg r -> row (l>>4) + 4r, col l&15.
   const bool has_r = J * NB - coff < n_rows;
+  const bool has_m = (J + 1) * NB - coff > n_rows;            // block holds mean columns
+  const bool fused = prm.spart != nullptr;
+  if (has_m) {
+    if (!fused) {
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
+        if (jm >= 0 && jm < n_m) {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int p = pos0 + mt * 16 + lk + 4 * r;
+              if (p < pos_end) prm.mu[(long long)(out_base + p) * prm.ld_mu + jm] = acc[mt][nt][r];
+            }
+        }
+      }
+    } else {
+      // sum_j (z_j - mu_j)^2 lam2_j over this block's mean columns (gpmdm_pf.py:188-192 with
+      // var_j = vc / lam2_j factored out; k_obs_ll finishes the likelihood).  A tile whose
+      // particles share one filter (always, for a single filter) reads z_j once per column.
+      const int Pf = (int)prm.Pf;
+      const int f0 = pos0 / Pf, f1 = (min(pos0 + PT, pos_end) - 1) / Pf;   // wave-uniform
+      double ss[MT][4];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ss[mt][r] = 0.0;
+#pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
+        if (jm >= 0 && jm < n_m) {
+          const double lam = prm.lam2[jm];
+          if (f0 == f1) {
+            const double zj = prm.z[(long long)f0 * n_m + jm];
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const double t = zj - acc[mt][nt][r];
+                ss[mt][r] = fma(t * t, lam, ss[mt][r]);
+              }
+          } else {
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                int p = pos0 + mt * 16 + lk + 4 * r;
+                p = p < pos_end ? p : pos0;
+                const double t = prm.z[(long long)(p / Pf) * n_m + jm] - acc[mt][nt][r];
+                ss[mt][r] = fma(t * t, lam, ss[mt][r]);
+              }
+          }
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double v = ss[mt][r];
+          v += __shfl_xor(v, 1);
+          v += __shfl_xor(v, 2);
+          v += __shfl_xor(v, 4);
+          v += __shfl_xor(v, 8);
+          if (li == 0) sred[w][mt * 16 + lk + 4 * r] = v;
+        }
+    }
+    // mean columns do not enter the quadratic form
+#pragma unroll
+    for (int nt = 0; nt < NTW; ++nt) {
+      const int col = J * NB + 16 * (NW * nt + w) + li - coff;
+      if (col >= n_rows) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = (d4){0.0, 0.0, 0.0, 0.0};
+      }
+    }
+  }
   if (has_r) {
+    // Sum of squares over the block's R columns.  Front-padding columns (col < 0) have
+    // B = 0, so V = 0 there: no mask (mean columns were zeroed above).
     double qs[MT][4];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        double s = 0.0;
+        double v = 0.0;
 #pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) {
-          const double x = acc[mt][nt][r];
-          const int col = J * NB + 16 * (NW * nt + w) + li - coff;
-          if (col >= 0 && col < n_rows) s = fma(x, x, s);
-        }
-        s += __shfl_xor(s, 1);
-        s += __shfl_xor(s, 2);
-        s += __shfl_xor(s, 4);
-        s += __shfl_xor(s, 8);
-        qs[mt][r] = s;
+        for (int nt = 0; nt < NTW; ++nt) v = fma(acc[mt][nt][r], acc[mt][nt][r], v);
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        v += __shfl_xor(v, 4);
+        v += __shfl_xor(v, 8);
+        qs[mt][r] = v;
       }
     if (li == 0) {
 #pragma unroll
@@ -575,59 +668,6 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
 #pragma unroll
         for (int r = 0; r < 4; ++r) qred[w][mt * 16 + lk + 4 * r] = qs[mt][r];
     }
-  }
-  const bool has_m = (J + 1) * NB - coff > n_rows;            // block holds mean columns
-  const bool fused = prm.spart != nullptr;
-  if (has_m && !fused) {
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-      const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
-      if (jm >= 0 && jm < n_m) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int p = pos0 + mt * 16 + lk + 4 * r;
-            if (p < pos_end) prm.mu[(long long)(out_base + p) * prm.ld_mu + jm] = acc[mt][nt][r];
-          }
-      }
-    }
-  }
-  if (has_m && fused) {
-    // sum_j (z_j - mu_j)^2 lam2_j over this block's mean columns (gpmdm_pf.py:188-192 with
-    // var_j = vc / lam2_j factored out; k_obs_ll finishes the likelihood)
-    double ss[MT][4];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ss[mt][r] = 0.0;
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-      const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
-      if (jm >= 0 && jm < n_m) {
-        const double lam = prm.lam2[jm];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            int p = pos0 + mt * 16 + lk + 4 * r;
-            p = p < pos_end ? p : pos0;
-            const double t = prm.z[(p / prm.Pf) * n_m + jm] - acc[mt][nt][r];
-            ss[mt][r] = fma(t * t, lam, ss[mt][r]);
-          }
-      }
-    }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double s = ss[mt][r];
-        s += __shfl_xor(s, 1);
-        s += __shfl_xor(s, 2);
-        s += __shfl_xor(s, 4);
-        s += __shfl_xor(s, 8);
-        if (li == 0) sred[w][mt * 16 + lk + 4 * r] = s;
-      }
   }
   if (has_r || (has_m && fused)) {
     __syncthreads();
