@@ -171,7 +171,12 @@ def main():
 
     from gpmdm_amd import GPMDM_PF, build
     from gpmdm_amd import _lib
-    build.build()
+    # one builder per node (a no-op when the in-tree library is current); the other ranks
+    # wait, so concurrent ranks never write the same objects
+    if local == 0:
+        build.build()
+    if dist is not None:
+        dist.barrier()
     _lib.load()
     t_setup = time.perf_counter()
     model, data = build_model(device)

@@ -208,6 +208,7 @@ __device__ __forceinline__ double exp2_64m(double t, const double* tab) {
 //   bit 12: generation split across the sub-steps + sched_group_barrier MFMA/VALU interleave
 //   bit 13: generation split across the sub-steps (no sched_group_barrier)
 //   bit 14: A/B -- B fragments by flat global loads instead of buffer loads
+//   bit 15: A/B -- one barrier per K-step (2-slot rings) instead of one per two K-steps
 //
 // Geometry: NW waves; each wave owns MT x NTW tiles of 16 x 16 (16 MT particles x 16 NTW
 // columns), so a workgroup covers PT = 16 MT particles x NB = 16 NTW NW columns.  K* costs
@@ -239,8 +240,18 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   constexpr int RW = DI + 1;                                 // row record: Xs[DI], |Xs|^2
   constexpr int NRV = kBK * RW;                              // row values per K-step
   constexpr int RPT = (NRV + NT - 1) / NT;                   // row values per thread
-  __shared__ double As[2][kBK][LDA];
-  __shared__ double RX[2][RPT * NT];                          // row records, then padding
+  // LDS rings.  SYNC2 (default): one barrier per two K-steps (after odd ones), K* generated
+  // two K-steps ahead into 4 slots, rows staged four ahead into 4 slots -- a slot is
+  // rewritten only after a barrier that follows its last read, and read only after a
+  // barrier that follows its write.  VAR bit 15 (A/B): one barrier per K-step, K* one ahead
+  // into 2 slots, rows two ahead into 2 slots.  (obs tile -0.6%, tile_bench)
+  constexpr bool SYNC2 = (VAR & 32768) == 0;
+  constexpr int ASL = SYNC2 ? 4 : 2;                         // K* slots
+  constexpr int RXS = SYNC2 ? 4 : 2;                         // row-record slots
+  constexpr int LOOK = SYNC2 ? 2 : 1;                        // generation lookahead (K-steps)
+  constexpr int RA = SYNC2 ? 4 : 2;                          // row staging lookahead
+  __shared__ double As[ASL][kBK][LDA];
+  __shared__ double RX[RXS][RPT * NT];                        // row records, then padding
   constexpr bool E256 = (VAR & 256) != 0;
   constexpr double kScale = E256 ? kLog2eX256 : kLog2eX64;
   __shared__ double tab[E256 ? 256 : 64];
@@ -362,7 +373,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   // |Xs|^2 = kPadSq, so the exponent of a padding row is ~ -1e300 and its kernel value is
   // exactly 0 (v_cvt_i32_f64 saturates, ldexp underflows): no masking per value.
   auto gen_one = [&](int ks, int s) -> double {
-    const int rb = ks & 1;
+    const int rb = ks & (RXS - 1);
     const int r = g + NG * s;
     const int i = ks * kBK + r;                            // training row
     const double* row = &RX[rb][r * RW];
@@ -439,12 +450,12 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   constexpr bool SPLIT = (VAR & (4096 | 8192)) != 0;
   auto full_step = [&](auto t0c, auto t1c, int ks, double (&bb)[4 * NTW]) {
     constexpr int T0 = decltype(t0c)::value, T1c = decltype(t1c)::value;
-    const int buf = ks & 1;
+    const int buf = ks & (ASL - 1);
     double v[GV];
     double rr[RPT];
     if constexpr (!(VAR & 16)) {
-      load_rows(ks + 2, rr);
-      if constexpr (!SPLIT) gen(ks + 1, v);
+      load_rows(ks + RA, rr);
+      if constexpr (!SPLIT) gen(ks + LOOK, v);
     }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
@@ -464,7 +475,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
         if (kk % PER == 0) {
 #pragma unroll
           for (int s = 0; s < GV; ++s)
-            if (s == kk / PER) v[s] = gen_one(ks + 1, s);
+            if (s == kk / PER) v[s] = gen_one(ks + LOOK, s);
         }
       }
       if constexpr ((VAR & 4096) != 0) {
@@ -478,10 +489,12 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       loadB_part(ks + 1, kk, bb);
     }
     if constexpr (!(VAR & 16)) {
-      store(buf ^ 1, v);
-      store_rows(buf, rr);
+      store((ks + LOOK) & (ASL - 1), v);
+      store_rows((ks + RA) & (RXS - 1), rr);
     }
-    if constexpr (!(VAR & 8)) __syncthreads();
+    if constexpr (!(VAR & 8)) {
+      if (!SYNC2 || (ks & 1)) __syncthreads();
+    }
   };
 
   double bb[4 * NTW];
@@ -491,16 +504,20 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   }
   {
     double rr[RPT];
-    load_rows(0, rr);
-    store_rows(0, rr);
-    load_rows(1, rr);
-    store_rows(1, rr);
+#pragma unroll
+    for (int j = 0; j < RA; ++j) {
+      load_rows(j, rr);
+      store_rows(j, rr);
+    }
   }
-  __syncthreads();                                           // table + rows of steps 0, 1
+  __syncthreads();                                           // table + rows of steps 0 .. RA-1
   {
     double v[GV];
-    gen(0, v);
-    store(0, v);
+#pragma unroll
+    for (int j = 0; j < LOOK; ++j) {
+      gen(j, v);
+      store(j, v);
+    }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) loadB_part(0, kk, bb);
   }
@@ -526,11 +543,11 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   for (; ks < nks; ++ks) {
     double v[GV];
     double rr[RPT];
-    load_rows(ks + 2, rr);
-    gen(ks + 1, v);
-    store((ks + 1) & 1, v);
-    store_rows(ks & 1, rr);
-    __syncthreads();
+    load_rows(ks + RA, rr);
+    gen(ks + LOOK, v);
+    store((ks + LOOK) & (ASL - 1), v);
+    store_rows((ks + RA) & (RXS - 1), rr);
+    if (!SYNC2 || (ks & 1)) __syncthreads();
   }
 
   if constexpr (DYN) {
