@@ -84,9 +84,10 @@ __host__ __device__ inline int col_offset(int n_cols, int nb) {
   return r ? ((nb - r) / 16) * 16 : 0;
 }
 __host__ __device__ inline int ksteps(int kmax) { return (kmax + kBK - 1) / kBK; }
-// Rows the Xs / Xsq arrays are padded to: the K loop stages rows up to four K-steps past the
-// last one it multiplies.  Padding rows have Xs = 0 and |Xs|^2 = kPadSq (kernel value 0).
-__host__ __device__ inline int row_cap(int n_rows) { return (ksteps(n_rows) + 4) * kBK; }
+// Rows the Xs / Xsq arrays are padded to: the K loop stages rows up to eight K-steps past
+// the last one it multiplies (A/B variants included).  Padding rows have Xs = 0 and
+// |Xs|^2 = kPadSq (kernel value 0).
+__host__ __device__ inline int row_cap(int n_rows) { return (ksteps(n_rows) + 8) * kBK; }
 constexpr double kPadSq = 1e300;
 // Dynamics linear kernel: K=4 MFMA sub-steps covering the d+1 rows of H.
 __host__ __device__ inline int lin_substeps(int d) { return (d + 1 + 3) / 4; }

@@ -209,6 +209,7 @@ __device__ __forceinline__ double exp2_64m(double t, const double* tab) {
 //   bit 13: generation split across the sub-steps (no sched_group_barrier)
 //   bit 14: A/B -- B fragments by flat global loads instead of buffer loads
 //   bit 15: A/B -- one barrier per K-step (2-slot rings) instead of one per two K-steps
+//   bit 16: A/B -- one barrier per four K-steps (8-slot rings)
 //
 // Geometry: NW waves; each wave owns MT x NTW tiles of 16 x 16 (16 MT particles x 16 NTW
 // columns), so a workgroup covers PT = 16 MT particles x NB = 16 NTW NW columns.  K* costs
@@ -240,16 +241,20 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   constexpr int RW = DI + 1;                                 // row record: Xs[DI], |Xs|^2
   constexpr int NRV = kBK * RW;                              // row values per K-step
   constexpr int RPT = (NRV + NT - 1) / NT;                   // row values per thread
-  // LDS rings.  SYNC2 (default): one barrier per two K-steps (after odd ones), K* generated
+  // LDS rings.  Default: one barrier per two K-steps (after odd ones), K* generated
   // two K-steps ahead into 4 slots, rows staged four ahead into 4 slots -- a slot is
   // rewritten only after a barrier that follows its last read, and read only after a
   // barrier that follows its write.  VAR bit 15 (A/B): one barrier per K-step, K* one ahead
-  // into 2 slots, rows two ahead into 2 slots.  (obs tile -0.6%, tile_bench)
-  constexpr bool SYNC2 = (VAR & 32768) == 0;
-  constexpr int ASL = SYNC2 ? 4 : 2;                         // K* slots
-  constexpr int RXS = SYNC2 ? 4 : 2;                         // row-record slots
-  constexpr int LOOK = SYNC2 ? 2 : 1;                        // generation lookahead (K-steps)
-  constexpr int RA = SYNC2 ? 4 : 2;                          // row staging lookahead
+  // into 2 slots, rows two ahead into 2 slots.  (obs tile -0.6%, tile_bench; four K-steps
+  // per barrier gains nothing more and doubles the LDS rings)
+  // General rule for S K-steps per barrier (after steps with ks % S == S-1): lookahead
+  // LOOK >= S, K* slots >= LOOK + S, row lookahead RA >= LOOK + S, row slots >= RA - LOOK + S.
+  // VAR bit 16 (A/B): S = 4.
+  constexpr int SB = (VAR & 32768) ? 1 : ((VAR & 65536) ? 4 : 2);   // K-steps per barrier
+  constexpr int ASL = 2 * SB;                                // K* slots
+  constexpr int RXS = 2 * SB;                                // row-record slots
+  constexpr int LOOK = SB;                                   // generation lookahead (K-steps)
+  constexpr int RA = 2 * SB;                                 // row staging lookahead
   __shared__ double As[ASL][kBK][LDA];
   __shared__ double RX[RXS][RPT * NT];                        // row records, then padding
   constexpr bool E256 = (VAR & 256) != 0;
@@ -493,7 +498,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       store_rows((ks + RA) & (RXS - 1), rr);
     }
     if constexpr (!(VAR & 8)) {
-      if (!SYNC2 || (ks & 1)) __syncthreads();
+      if (ks % SB == SB - 1) __syncthreads();
     }
   };
 
@@ -547,7 +552,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     gen(ks + LOOK, v);
     store((ks + LOOK) & (ASL - 1), v);
     store_rows((ks + RA) & (RXS - 1), rr);
-    if (!SYNC2 || (ks & 1)) __syncthreads();
+    if (ks % SB == SB - 1) __syncthreads();
   }
 
   if constexpr (DYN) {

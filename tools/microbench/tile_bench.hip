@@ -77,8 +77,8 @@ int main(int argc, char** argv) {
   typedef void (*L)(const TileParams&, hipStream_t);
   struct V { L fn; int pi; const char* name; };
   V vars[] = {{launch_var<32768, 4, 2, 8>, 2, "32x512 sync every K-step"}, {launch_var<0, 4, 2, 8>, 2, "32x512 sync every 2 K-steps"},
-              {launch_var<8, 4, 2, 8>, 2, "32x512 no barrier (ablation)"},
-              {launch_var<32768, 4>, 0, "64x256 sync every K-step"}, {launch_var<0, 4>, 0, "64x256 sync every 2 K-steps"}};
+              {launch_var<65536, 4, 2, 8>, 2, "32x512 sync every 4 K-steps"}, {launch_var<8, 4, 2, 8>, 2, "32x512 no barrier (ablation)"},
+              {launch_var<0, 4>, 0, "64x256 sync every 2 K-steps"}, {launch_var<65536, 4>, 0, "64x256 sync every 4 K-steps"}};
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
   std::vector<std::vector<float>> t(NV);
   for (int v = 0; v < NV; ++v) vars[v].fn(pp[vars[v].pi], s);
