@@ -210,6 +210,7 @@ __device__ __forceinline__ double exp2_64m(double t, const double* tab) {
 //   bit 14: A/B -- B fragments by flat global loads instead of buffer loads
 //   bit 15: A/B -- one barrier per K-step (2-slot rings) instead of one per two K-steps
 //   bit 16: A/B -- one barrier per four K-steps (8-slot rings)
+//   bit 17: particle coordinates from LDS in the generation (see PLDS)
 //
 // Geometry: NW waves; each wave owns MT x NTW tiles of 16 x 16 (16 MT particles x 16 NTW
 // columns), so a workgroup covers PT = 16 MT particles x NB = 16 NTW NW columns.  K* costs
@@ -261,6 +262,10 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   constexpr double kScale = E256 ? kLog2eX256 : kLog2eX64;
   __shared__ double tab[E256 ? 256 : 64];
   __shared__ double qred[NW][PT];
+  // VAR bit 17: particle coordinates read from LDS in the generation instead of held in
+  // VGPRs (frees 2 d VGPRs: large d on the 32-particle shapes)
+  constexpr bool PLDS = (VAR & 131072) != 0;
+  __shared__ double PA[PLDS ? PT : 1][PLDS ? DI + 1 : 1];
   __shared__ double sred[NW][PT];
 
   const int tid = threadIdx.x;
@@ -313,6 +318,12 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     a2[j] = (2.0 * kScale) * xs;
   }
   asq *= kScale;                                           // |x / l|^2 (64 / ln 2)
+  if constexpr (PLDS) {
+    if (g == 0) {
+#pragma unroll
+      for (int j = 0; j < DI; ++j) PA[m][j] = a2[j];
+    }
+  }
 
   // ---- K ranges ------------------------------------------------------------------
   const int nks = (VAR & 128) ? ksteps(n_rows) : ksteps(block_kmax(J, n_rows, NB, coff));
@@ -390,7 +401,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     } else {
       x = -(asq + row[DI]);
 #pragma unroll
-      for (int j = 0; j < DI; ++j) x = fma(a2[j], row[j], x);
+      for (int j = 0; j < DI; ++j) x = fma(PLDS ? PA[m][j] : a2[j], row[j], x);
     }
     double val;
     if constexpr (VAR & 2) val = fma(x, 1e-3, 1.0);

@@ -14,14 +14,18 @@ using namespace gpmdm;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
 
+#ifndef TB_D
+#define TB_D 3
+#endif
 template <int VAR, int NW, int MT = 4, int NTW = 4>
 void launch_var(const TileParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((k_gp_tile<3, false, VAR, NW, MT, NTW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, p);
+  hipLaunchKernelGGL((k_gp_tile<TB_D, false, VAR, NW, MT, NTW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, p);
 }
 
 int main(int argc, char** argv) {
-  const int N = 2000, D = 62, d = 3;
+  // argv: P N D (defaults: the config-2 observation GP); d = TB_D at compile time
   const int P = argc > 1 ? atoi(argv[1]) : 100000;
+  const int N = argc > 2 ? atoi(argv[2]) : 2000, D = argc > 3 ? atoi(argv[3]) : 62, d = TB_D;
   std::mt19937_64 rng(1);
   std::normal_distribution<double> nd(0.0, 1.0);
   const int cap = row_cap(N);   // padded like capi.hip::build_image
@@ -34,7 +38,7 @@ int main(int argc, char** argv) {
   for (auto& v : hX) v = 2.0 * nd(rng);
   double *Xs, *Xsq, *X, *q, *mu;
   CK(hipMalloc(&Xs, cap * d * 8)); CK(hipMalloc(&Xsq, cap * 8));
-  CK(hipMalloc(&X, (size_t)P * d * 8)); CK(hipMalloc(&q, (size_t)P * 32 * 8)); CK(hipMalloc(&mu, (size_t)P * D * 8));
+  CK(hipMalloc(&X, (size_t)P * d * 8)); CK(hipMalloc(&q, (size_t)P * (N + D + 4095) / 256 * 8)); CK(hipMalloc(&mu, (size_t)P * D * 8));
     CK(hipMemcpy(Xs, hXs.data(), cap * d * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(Xsq, hXsq.data(), cap * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(X, hX.data(), (size_t)P * d * 8, hipMemcpyHostToDevice));
@@ -76,9 +80,14 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   typedef void (*L)(const TileParams&, hipStream_t);
   struct V { L fn; int pi; const char* name; };
-  V vars[] = {{launch_var<32768, 4, 2, 8>, 2, "32x512 sync every K-step"}, {launch_var<0, 4, 2, 8>, 2, "32x512 sync every 2 K-steps"},
-              {launch_var<65536, 4, 2, 8>, 2, "32x512 sync every 4 K-steps"}, {launch_var<8, 4, 2, 8>, 2, "32x512 no barrier (ablation)"},
-              {launch_var<0, 4>, 0, "64x256 sync every 2 K-steps"}, {launch_var<65536, 4>, 0, "64x256 sync every 4 K-steps"}};
+#if TB_D > 12
+  V vars[] = {{launch_var<0, 4>, 0, "64x256"}, {launch_var<0, 8>, 1, "64x512 (NW8)"},
+              {launch_var<0, 4, 2, 8>, 2, "32x512 (VGPR coords)"}, {launch_var<131072, 4, 2, 8>, 2, "32x512 LDS coords"},
+              {launch_var<131072, 8>, 1, "64x512 LDS coords"}};
+#else
+  V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512"}, {launch_var<131072, 4, 2, 8>, 2, "32x512 LDS coords"},
+              {launch_var<0, 4>, 0, "64x256"}};
+#endif
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
   std::vector<std::vector<float>> t(NV);
   for (int v = 0; v < NV; ++v) vars[v].fn(pp[vars[v].pi], s);
