@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -301,8 +302,9 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
   // (above d = 12 the 32x512 shape's registers spill; 64x512 (8 waves) is the best of the
   // others there: config 5, d = 16, 0.79 of FP64 peak vs 0.70 for 64x256).  The dynamics
   // GPs run few rows (ancestor de-duplication) against short triangular blocks: their time
-  // is the K loop of the heaviest blocks, which 32-particle tiles halve (32x256).
-  TileGeo obs_geo = d <= 12 ? kGeo32x512 : kGeo64x512, dyn_geo = kGeo32x256;
+  // is the K loop of the heaviest blocks, which narrow particle tiles shorten (64 -> 32 ->
+  // 16 particles: dyn GEMM 0.215 -> 0.163 -> 0.150 ms per step at config 2).
+  TileGeo obs_geo = d <= 12 ? kGeo32x512 : kGeo64x512, dyn_geo = kGeo16x256;
   switch (desc->tile_shape) {
     case GPMDM_TILE_DEFAULT: break;
     case GPMDM_TILE_64x256: obs_geo = dyn_geo = kGeo64x256; break;

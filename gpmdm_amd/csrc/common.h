@@ -14,7 +14,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 //   (particles x training rows) is generated on the fly and B = [R | M] is the extended
 //   weight matrix stored in MFMA-fragment order (each wave owns MT x NTW tiles of 16 x 16).
 //   Shapes: 64x256 (NW 4, MT 4, NTW 4), 64x512 (8, 4, 4), 32x512 (4, 2, 8; the observation
-//   GP default for d <= 12) and 32x256 (4, 2, 4; the dynamics GP default).
+//   GP default for d <= 12), 32x256 (4, 2, 4) and 16x256 (4, 1, 4; the dynamics GP default).
 // ---------------------------------------------------------------------------------
 constexpr int kBK = 16;           // training rows per K-step (4 x K=4 MFMA sub-steps)
 constexpr int kMaxSeg = 8;        // segments (classes) per launch
@@ -31,6 +31,7 @@ constexpr TileGeo kGeo64x256{4, 4, 4};
 constexpr TileGeo kGeo64x512{8, 4, 4};
 constexpr TileGeo kGeo32x512{4, 2, 8};
 constexpr TileGeo kGeo32x256{4, 2, 4};
+constexpr TileGeo kGeo16x256{4, 1, 4};
 
 struct SegDesc {                  // one GP: the observation GP, or the class-c dynamics GP
   const double* Xs;               // n_rows x d : training inputs / lengthscales

@@ -228,7 +228,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 template <int DI, bool DYN, int VAR = 0, int NW = 4, int MT = 4, int NTW = 4>
 __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
-  static_assert(MT == 2 || MT == 4, "MT");
+  static_assert(MT == 1 || MT == 2 || MT == 4, "MT");
   static_assert(NTW == 4 || NTW == 8, "NTW");
   constexpr int NT = 64 * NW;                                // threads
   constexpr int PT = 16 * MT;                                // particles per tile
@@ -733,6 +733,8 @@ void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 8>), grid, dim3(512), 0, stream, p);
     else if (g.mt == 2)
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 2, 4>), grid, dim3(256), 0, stream, p);
+    else if (g.mt == 1)
+      hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 1, 4>), grid, dim3(256), 0, stream, p);
     else
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4>), grid, dim3(256), 0, stream, p);
   } else if (g.mt == 2) {

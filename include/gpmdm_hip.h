@@ -57,7 +57,7 @@ typedef struct gpmdm_pf* gpmdm_pf_t;
  */
 /* GP-tile workgroup shapes (particles x columns of K* B per workgroup).  The default runs
  * the observation GP as 32x512 (d <= 12) or 64x512 (d > 12) and the dynamics GPs as
- * 64x256; an explicit 64x512 applies to both. */
+ * 16x256; an explicit 64x256 or 64x512 applies to both. */
 enum {
   GPMDM_TILE_DEFAULT = 0,
   GPMDM_TILE_64x256 = 1,
