@@ -207,6 +207,7 @@ struct gpmdm_pf {
   int *cls = nullptr, *cls_new = nullptr, *perm = nullptr, *ridx = nullptr;
   int *blockcounts = nullptr, *blockoff = nullptr, *small = nullptr;   // small: class tables
   int *obs_tab = nullptr;
+  int* guide = nullptr;             // F x (GB + 3) inverse-CDF guide table
   // ancestor de-duplication: owner/slot are C x P keyed by (class, ancestor)
   unsigned* owner = nullptr;
   int *slot = nullptr, *lflag = nullptr, *lblock = nullptr, *ltab = nullptr, *lperm = nullptr;
@@ -239,7 +240,7 @@ struct gpmdm_pf {
                     e, local, blocksum, blockoffw, total, cum, partials, readout};
     for (double* p : ds) dfree(p);
     int* is[] = {cls, cls_new, perm, ridx, blockcounts, blockoff, small, obs_tab,
-                 slot, lflag, lblock, ltab, lperm};
+                 slot, lflag, lblock, ltab, lperm, guide};
     for (int* p : is) dfree(p);
     dfree(gmax);
     dfree(owner);
@@ -526,6 +527,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   ALLOC(blockoffw, F * pf->nbf);
   ALLOC(total, F);
   ALLOC(cum, P);
+  ALLOC(guide, guide_buckets_used(Pf) > 0 ? F * (guide_buckets(Pf) + 3) : 1);
   ALLOC(partials, F * pf->nbf * (C + 1 + d));
   ALLOC(readout, F * (C + d + 1));
 #undef ALLOC
@@ -585,6 +587,8 @@ static ResampleArgs resample_args(gpmdm_pf* pf) {
   ra.ridx = pf->ridx;
   ra.partials = pf->partials;
   ra.readout = pf->readout;
+  ra.guide = pf->guide;
+  ra.GB = guide_buckets_used(pf->Pf);   // 0: plain search
   return ra;
 }
 

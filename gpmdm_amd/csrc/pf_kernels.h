@@ -157,7 +157,17 @@ struct ResampleArgs {
   int* ridx;                      // in-filter source index of each slot
   double* partials;               // F x nb x (C + 1 + d)
   double* readout;                // per filter: C posterior, d mean, 1 likelihood sum
+  int* guide;                     // F x (GB + 3): guide[b] = first i with cum[i] >= b / GB
+  long long GB;                   // guide buckets per filter
 };
+
+// Guide buckets per filter for the inverse-CDF search (P / 4: a resample search then spans
+// ~4-8 particles instead of all P).  Below kGuideMinP the plain search over [0, P] is
+// cheaper than building the table (P = 100k: 12.7 us plain vs 6.3 + 10.3 us guided;
+// P = 800k: the guided search saves ~35 us per step).
+constexpr long long kGuideMinP = 262144;
+inline long long guide_buckets(long long P) { return P / 4 > 1 ? P / 4 : 1; }
+inline long long guide_buckets_used(long long P) { return P >= kGuideMinP ? guide_buckets(P) : 0; }
 
 struct PackArgs {
   long long n, lo;

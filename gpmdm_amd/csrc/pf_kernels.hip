@@ -17,6 +17,7 @@
 namespace gpmdm {
 
 constexpr int kB = 256;   // threads per block of the O(P) kernels
+constexpr unsigned kMaxNormBlocks = 128;   // blocks per filter of k_norm_max
 
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(kB) void k_switch(SwitchArgs a) {
@@ -370,8 +371,11 @@ __global__ __launch_bounds__(kB) void k_obs_ll(ObsFinishArgs a) {
 __global__ __launch_bounds__(kB) void k_norm_max(NormArgs a) {
   __shared__ double s[kB / 64];
   const long long f = blockIdx.y;
-  const long long p = (long long)blockIdx.x * kB + threadIdx.x;
-  double v = p < a.P ? a.ll[f * a.P + p] : -INFINITY;
+  // grid-stride over the filter's particles: at most kMaxNormBlocks atomics per filter
+  // address (one per block; thousands of same-address atomics serialise at the L2)
+  double v = -INFINITY;
+  for (long long p = (long long)blockIdx.x * kB + threadIdx.x; p < a.P; p += (long long)gridDim.x * kB)
+    v = fmax(v, a.ll[f * a.P + p]);
   v = wave_max(v);
   if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -450,6 +454,23 @@ __global__ __launch_bounds__(kB) void k_cdf(NormArgs a) {
 
 // One thread per output slot s: inverse-CDF search, gather, read-out partials.
 // identity=1 computes the read-outs of the current state without resampling (after init).
+// Guide table for the inverse-CDF search: guide[b] = first i with cum[i] >= b / GB (P if
+// none), for b = 0 .. GB + 2.  The queries b / GB are sorted, so neighbouring threads walk
+// nearly the same binary-search path (cache-friendly, unlike the random uniforms).
+__global__ __launch_bounds__(kB) void k_guide(ResampleArgs a) {
+  const long long f = blockIdx.y;
+  const long long b = (long long)blockIdx.x * kB + threadIdx.x;
+  if (b > a.GB + 2) return;
+  const double t = (double)b / (double)a.GB;
+  const double* cum = a.cum + f * a.P;
+  long long lo = 0, hi = a.P;
+  while (hi - lo > 0) {
+    const long long mid = lo + (hi - lo) / 2;
+    if (cum[mid] < t) lo = mid + 1; else hi = mid;
+  }
+  a.guide[f * (a.GB + 3) + b] = (int)lo;
+}
+
 __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
   __shared__ double red[kB / 64][kMaxReadout];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -484,7 +505,17 @@ __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
         u = u01_co(r.x, r.y);
       }
       const double* cum = a.cum + g0;
-      long long lo = 0, hi = a.P;               // first index with cum >= u
+      // first index with cum >= u (torch's searchsorted), searched between two guide
+      // entries that bracket it: t_lo = (q0 - 1) / GB <= u and t_hi = (q0 + 2) / GB > u for
+      // q0 = floor(u GB) whatever its rounding, so the result is exactly that of a search
+      // over [0, P]
+      long long lo = 0, hi = a.P;
+      if (a.GB > 0) {                           // guided (large P): bracket, then search
+        const int* gd = a.guide + f * (a.GB + 3);
+        const long long q0 = (long long)floor(u * (double)a.GB);
+        lo = gd[q0 - 1 > 0 ? q0 - 1 : 0];
+        hi = gd[q0 + 2 < a.GB + 2 ? q0 + 2 : a.GB + 2];
+      }
       while (hi - lo > 0) {
         const long long mid = lo + (hi - lo) / 2;
         if (cum[mid] < u) lo = mid + 1; else hi = mid;
@@ -597,12 +628,15 @@ void launch_obs_finish(const ObsFinishArgs& a, hipStream_t s) {
 }
 void launch_normalise(const NormArgs& a, hipStream_t s) {
   const dim3 g(nblk(a.P, kB), (unsigned)a.F);
-  hipLaunchKernelGGL(k_norm_max, g, dim3(kB), 0, s, a);
+  const unsigned nbm = nblk(a.P, kB) < kMaxNormBlocks ? nblk(a.P, kB) : kMaxNormBlocks;
+  hipLaunchKernelGGL(k_norm_max, dim3(nbm, (unsigned)a.F), dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_norm_exp_scan, g, dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_norm_total, dim3((unsigned)a.F), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(k_cdf, g, dim3(kB), 0, s, a);
 }
 void launch_resample(const ResampleArgs& a, hipStream_t s) {
+  if (!a.identity && a.GB > 0)
+    hipLaunchKernelGGL(k_guide, dim3(nblk(a.GB + 3, kB), (unsigned)a.F), dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_resample, dim3(nblk(a.P, kB), (unsigned)a.F), dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_readout, dim3((unsigned)a.F), dim3(256), 0, s, a);
 }

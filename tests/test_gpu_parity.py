@@ -339,3 +339,35 @@ def test_tile_shapes_vs_oracle(shape, d, D, monkeypatch):
     assert np.array_equal(st["classes"], r.classes)
     assert nrel(st["states"], r.states) < 1e-6
     assert nrel(st["w"], r.w) < 1e-5
+
+
+@pytest.mark.parametrize("resample", ["multinomial", "systematic"])
+def test_guided_resample_large_filter(m1, fx_config1, resample):
+    """Filters of >= 262144 particles search the inverse CDF between two entries of a guide
+    table (pf_kernels.hip, k_guide).  P = 300001: multinomial indices for given uniforms
+    equal the oracle's (torch's algorithm) up to last-ulp CDF ties; systematic offspring
+    counts stay within floor/ceil(P w_i)."""
+    from oracle import gpmdm_oracle as O
+    from gpmdm_amd import GPMDM_PF
+    f = fx_config1
+    P = 300_001
+    T = np.asarray(f["T"])
+    pf = GPMDM_PF(m1, torch.tensor(T), P, rng="torch", resample=resample)
+    torch.manual_seed(3)
+    pf.update(f["z"][0])
+    rng = np.random.RandomState(8)
+    st = pf.export_state()
+    E = rng.exponential(size=(P, 2))
+    nrm = rng.randn(P, m1.d)
+    u = rng.rand(P if resample == "multinomial" else 1)
+    pf.update_with_draws(f["z"][1], E, nrm, u)
+    st2 = pf.export_state()
+    assert st2["resample_idx"].min() >= 0 and st2["resample_idx"].max() < P
+    if resample == "multinomial":
+        idx_ref = O.multinomial_resample_indices(st2["w"], u)
+        assert int(np.sum(idx_ref != st2["resample_idx"])) <= 2
+    else:
+        n = np.bincount(st2["resample_idx"], minlength=P)
+        Pw = P * st2["w"]
+        assert np.all(n >= np.floor(Pw - 1e-9)) and np.all(n <= np.ceil(Pw + 1e-9))
+    assert st["states"].shape == (P, m1.d)
