@@ -1,7 +1,7 @@
 #pragma once
 // Fused GP predictive tile for gfx950: kernel-row generation + FP64 MFMA contraction.
 //
-// Replaces, for a tile of 64 particles x 256 columns:
+// Replaces, for a tile of PT particles x NB columns (shapes in common.h: TileGeo):
 //   observation GP  (gpmdm.py:955-959)  Ky* = exp(-|x*-X|^2/l^2),
 //                   mean = Ky*^T beta, var-quadratic form = Ky*^T Ky^-1 Ky*
 //   dynamics GP     (gpmdm.py:1061-1065) Kx* = RBF + linear kernel over the class-c rows,
@@ -13,24 +13,28 @@
 // (the same code as the observation GP).
 // With K^-1 = R R^T (R = U^-1 from the reference's own Cholesky recipe, gpmdm.py:1286-1289)
 // the quadratic form is |R^T k|^2.  R is upper triangular, so column block J only needs
-// training rows [0, (J+1)*256), and each wave stops at its own 64 columns: about half the
-// dense FLOPs.  B = [R | M] carries the mean weights M (beta or alpha_c) as extra columns,
-// so one pass produces both.
+// training rows up to its last column, and each 16-column tile stops at its own diagonal:
+// about half the dense FLOPs.  B = [R | M] carries the mean weights M (beta or alpha_c) as
+// extra columns, so one pass produces both.
 //
-// Workgroup = 4 waves; wave w owns the four 16-column tiles at columns
-// 256J + 16(4t + w), t = 0..3 (interleaved, so all waves reach nearly the same K), for all
-// 64 particles (4 x 4 tiles of v_mfma_f64_16x16x4_f64, 128 accumulator VGPRs).  A tile of R
-// columns retires once K passes its diagonal: the K loop runs in phases with tiles
-// [T0, T1) active, so no MFMA multiplies the zero triangle and no wave idles while its
-// siblings (and the barrier) wait.  Per K-step of 16 training rows:
-//   * K* tile (64 x 16) generated once per workgroup: each thread makes 4 values
-//     (expansion-form distance as gpmdm.py:508-515, table-driven fp64 exp), stored to a
-//     double-buffered LDS image that all 4 waves read as A fragments;
-//   * B fragments stream from HBM/L2 straight into VGPRs (8 x 16 B per lane, one K-step
-//     ahead): B is stored in fragment order, so no LDS round trip and no re-layout;
-//   * one barrier per K-step.  Two workgroups per CU overlap each other's barriers.
+// Workgroup = NW waves; wave w owns MT x NTW tiles of 16 x 16 (v_mfma_f64_16x16x4_f64,
+// 128 accumulator VGPRs at MT x NTW = 16), its column tiles interleaved with the other
+// waves' at columns NB J + 16 (NW t + w) so that all waves reach nearly the same K.  A tile
+// of R columns retires once K passes its diagonal: the K loop runs in phases with tiles
+// [T0, T1) active, so no MFMA multiplies the zero triangle.  Per K-step of 16 training rows:
+//   * the K* tile (PT x 16) is generated once per workgroup (expansion-form distance as
+//     gpmdm.py:508-515, table-driven fp64 exp), two K-steps ahead, into an LDS ring that
+//     all waves read as A fragments; training rows are staged through a second LDS ring;
+//   * B fragments stream from L2 straight into VGPRs by buffer loads (SGPR resource and
+//     K-step offset, constant lane offset: no VALU address arithmetic), one K-step ahead;
+//     B is stored in fragment order, so no LDS round trip and no re-layout;
+//   * one barrier per two K-steps.  Two workgroups per CU overlap each other's barriers.
+// Every VALU instruction costs MFMA issue time on gfx950 (tools/microbench/mix_probe), so
+// the loop is written to minimise them (padded rows instead of masks, buffer addressing).
 // Workgroups are ordered heavy-first (column block J descending), which both balances the
 // triangular work and makes concurrent workgroups share a B panel in each XCD's L2.
+// In the filter the observation GP's mean blocks reduce the likelihood partial sums
+// (TileParams::spart) instead of storing the P x D mean.
 #include <type_traits>
 
 #include "common.h"
@@ -391,11 +395,10 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   auto gen_one = [&](int ks, int s) -> double {
     const int rb = ks & (RXS - 1);
     const int r = g + NG * s;
-    const int i = ks * kBK + r;                            // training row
     const double* row = &RX[rb][r * RW];
     double x;
     if constexpr (VAR & 4) {
-      x = -(asq + 0.5 * i);
+      x = -(asq + 0.5 * (ks * kBK + r));
 #pragma unroll
       for (int j = 0; j < DI; ++j) x = fma(a2[j], 0.25 * j, x);
     } else {
@@ -408,7 +411,6 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     else if constexpr (E256) val = exp2_256(x, tab);
     else if constexpr ((VAR & 512) != 0) val = exp2_64m(x, tab);
     else val = exp2_64(x, tab);
-    (void)i;
     return val;                                            // padding rows: exactly 0
   };
   auto gen = [&](int ks, double (&v)[GV]) {

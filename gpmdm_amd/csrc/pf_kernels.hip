@@ -322,7 +322,6 @@ __global__ __launch_bounds__(kB) void k_dyn_finish(DynFinishArgs a) {
 __global__ __launch_bounds__(kB) void k_obs_finish(ObsFinishArgs a) {
   const int lane = threadIdx.x & 63;
   const long long o = (long long)blockIdx.x * (kB / 64) + (threadIdx.x >> 6);
-  __shared__ double smax[kB / 64];
   double llv = -INFINITY;
   if (o < a.n_out) {
     double q = 0.0;
@@ -348,7 +347,6 @@ __global__ __launch_bounds__(kB) void k_obs_finish(ObsFinishArgs a) {
       if (lane == 0) a.ll[a.ll_offset + o] = llv;
     }
   }
-  (void)smax;
 }
 
 // Fused form of k_obs_finish for the filter (one thread per particle): the tile kernel
