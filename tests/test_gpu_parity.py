@@ -371,3 +371,44 @@ def test_guided_resample_large_filter(m1, fx_config1, resample):
         Pw = P * st2["w"]
         assert np.all(n >= np.floor(Pw - 1e-9)) and np.all(n <= np.ceil(Pw + 1e-9))
     assert st["states"].shape == (P, m1.d)
+
+
+@pytest.mark.parametrize("P", [1, 3, 33])
+def test_tiny_model_and_particle_counts(P):
+    """Edge sizes: a model smaller than one K-step per class (N = 24 latents, 10 dynamics
+    rows per class, D = 5, d = 2) and particle counts of 1 (the reference's squeeze()
+    case, gpmdm_pf.py:150), 3 and 33 (not multiples of any tile).  Predictive maps and
+    three resynced filter steps against the oracle."""
+    from gpmdm_amd import GPMDM, GPMDM_PF, synthetic
+    from oracle import gpmdm_oracle as O
+    C, S, L, D, d = 2, 2, 6, 5, 2
+    data = synthetic.make_sequences(C=C, S=S, L=L, D=D, d=d, seed=31)
+    rng = np.random.RandomState(32)
+    N = C * S * L
+    X = rng.randn(N, d)
+    lp = dict(y_log_lengthscales=np.log([1.2, 0.9]), y_log_lambdas=np.log(rng.uniform(0.5, 2, D)),
+              y_log_sigma_n=np.log(0.2), x_log_lengthscales=np.log([1.1, 1.4]),
+              x_log_lambdas=np.log([1.3, 0.8]), x_log_sigma_n=np.log(0.2),
+              x_log_lin_coeff=np.log([0.5, 0.6, 0.4]))
+    m = GPMDM.from_arrays(X, data.sequences, **lp)
+    om = O.OracleModel(X=X, Y=np.concatenate([y for c in data.sequences for y in c]).astype(np.float64),
+                       seq_lengths=[[L] * S] * C, **lp).precompute()
+    xs = X[:1] + 0.05
+    mu, var = m.map_x_to_y(torch.tensor(xs))
+    omu, ovar = om.map_x_to_y(xs)
+    assert nrel(mu.numpy(), omu) < 1e-9 and nrel(var.numpy(), ovar) < 1e-8
+    T = synthetic.markov_matrix(C)
+    pf = GPMDM_PF(m, torch.tensor(T), P, rng="torch")
+    for k in range(3):
+        st0 = pf.export_state()
+        E = rng.exponential(size=(P, C))
+        nrm = rng.randn(P, d)
+        u = rng.rand(P)
+        z = data.sequences[k % C][0][k].astype(np.float64)
+        pf.update_with_draws(z, E, nrm, u)
+        r = O.step(om, T, st0["states"], st0["classes"], z, E, nrm, u)
+        st = pf.export_state()
+        assert np.array_equal(st["classes"], r.classes), k
+        assert nrel(st["states"], r.states) < 1e-6, k
+        assert np.max(np.abs(pf.class_probabilities().numpy() - r.posterior)) < 1e-6, k
+        assert nrel(pf.current_state_mean().numpy(), r.mean) < 1e-6, k
