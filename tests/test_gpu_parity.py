@@ -412,3 +412,85 @@ def test_tiny_model_and_particle_counts(P):
         assert nrel(st["states"], r.states) < 1e-6, k
         assert np.max(np.abs(pf.class_probabilities().numpy() - r.posterior)) < 1e-6, k
         assert nrel(pf.current_state_mean().numpy(), r.mean) < 1e-6, k
+
+
+@pytest.mark.parametrize("world,rng_mode", [(4, "philox"), (8, "philox"), (3, "torch")])
+def test_logical_shards_match_one_rank(m2, world, rng_mode):
+    """results at R ranks equal the single-rank filter, with R logical shards
+    on one GPU and the all-gather done in-process.  Philox draws at 4 and 8 ranks; the
+    replay stream (torch generator) at 3 ranks, every rank drawing the same full streams
+    in the reference's order (gpmdm_amd.replay).  P = 10007 (uneven shards)."""
+    from gpmdm_amd import GPMDM_PF, _lib, replay
+    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
+    P = 10_007
+    Y = m2.get_Y()
+    torch.manual_seed(4)
+    ref = GPMDM_PF(m2, T, P, rng=rng_mode, seed=91)
+    ranks = []
+    for r in range(world):
+        torch.manual_seed(4)
+        ranks.append(GPMDM_PF(m2, T, P, rng=rng_mode, seed=91, shard=(world, r)))
+    lib = _lib.load()
+    for k in range(3):
+        z = np.ascontiguousarray(np.asarray(Y[60 + 3 * k], dtype=np.float64))
+        if rng_mode == "torch":
+            state = torch.get_rng_state()
+            ref.update(z)
+            after = torch.get_rng_state()
+            draws_u = []
+            for pf in ranks:                                  # switch + propagate + pack
+                torch.set_rng_state(state)
+                h, s = pf._h, pf._stream()
+                E = np.ascontiguousarray(replay.switch_draws(P, 2))
+                counts = np.zeros(2, dtype=np.int64)
+                _lib.check(lib.gpmdm_pf_switch(h, _lib.dptr(E), _lib.i64ptr(counts), s), "switch")
+                nrm = np.ascontiguousarray(replay.dynamics_draws(counts, m2.d))
+                _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), _lib.dptr(nrm), s), "propagate")
+                _lib.check(lib.gpmdm_pf_pack(h, pf._send.data_ptr(), s), "pack")
+                draws_u.append(np.ascontiguousarray(replay.resample_draws(P)))
+            assert torch.equal(torch.get_rng_state(), after)
+            full = torch.cat([pf._send for pf in ranks], 0)
+            for pf, U in zip(ranks, draws_u):                 # unpack + resample
+                pf._recv.copy_(full)
+                h, s = pf._h, pf._stream()
+                _lib.check(lib.gpmdm_pf_unpack(h, pf._recv.data_ptr(), s), "unpack")
+                _lib.check(lib.gpmdm_pf_resample(h, _lib.dptr(U), s), "resample")
+                pf._readout = None
+        else:
+            ref.update(z)
+            full = torch.cat([pf._stage_propagate(z) for pf in ranks], 0)
+            for pf in ranks:
+                pf._recv.copy_(full)
+                pf._stage_resample()
+        a = ref.export_state()
+        for pf in ranks:
+            b = pf.export_state()
+            for key in ("states", "classes", "ll", "resample_idx"):
+                assert np.array_equal(a[key], b[key]), (k, key)
+            assert np.array_equal(ref.class_probabilities().numpy(), pf.class_probabilities().numpy())
+            assert np.array_equal(ref.current_state_mean().numpy(), pf.current_state_mean().numpy())
+
+
+def test_empty_class_segments(m2, fx_config2):
+    """A class no particle switches into (its column of T is zero): its dynamics segment is
+    empty every frame.  Three resynced steps against the oracle."""
+    from gpmdm_amd import GPMDM_PF
+    from oracle import gpmdm_oracle as O
+    T = np.array([[1.0, 0.0], [1.0, 0.0]])
+    P = 777
+    pf = GPMDM_PF(m2, torch.tensor(T), P, rng="torch")
+    om = oracle_model(fx_config2)
+    rng = np.random.RandomState(12)
+    Y = m2.get_Y()
+    for k in range(3):
+        st0 = pf.export_state()
+        E = rng.exponential(size=(P, 2))
+        nrm = rng.randn(P, m2.d)
+        u = rng.rand(P)
+        pf.update_with_draws(Y[100 + k], E, nrm, u)
+        r = O.step(om, T, st0["states"], st0["classes"], Y[100 + k], E, nrm, u)
+        st = pf.export_state()
+        assert np.all(st["classes"] == 0) and np.array_equal(st["classes"], r.classes)
+        assert nrel(st["states"], r.states) < 1e-6
+        post = pf.class_probabilities().numpy()
+        assert post[1] == 0.0 and abs(post[0] - 1.0) < 1e-15
