@@ -39,9 +39,12 @@ def _flags():
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
+    newest_hdr = max(h.stat().st_mtime for h in HEADERS)
+    newest_src = max((CSRC / src).stat().st_mtime for src in SOURCES)
+    if not force and LIB.exists() and LIB.stat().st_mtime >= max(newest_hdr, newest_src):
+        return LIB                      # current (objects need not be present, e.g. on a GPU box)
     OBJ.mkdir(exist_ok=True)
     cc = hipcc()
-    newest_hdr = max(h.stat().st_mtime for h in HEADERS)
     jobs = []
     for src in SOURCES:
         s = CSRC / src
