@@ -125,11 +125,59 @@ class GPMDM:
         # GP-tile workgroup shape (include/gpmdm_hip.h GPMDM_TILE_*: 0 default, 1 64x256,
         # 2 64x512, 3 32x512); env override for A/B runs
         self.tile_shape = int(os.environ.get("GPMDM_TILE_SHAPE", "0"))
+        self._trainable = {}        # set_training_mode (gpmdm.py:247-279); empty = all
 
     # ---- reference API: data registry (gpmdm.py:239-309) -------------------------
     def set_evaluation_mode(self):
         """gpmdm.py:239-245 (no autograd state is kept here)."""
         self.flg_trainable_list = []
+
+    # ---- reference API: training (gpmdm.py:247-279, 550-628, 721-885) ---------------
+    _Y_PARAMS = ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n")
+    _X_PARAMS = ("x_log_lengthscales", "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff")
+
+    def set_training_mode(self, model='all'):
+        """gpmdm.py:247-279: which parameters ``train_adam``'s optimiser updates."""
+        if model == 'all':
+            self._trainable = {n: True for n in self._Y_PARAMS + self._X_PARAMS + ("X",)}
+        elif model == 'latent':
+            self._trainable = {**{n: True for n in self._Y_PARAMS}, **{n: False for n in self._X_PARAMS}, "X": True}
+        elif model == 'dynamics':
+            self._trainable = {**{n: False for n in self._Y_PARAMS}, **{n: True for n in self._X_PARAMS}, "X": True}
+        else:
+            raise ValueError('model must be \'all\', \'latent\' or \'dynamics\'')
+
+    def get_y_neg_log_likelihood(self, Y, X, N):
+        """gpmdm.py:550-590 on the model's device (fp64 Cholesky + triangular solve); returns
+        a device scalar.  ``Y``/``X`` may be host or device arrays."""
+        from . import training
+        f64 = dict(dtype=torch.float64, device=self.device)
+        p = {n: getattr(self, n).to(**f64) for n in self._Y_PARAMS}
+        p["X"] = torch.as_tensor(_to_np(X) if not isinstance(X, torch.Tensor) else X).to(**f64)
+        Y = torch.as_tensor(_to_np(Y) if not isinstance(Y, torch.Tensor) else Y).to(**f64)
+        return training.y_neg_log_likelihood(p, Y, self.sigma_n_num_Y)
+
+    def get_x_neg_log_likelihood(self, Xout, Xin):
+        """gpmdm.py:592-628 (class-masked K_x, evaluated block by block) on the device."""
+        from . import training
+        f64 = dict(dtype=torch.float64, device=self.device)
+        p = {n: getattr(self, n).to(**f64) for n in self._X_PARAMS}
+        Xin = torch.as_tensor(Xin).to(**f64)
+        Xout = torch.as_tensor(Xout).to(**f64)
+        return training.x_neg_log_likelihood(p, Xin, Xout, self._class_dynamics_rows(), self.sigma_n_num_X)
+
+    def gpdm_loss(self, Y, N, M=None, balance=1):
+        """gpmdm.py:721-760: L_y + balance * L_x (``M`` is unused, as in the reference, which
+        reads its own mask)."""
+        Xin, Xout, _ = self.get_Xin_Xout_matrices()
+        return self.get_y_neg_log_likelihood(Y, self.X, N) + balance * self.get_x_neg_log_likelihood(Xout, Xin)
+
+    def train_adam(self, num_opt_steps: int, num_print_steps: int = 0, lr: float = 0.01, balance: float = 1):
+        """gpmdm.py:817-885 on the GPU (gpmdm_amd/training.py): Adam over every parameter,
+        then the kernel-inverse precompute and device upload.  Returns the losses."""
+        from . import training
+        self.set_training_mode('all')
+        return training.train_adam(self, num_opt_steps, num_print_steps, lr, balance)
 
     def add_data(self, Y, class_index: int):
         """gpmdm.py:281-298."""

@@ -183,6 +183,46 @@ class OracleModel:
 
 
 # ----------------------------------------------------------------------------
+# training loss (gpmdm.py:550-628, 721-760): next-row oracle for GPMDM.gpdm_loss
+# ----------------------------------------------------------------------------
+
+def y_neg_log_likelihood(model: OracleModel):
+    """gpmdm.py:550-590: D/2 log|K_y| + 1/2 tr(K_y^-1 Y W^2 Y^T) - N * 2 sum(y_log_lambdas)
+    (the reference's ``log_det_W`` is 2 sum(log lambda), i.e. log|W^2|)."""
+    N, D = model.Y.shape
+    Ky = rbf_kernel(model.X, model.X, model.y_log_lengthscales, model.y_log_sigma_n,
+                    model.sigma_n_num_Y, noise=True)
+    L = np.linalg.cholesky(Ky)
+    logdet = 2.0 * np.sum(np.log(np.diag(L)))
+    W2 = np.exp(model.y_log_lambdas) ** 2
+    tr = np.trace(chol_inverse(Ky) @ ((model.Y * W2) @ model.Y.T))
+    return D / 2 * logdet + 0.5 * tr - N * 2.0 * np.sum(model.y_log_lambdas)
+
+
+def x_neg_log_likelihood(model: OracleModel):
+    """gpmdm.py:592-628 with the class mask (gpmdm.py:311-341): K_x = (RBF + noise + lin)
+    (Xin, Xin) * M is block diagonal, so log|K_x| and the trace split over class blocks."""
+    Xin, Xout, cls = model.xin_xout()
+    d = Xout.shape[1]
+    W2 = np.exp(model.x_log_lambdas) ** 2
+    logdet, tr = 0.0, 0.0
+    for c in range(model.n_classes):
+        m = cls == c
+        xi, xo = Xin[m], Xout[m]
+        K = rbf_kernel(xi, xi, model.x_log_lengthscales, model.x_log_sigma_n,
+                       model.sigma_n_num_X, noise=True) + lin_kernel(xi, xi, model.x_log_lin_coeff)
+        L = np.linalg.cholesky(K)
+        logdet += 2.0 * np.sum(np.log(np.diag(L)))
+        tr += np.trace(chol_inverse(K) @ ((xo * W2) @ xo.T))
+    return d / 2 * logdet + 0.5 * tr - Xin.shape[0] * 2.0 * np.sum(model.x_log_lambdas)
+
+
+def gpdm_loss(model: OracleModel, balance: float = 1.0):
+    """gpmdm.py:721-760: L_y + balance * L_x."""
+    return y_neg_log_likelihood(model) + balance * x_neg_log_likelihood(model)
+
+
+# ----------------------------------------------------------------------------
 # particle filter (gpmdm_pf.py)
 # ----------------------------------------------------------------------------
 

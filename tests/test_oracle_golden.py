@@ -10,7 +10,7 @@ BASELINE tolerance.
 import numpy as np
 import pytest
 
-from conftest import nrel, oracle_model
+from conftest import load_fixture, nrel, oracle_model
 from oracle import gpmdm_oracle as O
 
 
@@ -106,3 +106,15 @@ def test_switch_first_max_tie():
     T = np.array([[0.5, 0.5], [0.0, 1.0]])
     E = np.array([[1.0, 1.0], [1.0, 1.0]])
     assert list(O.switch_classes(np.array([0, 1]), T, E)) == [0, 1]
+
+
+def test_oracle_training_loss_matches_reference():
+    """The oracle's GPDM loss terms (gpmdm.py:550-628, 721-760) against the reference's
+    values at the PCA initialisation of the config-1 model (tests/golden/training_n500.npz)."""
+    from oracle import gpmdm_oracle as O
+    f = load_fixture("training_n500")
+    om = oracle_model(f)
+    ly, lx = O.y_neg_log_likelihood(om), O.x_neg_log_likelihood(om)
+    assert abs(ly - f["loss_y0"]) <= 1e-9 * abs(f["loss_y0"])
+    assert abs(lx - f["loss_x0"]) <= 1e-9 * abs(f["loss_x0"])
+    assert abs(O.gpdm_loss(om) - f["loss0"]) <= 1e-9 * abs(f["loss0"])
