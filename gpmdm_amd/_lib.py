@@ -59,6 +59,7 @@ _SIGS = {
     "gpmdm_pf_dyn_rows": (c_int, [c_void_p, _i64p, c_void_p]),
     "gpmdm_gp_factor": (c_int, [c_int, _dp, c_int64, c_int32, _dp, _dp, c_double, c_double, c_double,
                                 _dp, c_int64, _dp, _dp]),
+    "gpmdm_spd_inverse": (c_int, [c_int, c_void_p, c_int64, _dp, c_void_p]),
     "gpmdm_last_error": (c_char_p, []),
     "gpmdm_version": (c_char_p, []),
 }

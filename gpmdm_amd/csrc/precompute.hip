@@ -18,6 +18,8 @@
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
 
+#include <cmath>
+#include <mutex>
 #include <vector>
 
 #include "common.h"
@@ -55,6 +57,28 @@ __global__ __launch_bounds__(256) void k_zero_lower(double* R, int n) {
   const int j = blockIdx.x * 16 + (threadIdx.x & 15);
   const int i = blockIdx.y * 16 + (threadIdx.x >> 4);
   if (i < n && j < i) R[(long long)i * n + j] = 0.0;
+}
+
+// Mirror the stored (column-major lower = row-major upper) triangle into the other one.
+__global__ __launch_bounds__(256) void k_symmetrize_from_upper(double* A, int n) {
+  const int j = blockIdx.x * 16 + (threadIdx.x & 15);
+  const int i = blockIdx.y * 16 + (threadIdx.x >> 4);
+  if (i < n && j < i) A[(long long)i * n + j] = A[(long long)j * n + i];
+}
+
+// 2 sum_i log L_ii into *out (one block; the diagonal of a Cholesky factor).
+__global__ __launch_bounds__(1024) void k_logdet_diag(const double* A, int n, double* out) {
+  __shared__ double red[1024 / 64];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) s += log(A[(long long)i * n + i]);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < 1024 / 64; ++w) t += red[w];
+    *out = 2.0 * t;
+  }
 }
 
 struct Handle {
@@ -145,5 +169,50 @@ extern "C" int gpmdm_gp_factor(int device, const double* X, int64_t n, int32_t d
     HIPCHK(hipMemcpy(M, b.B0, (size_t)N * K * sizeof(double), hipMemcpyDeviceToHost));
   }
   HIPCHK(hipMemcpy(R, b.K, (size_t)N * N * sizeof(double), hipMemcpyDeviceToHost));
+  return GPMDM_OK;
+}
+
+// One rocBLAS handle per device, created on first use (handle creation costs milliseconds;
+// a training step at small N costs a few).  rocBLAS manages its own workspace on it.
+static rocblas_handle cached_handle(int device) {
+  static std::mutex mu;
+  static std::vector<rocblas_handle> handles;
+  std::lock_guard<std::mutex> lock(mu);
+  if ((int)handles.size() <= device) handles.resize(device + 1, nullptr);
+  if (!handles[device] && rocblas_create_handle(&handles[device]) != rocblas_status_success) handles[device] = nullptr;
+  return handles[device];
+}
+
+extern "C" int gpmdm_spd_inverse(int device, double* A, int64_t n, double* logdet, void* stream) {
+  CHECK(A && logdet, "null argument");
+  CHECK(n >= 1 && n <= 46340, "n out of range (1..46340: n*n must fit rocBLAS' int32 indexing)");
+  *logdet = NAN;
+  HIPCHK(hipSetDevice(device));
+  rocblas_handle h = cached_handle(device);
+  if (!h) return fail(GPMDM_E_HIP, "rocblas_create_handle failed");
+  hipStream_t s = (hipStream_t)stream;
+  RBCHK(rocblas_set_stream(h, s));
+  const int N = (int)n;
+  DevBufs b;
+  TRY(dalloc(&b.info, 1));
+  TRY(dalloc(&b.sq, 1));                                    // logdet scratch
+  int info = 0;
+  RBCHK(rocsolver_dpotrf(h, rocblas_fill_lower, N, A, N, b.info));
+  HIPCHK(hipMemcpyAsync(&info, b.info, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (info != 0)
+    return fail(GPMDM_E_INVALID, "matrix is not positive definite (potrf info=" + std::to_string(info) + ")");
+  hipLaunchKernelGGL(k_logdet_diag, dim3(1), dim3(1024), 0, s, A, N, b.sq);
+  HIPCHK(hipGetLastError());
+  RBCHK(rocsolver_dpotri(h, rocblas_fill_lower, N, A, N, b.info));
+  const dim3 g2((unsigned)cdiv(N, 16), (unsigned)cdiv(N, 16));
+  hipLaunchKernelGGL(k_symmetrize_from_upper, g2, dim3(256), 0, s, A, N);
+  HIPCHK(hipGetLastError());
+  double ld = NAN;
+  HIPCHK(hipMemcpyAsync(&ld, b.sq, sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(&info, b.info, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (info != 0) return fail(GPMDM_E_INVALID, "Cholesky factor is singular (potri info=" + std::to_string(info) + ")");
+  *logdet = ld;
   return GPMDM_OK;
 }

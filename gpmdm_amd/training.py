@@ -11,11 +11,11 @@ Mirrors ``/root/reference/gpmdm/gpmdm.py``:
 * ``train_adam`` (gpmdm.py:817-885): Adam over every parameter (``set_training_mode('all')``).
 
 Design (MI355X): everything runs in fp64 on the model's device through torch (rocSOLVER
-Cholesky, rocBLAS triangular solves, autograd).  Where the reference forms explicit
-inverses (``U^-1 U^-T``) and a dense Nx x Nx mask, this computes each log-determinant from
-the Cholesky diagonal and each trace term as ||L^-1 (Y W)||_F^2 by a triangular solve, and
-the dynamics term block by block (the masked matrix is block diagonal, so the blocks are
-the whole of it): O(sum N_c^2) memory instead of the mask's O(Nx^2), and no inverse.
+Cholesky and inverse, rocBLAS GEMMs, autograd).  Each log-determinant comes from the
+Cholesky diagonal and each (log|K|, trace) pair has a closed-form backward
+(``_LogdetTrace``); the dynamics term is evaluated block by block (the masked matrix is
+block diagonal, so the blocks are the whole of it): O(sum N_c^2) memory instead of the
+dense mask's O(Nx^2).
 
 Reference behaviour kept: ``cholesky_ex`` info is not checked (a non-positive-definite
 kernel gives NaN, and ``train_adam`` stops with a message as the reference does); the
@@ -48,12 +48,61 @@ def lin_kernel(X1, X2, log_c):
     return (torch.cat([X1, o1], 1) * c2) @ torch.cat([X2, o2], 1).T
 
 
+# Above this size K^-1 and log|K| come from the library (gpmdm_spd_inverse: rocSOLVER potrf +
+# potri on the tensor's own buffer, with a library-owned rocBLAS handle): this ROCm build's
+# torch hipSOLVER / hipBLAS paths fail to allocate workspace for N x N right-hand sides at
+# N >= 10^4 (tools/inv_probe.sh).  Below it, torch's cholesky_ex + cholesky_inverse.
+_LIB_MIN_N = 8193
+
+
+def _inverse_and_logdet(K):
+    """(K^-1, log|K|) of a symmetric positive-definite device matrix.  A matrix that is not
+    positive definite gives NaN (the reference ignores cholesky_ex's info)."""
+    n = K.shape[0]
+    if n < _LIB_MIN_N:
+        L, _ = torch.linalg.cholesky_ex(K)
+        return torch.cholesky_inverse(L), 2.0 * torch.sum(torch.log(torch.diagonal(L)))
+    import ctypes
+    from . import _lib
+    A = K.detach().contiguous().clone()
+    ld = ctypes.c_double()
+    rc = _lib.load().gpmdm_spd_inverse(A.device.index or 0, ctypes.c_void_p(A.data_ptr()), n, ctypes.byref(ld),
+                                       ctypes.c_void_p(torch.cuda.current_stream(A.device).cuda_stream))
+    if rc != 0:
+        A.fill_(float("nan"))
+    return A, torch.tensor(ld.value, dtype=K.dtype, device=K.device)
+
+
+class _LogdetTrace(torch.autograd.Function):
+    """(log|K|, tr(K^-1 B B^T)) with a closed-form backward.
+
+    forward:  K^-1 and log|K| from the Cholesky factor (potrf + potri; info unchecked, as
+              the reference: NaN), A = K^-1 B, tr = sum(A * B)
+    backward: d log|K| / dK = K^-1,  d tr / dK = -A A^T,  d tr / dB = 2 A
+    Autograd through the Cholesky factor would run a trsm with an N x N right-hand side,
+    which this ROCm build's hipBLAS fails to allocate for at N = 10^4; the closed form needs
+    only GEMMs and the inverse the forward already has (the reference's own explicit
+    inverse, gpmdm.py:582-584).
+    """
+
+    @staticmethod
+    def forward(ctx, K, B):
+        Kinv, logdet = _inverse_and_logdet(K)
+        A = Kinv @ B
+        ctx.save_for_backward(Kinv, A)
+        return logdet, torch.sum(A * B)
+
+    @staticmethod
+    def backward(ctx, g_logdet, g_tr):
+        Kinv, A = ctx.saved_tensors
+        gK = g_logdet * Kinv - g_tr * (A @ A.T)
+        gB = (2.0 * g_tr) * A
+        return gK, gB
+
+
 def _logdet_and_trace(K, B):
-    """(log|K|, tr(K^-1 B B^T)) from one Cholesky factor (info unchecked, as the reference)."""
-    L, _ = torch.linalg.cholesky_ex(K)
-    logdet = 2.0 * torch.sum(torch.log(torch.diagonal(L)))
-    Z = torch.linalg.solve_triangular(L, B, upper=False)
-    return logdet, torch.sum(Z * Z)
+    """(log|K|, tr(K^-1 B B^T))."""
+    return _LogdetTrace.apply(K, B)
 
 
 def y_neg_log_likelihood(p, Y, sigma_n_num_Y):

@@ -200,6 +200,14 @@ int gpmdm_gp_factor(int device, const double* X, int64_t n, int32_t d, const dou
                     const double* lin_c2, double diag_a, double diag_b, double diag_c,
                     const double* B, int64_t k, double* R, double* M);
 
+/* In-place inverse of a symmetric positive-definite n x n matrix on the device (the
+ * training loss's K^-1 and log|K|, gpmdm.py:576-584 / 612-619; gpmdm_amd/training.py):
+ * rocSOLVER potrf + potri on the caller's buffer A (device, row-major = column-major for a
+ * symmetric matrix, leading dimension n), symmetrised; *logdet (host) = 2 sum log diag of
+ * the Cholesky factor.  Runs on `stream` (NULL: default) and returns after it completes.
+ * A matrix that is not positive definite is GPMDM_E_INVALID and *logdet is NaN. */
+int gpmdm_spd_inverse(int device, double* A_dev, int64_t n, double* logdet, void* stream);
+
 /* Message of the last failed call on this thread ("" if none). */
 const char* gpmdm_last_error(void);
 

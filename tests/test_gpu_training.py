@@ -71,3 +71,28 @@ def test_train_adam_balance_is_ignored_like_the_reference(ft):
     m = product_model(ft)
     losses = m.train_adam(1, lr=0.01, balance=0.25)
     assert abs(losses[0] - ft["adam_losses"][0]) <= 1e-9 * abs(ft["adam_losses"][0])
+
+
+def test_library_inverse_path_matches_reference(ft, monkeypatch):
+    """The large-N path (K^-1 and log|K| from gpmdm_spd_inverse: rocSOLVER potrf + potri in
+    the HIP library), forced at N = 500: loss terms and gradients against the reference."""
+    from gpmdm_amd import training
+    monkeypatch.setattr(training, "_LIB_MIN_N", 1)
+    m = product_model(ft)
+    tr = training.Trainer(m)
+    ly, lx = tr.terms()
+    assert abs(float(ly) - ft["loss_y0"]) <= 1e-9 * abs(ft["loss_y0"])
+    assert abs(float(lx) - ft["loss_x0"]) <= 1e-9 * abs(ft["loss_x0"])
+    (ly + lx).backward()
+    for p in PARAMS:
+        assert nrel(tr.p[p].grad.detach().cpu().numpy().reshape(-1), ft[f"grad0_{p}"]) < 1e-7, p
+
+
+def test_spd_inverse_rejects_indefinite():
+    import ctypes
+    from gpmdm_amd import _lib
+    A = torch.tensor([[1.0, 2.0], [2.0, 1.0]], dtype=torch.float64, device="cuda")
+    ld = ctypes.c_double()
+    rc = _lib.load().gpmdm_spd_inverse(0, ctypes.c_void_p(A.data_ptr()), 2, ctypes.byref(ld), None)
+    assert rc == -1 and np.isnan(ld.value)
+    assert b"positive definite" in _lib.load().gpmdm_last_error()
