@@ -211,6 +211,18 @@ struct gpmdm_pf {
   // ancestor de-duplication: owner/slot are C x P keyed by (class, ancestor)
   unsigned* owner = nullptr;
   int *slot = nullptr, *lflag = nullptr, *lblock = nullptr, *ltab = nullptr, *lperm = nullptr;
+  // ancestor-ordered shards (multi-rank philox filters, shard_order.hip): own = particles
+  // in order of their resampling ancestor's bucket; this rank evaluates positions [lo, hi)
+  int* own = nullptr;
+  unsigned char* own_tmp = nullptr;
+  size_t own_tmp_bytes = 0;
+  bool own_valid = false;
+  bool shard_order = true;            // gpmdm_pf_set_shard_order
+  // observation upload through two pinned slots (a pageable hipMemcpyAsync is staged by the
+  // runtime and stalls the launching thread); each slot's event guards its reuse
+  double* zpin[2] = {nullptr, nullptr};
+  hipEvent_t zev[2] = {nullptr, nullptr};
+  int zslot = 0;
   double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *sobs = nullptr;
   int nparts_dyn_max = 0;
   double *z = nullptr, *E = nullptr, *normals = nullptr, *U = nullptr;
@@ -234,24 +246,32 @@ struct gpmdm_pf {
   int* lseg_end() const { return ltab + 40; }
   int* lseg_out() const { return ltab + 80; }
   int* lseg_tiles() const { return ltab + 120; }
+  const int* own_order() const { return own_valid ? own : nullptr; }
 
   ~gpmdm_pf() {
     double* ds[] = {T, X, X_prop, ll, qdyn, mudyn, qobs, sobs, z, E, normals, U,
                     e, local, blocksum, blockoffw, total, cum, partials, readout};
     for (double* p : ds) dfree(p);
     int* is[] = {cls, cls_new, perm, ridx, blockcounts, blockoff, small, obs_tab,
-                 slot, lflag, lblock, ltab, lperm, guide};
+                 slot, lflag, lblock, ltab, lperm, guide, own};
     for (int* p : is) dfree(p);
+    dfree(own_tmp);
     dfree(gmax);
     dfree(owner);
     for (auto& r : recs) { pool.push_back(r.a); pool.push_back(r.b); }
     for (auto ev : pool) (void)hipEventDestroy(ev);
+    for (int k = 0; k < 2; ++k) {
+      if (zpin[k]) (void)hipHostFree(zpin[k]);
+      if (zev[k]) (void)hipEventDestroy(zev[k]);
+    }
   }
 
   hipEvent_t ev() {
     if (!pool.empty()) { hipEvent_t x = pool.back(); pool.pop_back(); return x; }
     hipEvent_t x = nullptr;
-    (void)hipEventCreate(&x);
+    // timing-only events: no system-scope fence at record time (a fenced record left a
+    // ~10 us bubble between the stages it separates)
+    (void)hipEventCreateWithFlags(&x, hipEventDisableSystemFence);
     return x;
   }
   void mark_begin(hipStream_t s, hipEvent_t& a) {
@@ -530,7 +550,19 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   ALLOC(guide, guide_buckets_used(Pf) > 0 ? F * (guide_buckets(Pf) + 3) : 1);
   ALLOC(partials, F * pf->nbf * (C + 1 + d));
   ALLOC(readout, F * (C + d + 1));
+  if (n_ranks > 1 && rng_mode == GPMDM_RNG_PHILOX) {
+    pf->own_tmp_bytes = std::max<size_t>(ancestor_order_temp_bytes(P), 1);
+    ALLOC(own, P);
+    ALLOC(own_tmp, pf->own_tmp_bytes);
+  }
 #undef ALLOC
+  for (int k = 0; k < 2; ++k) {
+    if (hipHostMalloc((void**)&pf->zpin[k], sizeof(double) * F * D) != hipSuccess ||
+        hipEventCreateWithFlags(&pf->zev[k], hipEventDisableTiming) != hipSuccess) {
+      delete pf;
+      return fail(GPMDM_E_NOMEM, "pinned observation buffer");
+    }
+  }
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, m->obs.tiles(pf->nloc)};
   if (hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(pf->T, T, sizeof(double) * C * C, hipMemcpyHostToDevice) != hipSuccess) {
@@ -635,6 +667,7 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   pf->initialised = true;
+  pf->own_valid = false;               // no ancestors yet: identity ownership
   pf->switched = pf->propagated = false;
   return GPMDM_OK;
 }
@@ -674,6 +707,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
     sa.lo = pf->lo;
     sa.hi = pf->hi;
   }
+  sa.own = pf->own_order();
   launch_switch(sa, s);
   ScanArgs sc{};
   sc.nb = pf->nb;
@@ -681,6 +715,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   sc.pt = m->dyn[0].geo.pt();
   sc.lo = pf->lo;
   sc.hi = pf->hi;
+  sc.own = pf->own_order();
   sc.blockcounts = pf->blockcounts;
   sc.cls_new = pf->cls_new;
   sc.blockoff = pf->blockoff;
@@ -697,6 +732,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   ga.cls_new = pf->cls_new;
   ga.class_start = pf->class_start();
   ga.blockoff = pf->blockoff;
+  ga.own = pf->own_order();
   ga.perm = pf->perm;
   launch_group(ga, s);
   if (pf->dedup && pf->nloc > 0) {
@@ -743,7 +779,14 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipSetDevice(m->device));
   const int C = m->C, d = m->d, D = m->D;
-  HIPCHK(hipMemcpyAsync(pf->z, zh, sizeof(double) * D * pf->F, hipMemcpyHostToDevice, s));
+  {
+    const int k = pf->zslot;
+    HIPCHK(hipEventSynchronize(pf->zev[k]));      // the slot's previous upload has run
+    std::memcpy(pf->zpin[k], zh, sizeof(double) * D * pf->F);
+    HIPCHK(hipMemcpyAsync(pf->z, pf->zpin[k], sizeof(double) * D * pf->F, hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(pf->zev[k], s));
+    pf->zslot ^= 1;
+  }
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
     CHECK(normals, "replay mode needs the dynamics normals");
     HIPCHK(hipMemcpyAsync(pf->normals, normals, sizeof(double) * pf->P * d, hipMemcpyHostToDevice, s));
@@ -829,7 +872,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     tp.seg_pos_end = pf->obs_tab + 1;
     tp.seg_out_base = pf->obs_tab + 2;
     tp.seg_tile_start = pf->obs_tab + 3;
-    tp.perm = nullptr;
+    tp.perm = pf->own_order();           // positions [lo, hi) of the ownership order
     tp.X = pf->X_prop;
     fill_tile_common(tp, m, false);
     tp.qpart = pf->qobs;
@@ -857,6 +900,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     oa.ll_const = (double)((float)(0.5 * D) * (float)1.8378770351409912);
     oa.ll = pf->ll;
     oa.ll_offset = pf->lo;
+    oa.own = pf->own_order();
     launch_obs_finish(oa, s);
     pf->mark_end(s, GPMDM_STAGE_OBS_FINISH, t0);
   }
@@ -881,6 +925,7 @@ int gpmdm_pf_pack(gpmdm_pf_t pf, double* send, void* stream) {
   a.n = pf->nloc;
   a.lo = pf->lo;
   a.d = pf->m->d;
+  a.own = pf->own_order();
   a.buf = send;
   a.ll = pf->ll;
   a.cls = pf->cls_new;
@@ -897,6 +942,7 @@ int gpmdm_pf_unpack(gpmdm_pf_t pf, const double* recv, void* stream) {
   a.n = pf->P;
   a.lo = 0;
   a.d = pf->m->d;
+  a.own = pf->own_order();
   a.buf = const_cast<double*>(recv);
   a.ll = pf->ll;
   a.cls = pf->cls_new;
@@ -923,6 +969,13 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   ResampleArgs ra = resample_args(pf);
   ra.U = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->U : nullptr;
   launch_resample(ra, s);
+  // next frame's ownership order (identical on every rank: same replicated ancestors)
+  pf->own_valid = false;
+  if (pf->own && pf->dedup && pf->shard_order) {
+    if (launch_ancestor_order(pf->ridx, pf->own, pf->P, pf->own_tmp, pf->own_tmp_bytes, s) != 0)
+      return fail(GPMDM_E_HIP, "ancestor-order pass failed");
+    pf->own_valid = true;
+  }
   pf->mark_end(s, GPMDM_STAGE_RESAMPLE, t0);
   HIPCHK(hipGetLastError());
   pf->frame += 1;
@@ -1001,6 +1054,14 @@ int gpmdm_pf_set_dedup(gpmdm_pf_t pf, int enable) {
   CHECK(pf, "null handle");
   if (pf->switched) return fail(GPMDM_E_STATE, "set_dedup between switch and propagate");
   pf->dedup = enable != 0;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_set_shard_order(gpmdm_pf_t pf, int enable) {
+  CHECK(pf, "null handle");
+  if (pf->switched || pf->propagated) return fail(GPMDM_E_STATE, "set_shard_order inside a step");
+  pf->shard_order = enable != 0;
+  if (!pf->shard_order) pf->own_valid = false;
   return GPMDM_OK;
 }
 

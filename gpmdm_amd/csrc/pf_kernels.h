@@ -34,12 +34,16 @@ struct SwitchArgs {
   const int* anc;                 // P   in-filter ancestor index (resample source; identity after init)
   unsigned* owner;                // C x P, preset to 0xffffffff
   long long lo, hi;
+  // ancestor-ordered shards (multi-rank philox; nullptr: identity): thread i handles particle
+  // own[i], and this rank's slice is positions [lo, hi) of that order
+  const int* own;
 };
 
 struct ScanArgs {
   int nb, C;
   int pt;                         // particles per dynamics-GP tile (seg_tile_start unit)
-  long long lo, hi;               // this rank's particle slice
+  long long lo, hi;               // this rank's particle slice (positions of the own order)
+  const int* own;                 // ownership order (nullptr: identity)
   const int* blockcounts;
   const int* cls_new;
   int* blockoff;                  // nb x C
@@ -57,6 +61,7 @@ struct GroupArgs {
   const int* cls_new;
   const int* class_start;
   const int* blockoff;
+  const int* own;                 // ownership order (nullptr: identity)
   int* perm;                      // grouped position -> particle
 };
 
@@ -119,6 +124,7 @@ struct ObsFinishArgs {
   double ll_const;                // 0.5 * D * ln(2 pi) in float32 (gpmdm_pf.py:5, 191)
   double* ll;                     // PF output (ll[ll_offset + o]) or nullptr
   long long ll_offset;
+  const int* own;                 // PF ownership order: ll[own[ll_offset + o]] (nullptr: identity)
   double* var_out;                // predictive map output n x D, or nullptr
   // fused mode (the tile kernel wrote spart instead of mu): ll from q and S partials
   const double* spart;            // [J][ld_q] for J in [jm0, n_j), or nullptr
@@ -172,11 +178,19 @@ inline long long guide_buckets_used(long long P) { return P >= kGuideMinP ? guid
 struct PackArgs {
   long long n, lo;
   int d;
+  const int* own;                 // row r holds particle own[lo + r] (nullptr: identity)
   double* buf;
   double* ll;
   int* cls;
   double* X;
 };
+
+// Ancestor-ordered shards (shard_order.hip): own = particles in stable order of their
+// resampling ancestor's bucket (256 contiguous ancestor ranges), so each rank's contiguous
+// slice of that order covers a contiguous range of ancestors.  Deterministic (identical on
+// every rank).  temp: ancestor_order_temp_bytes(P) of device memory.
+size_t ancestor_order_temp_bytes(long long P);
+int launch_ancestor_order(const int* anc, int* own, long long P, void* temp, size_t temp_bytes, hipStream_t s);
 
 void launch_switch(const SwitchArgs& a, hipStream_t s);
 void launch_scan_counts(const ScanArgs& a, hipStream_t s);

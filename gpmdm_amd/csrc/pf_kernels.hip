@@ -20,15 +20,21 @@ constexpr int kB = 256;   // threads per block of the O(P) kernels
 constexpr unsigned kMaxNormBlocks = 128;   // blocks per filter of k_norm_max
 
 // ---------------------------------------------------------------------------------
+// OWN: ancestor-ordered shards (thread i handles particle own[i]); the identity
+// instantiation keeps p == i visible to the compiler (one-rank path unchanged).
+template <bool OWN>
 __global__ __launch_bounds__(kB) void k_switch(SwitchArgs a) {
   __shared__ int hist[kMaxClasses];
   const int tid = threadIdx.x;
   if (tid < a.C) hist[tid] = 0;
-  const long long p = (long long)blockIdx.x * kB + tid;
+  const long long i = (long long)blockIdx.x * kB + tid;     // position in the ownership order
   long long dkey = -1;                              // de-duplication key (owner index)
-  if (a.gmax_reset && p < a.F) a.gmax_reset[p] = ord_enc(-INFINITY);
+  unsigned pid = 0;                                 // this thread's particle
+  if (a.gmax_reset && i < a.F) a.gmax_reset[i] = ord_enc(-INFINITY);
   __syncthreads();
-  if (p < a.P) {
+  if (i < a.P) {
+    const long long p = OWN ? (long long)a.own[i] : i;
+    pid = (unsigned)p;
     const int c0 = a.cls[p];
     const long long f = p / a.Pf;
     const uint2 key = filter_key(a.seed_lo, a.seed_hi, f);
@@ -55,12 +61,12 @@ __global__ __launch_bounds__(kB) void k_switch(SwitchArgs a) {
     }
     a.cls_new[p] = best;
     atomicAdd(&hist[best], 1);
-    if (a.owner && p >= a.lo && p < a.hi) dkey = (long long)best * a.P + f * a.Pf + a.anc[p];
+    if (a.owner && i >= a.lo && i < a.hi) dkey = (long long)best * a.P + f * a.Pf + a.anc[p];
   }
   if (a.owner) {
-    // Leader election: one atomicMin per distinct key per wave (its lowest lane = smallest
-    // p), so a collapsed cloud (every particle one ancestor) does not serialise P atomics
-    // on one address.
+    // Leader election: one atomicMin per distinct key per wave (its lowest lane), so a
+    // collapsed cloud (every particle one ancestor) does not serialise P atomics on one
+    // address.  The leader is deterministic; which particle leads does not change any value.
     const int lane = tid & 63;
     unsigned long long pending = __ballot(dkey >= 0);
     while (pending) {
@@ -69,7 +75,7 @@ __global__ __launch_bounds__(kB) void k_switch(SwitchArgs a) {
       const int hi32 = __shfl((int)(dkey >> 32), l0);
       const long long k0 = ((long long)hi32 << 32) | lo32;
       const unsigned long long same = __ballot(dkey == k0);
-      if (lane == l0) atomicMin(&a.owner[k0], (unsigned)p);
+      if (lane == l0) atomicMin(&a.owner[k0], pid);
       pending &= ~same;
     }
   }
@@ -119,7 +125,10 @@ __global__ __launch_bounds__(1024) void k_scan_counts(ScanArgs a) {
     const long long bound = which ? a.hi : a.lo;
     const long long bb = bound / kB;
     const long long start = bb * kB;
-    if (tid < kB && start + tid < bound) atomicAdd(which ? &hi_cnt[a.cls_new[start + tid]] : &lo_cnt[a.cls_new[start + tid]], 1);
+    if (tid < kB && start + tid < bound) {
+      const int cc = a.cls_new[a.own ? a.own[start + tid] : start + tid];
+      atomicAdd(which ? &hi_cnt[cc] : &lo_cnt[cc], 1);
+    }
     __syncthreads();
     if (tid < a.C) {
       const int base = bb < nb ? a.blockoff[bb * a.C + tid] : tot[tid];
@@ -147,11 +156,13 @@ __global__ __launch_bounds__(1024) void k_scan_counts(ScanArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
+template <bool OWN>
 __global__ __launch_bounds__(kB) void k_group(GroupArgs a) {
   __shared__ int wcount[kB / 64][kMaxClasses];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const long long p = (long long)blockIdx.x * kB + tid;
-  const int c = p < a.P ? a.cls_new[p] : -1;
+  const long long i = (long long)blockIdx.x * kB + tid;   // position in the ownership order
+  const long long p = i < a.P ? (OWN ? (long long)a.own[i] : i) : -1;
+  const int c = p >= 0 ? a.cls_new[p] : -1;
   int rank = 0;
   for (int k = 0; k < a.C; ++k) {
     const unsigned long long m = __ballot(c == k);
@@ -178,7 +189,7 @@ __global__ __launch_bounds__(kB) void k_group(GroupArgs a) {
 __device__ __forceinline__ int lead_flag(const LeadArgs& a, long long pos) {
   if (pos >= a.P) return 0;
   const long long p = a.perm[pos];
-  if (p < a.lo || p >= a.hi) return 0;
+  // only this rank's slice registered owners, so owner == p also means "p is in the slice"
   const long long f = p / a.Pf;
   return a.owner[(long long)a.cls_new[p] * a.P + f * a.Pf + a.anc[p]] == (unsigned)p;
 }
@@ -362,7 +373,7 @@ __global__ __launch_bounds__(kB) void k_obs_ll(ObsFinishArgs a) {
   double S = 0.0;
   for (int k = a.jm0; k < a.n_j; ++k) S += a.spart[(long long)k * a.ld_q + o];
   const double vc = 1.0 - q;                           // k(x*,x*) = 1 (gpmdm.py:991)
-  a.ll[a.ll_offset + o] = -0.5 * S / vc - a.D * log(vc) - a.sum_log_il2 - a.ll_const;
+  a.ll[a.own ? a.own[a.ll_offset + o] : a.ll_offset + o] = -0.5 * S / vc - a.D * log(vc) - a.sum_log_il2 - a.ll_const;
 }
 
 // ---------------------------------------------------------------------------------
@@ -581,7 +592,7 @@ __global__ __launch_bounds__(256) void k_readout(ResampleArgs a) {
 __global__ __launch_bounds__(kB) void k_pack(PackArgs a) {
   const long long r = (long long)blockIdx.x * kB + threadIdx.x;
   if (r >= a.n) return;
-  const long long p = a.lo + r;
+  const long long p = a.own ? a.own[a.lo + r] : a.lo + r;
   double* o = a.buf + r * (a.d + 2);
   o[0] = a.ll[p];
   o[1] = (double)a.cls[p];
@@ -589,9 +600,10 @@ __global__ __launch_bounds__(kB) void k_pack(PackArgs a) {
 }
 
 __global__ __launch_bounds__(kB) void k_unpack(PackArgs a) {
-  const long long p = (long long)blockIdx.x * kB + threadIdx.x;
-  if (p >= a.n) return;
-  const double* i = a.buf + p * (a.d + 2);
+  const long long r = (long long)blockIdx.x * kB + threadIdx.x;   // row = ownership position
+  if (r >= a.n) return;
+  const long long p = a.own ? a.own[r] : r;
+  const double* i = a.buf + r * (a.d + 2);
   a.ll[p] = i[0];
   a.cls[p] = (int)i[1];
   for (int j = 0; j < a.d; ++j) a.X[p * a.d + j] = i[2 + j];
@@ -601,13 +613,19 @@ __global__ __launch_bounds__(kB) void k_unpack(PackArgs a) {
 static inline unsigned nblk(long long n, int b) { return (unsigned)((n + b - 1) / b); }
 
 void launch_switch(const SwitchArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_switch, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+  if (a.own)
+    hipLaunchKernelGGL(k_switch<true>, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_switch<false>, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
 }
 void launch_scan_counts(const ScanArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, a);
 }
 void launch_group(const GroupArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_group, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+  if (a.own)
+    hipLaunchKernelGGL(k_group<true>, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_group<false>, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
 }
 void launch_lead(const LeadArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_lead_flags, dim3((unsigned)a.nb), dim3(kB), 0, s, a);

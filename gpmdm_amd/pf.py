@@ -14,6 +14,9 @@ every per-frame computation runs in the HIP library.  Extra keyword options:
 * ``dedup`` (default True): evaluate the dynamics GP once per distinct (resampling
   ancestor, new class) pair -- offspring of one ancestor hold bit-identical states -- and
   share the result; bitwise identical to ``dedup=False`` (every particle evaluated).
+* ``shard_order`` (default True; multi-rank philox filters): each rank evaluates a slice of
+  the particles ordered by resampling ancestor rather than a slice of particle indices, so
+  de-duplication keeps ~1/R of the distinct keys per rank; bitwise identical either way.
 
 Reference quirks kept for parity: log variance counted twice in the
 log-likelihood, float32 ``ln 2pi``, non-recursive weights, read-outs pairing
@@ -34,7 +37,7 @@ from .model import GPMDM
 class GPMDM_PF:
     def __init__(self, gpmdm: GPMDM, markov_switching_model, num_particles: int, *,
                  rng: str = "torch", seed=None, resample: str = "multinomial", process_group=None,
-                 shard=None, exchange=None, dedup: bool = True):
+                 shard=None, exchange=None, dedup: bool = True, shard_order: bool = True):
         self._gpmdm = gpmdm
         self._gpmdm.set_evaluation_mode()
         self._markov_switching_model = torch.as_tensor(markov_switching_model).type(self.dtype)
@@ -70,6 +73,7 @@ class GPMDM_PF:
             self._world, self._rank, ctypes.byref(h)), "GPMDM_PF")
         self._h = h
         _lib.check(lib.gpmdm_pf_set_dedup(h, 1 if dedup else 0), "dedup")
+        _lib.check(lib.gpmdm_pf_set_shard_order(h, 1 if shard_order else 0), "shard_order")
         self._readout = None
         if self._world > 1:
             w, lo, hi = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()

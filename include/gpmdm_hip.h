@@ -185,6 +185,15 @@ int gpmdm_pf_stage_times(gpmdm_pf_t pf, double* ms, int64_t* launches);
 int gpmdm_pf_set_dedup(gpmdm_pf_t pf, int enable);
 int gpmdm_pf_dyn_rows(gpmdm_pf_t pf, int64_t* rows, void* stream);
 
+/* Ancestor-ordered shards (multi-rank philox filters; default on).  After each resample the
+ * particles are put in a stable order of their resampling ancestor's bucket (256 contiguous
+ * ancestor ranges; identical on every rank) and rank r evaluates positions [lo, hi) of that
+ * order instead of particles [lo, hi), so its slice covers a contiguous ancestor range and
+ * de-duplication keeps ~1/R of the distinct (ancestor, class) keys.  Pack/unpack rows follow the same order, so the all-gathered
+ * filter is bitwise the same either way.  No effect on one rank, replay draws or without
+ * de-duplication.  Every rank must make the same call, outside switch..resample. */
+int gpmdm_pf_set_shard_order(gpmdm_pf_t pf, int enable);
+
 /* Device-side GP factor: the recipe of _precompute_kernel_inverses
  * (gpmdm.py:1284-1305) for one GP block -- the observation GP, or one class block of the
  * dynamics GP (the reference's full masked matrix has exact zeros off the class blocks):

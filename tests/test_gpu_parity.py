@@ -414,12 +414,14 @@ def test_tiny_model_and_particle_counts(P):
         assert nrel(pf.current_state_mean().numpy(), r.mean) < 1e-6, k
 
 
-@pytest.mark.parametrize("world,rng_mode", [(4, "philox"), (8, "philox"), (3, "torch")])
-def test_logical_shards_match_one_rank(m2, world, rng_mode):
+@pytest.mark.parametrize("world,rng_mode,order", [(4, "philox", True), (8, "philox", True), (8, "philox", False),
+                                                  (3, "torch", True)])
+def test_logical_shards_match_one_rank(m2, world, rng_mode, order):
     """results at R ranks equal the single-rank filter, with R logical shards
     on one GPU and the all-gather done in-process.  Philox draws at 4 and 8 ranks; the
     replay stream (torch generator) at 3 ranks, every rank drawing the same full streams
-    in the reference's order (gpmdm_amd.replay).  P = 10007 (uneven shards)."""
+    in the reference's order (gpmdm_amd.replay).  P = 10007 (uneven shards).  Philox ranks
+    run with and without ancestor-ordered shards (``shard_order``)."""
     from gpmdm_amd import GPMDM_PF, _lib, replay
     T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
     P = 10_007
@@ -429,7 +431,7 @@ def test_logical_shards_match_one_rank(m2, world, rng_mode):
     ranks = []
     for r in range(world):
         torch.manual_seed(4)
-        ranks.append(GPMDM_PF(m2, T, P, rng=rng_mode, seed=91, shard=(world, r)))
+        ranks.append(GPMDM_PF(m2, T, P, rng=rng_mode, seed=91, shard=(world, r), shard_order=order))
     lib = _lib.load()
     for k in range(3):
         z = np.ascontiguousarray(np.asarray(Y[60 + 3 * k], dtype=np.float64))
@@ -462,6 +464,13 @@ def test_logical_shards_match_one_rank(m2, world, rng_mode):
             for pf in ranks:
                 pf._recv.copy_(full)
                 pf._stage_resample()
+            if k > 0 and order:
+                # ancestor-ordered shards: each rank's slice covers a contiguous range of
+                # ancestor buckets (256 per filter), so the ranks together evaluate the
+                # single rank's distinct (ancestor, class) keys plus at most those of one
+                # shared bucket per shard boundary (C x P/256 keys)
+                rows = [pf.dynamics_rows() for pf in ranks]
+                assert sum(rows) <= ref.dynamics_rows() + 2 * (world - 1) * -(-P // 256), (k, rows, ref.dynamics_rows())
         a = ref.export_state()
         for pf in ranks:
             b = pf.export_state()

@@ -7,6 +7,12 @@ switch / grouping / normalise / resample / read-out kernels grow with N -- and o
 collective itself is missing, so the result is the compute floor of each rank's step.
 
     python tools/scale_sim.py [steps] [N,N,...]
+    python tools/scale_sim.py --ranks [--no-order] [steps] [N,N,...]
+
+--ranks runs all N ranks on the one GPU, one after another, with the real exchange done
+in-process (the data every rank sees is exactly what an N-GPU run sees), and reports each
+rank's GPU time per step from its stage events (kernels only, no host gaps) and its
+dynamics-GP rows; the slowest rank bounds the N-GPU step.
 """
 import sys
 import time
@@ -39,6 +45,8 @@ def main():
             pf.update(zs[k])
             pf.class_probabilities()
         torch.cuda.synchronize()
+        pf.stage_times()
+        pf.enable_timing(True)
         t0 = time.perf_counter()
         for k in range(steps):
             pf.update(zs[5 + k])
@@ -47,10 +55,66 @@ def main():
             pf.current_state_mean()
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / steps * 1e3
+        pf.enable_timing(False)
+        st = {k: round(v[0] / max(v[1], 1), 4) for k, v in pf.stage_times().items()}
         print(f"N={n}: P_total={P}, per-rank step {ms:.3f} ms (no collective), "
-              f"weak-scaling floor {100_000 * n * 1e3 / ms:.3e} particle-steps/s", flush=True)
+              f"weak-scaling floor {100_000 * n * 1e3 / ms:.3e} particle-steps/s; "
+              f"dyn rows {pf.dynamics_rows()}; stages ms {st}", flush=True)
         del pf
 
 
+def ranks_mode():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    order = "--no-order" not in sys.argv
+    steps = int(args[0]) if args else 20
+    bench.WORKLOAD = bench.workload(2)
+    from gpmdm_amd import GPMDM_PF, synthetic
+    dev = torch.device("cuda", 0)
+    model, data = bench.build_model(dev)
+    T = torch.from_numpy(synthetic.markov_matrix(2))
+    zs = data.observation_stream(steps + 5, seed=1)
+    ns = [int(x) for x in args[1].split(",")] if len(args) > 1 else [1, 2, 4, 8]
+    for n in ns:
+        P = 100_000 * n
+        pfs = [GPMDM_PF(model, T, P, rng="philox", seed=11, shard=(n, r) if n > 1 else None,
+                        shard_order=order) for r in range(n)]
+
+        def step(k):
+            if n == 1:
+                pfs[0].update(zs[k])
+            else:
+                full = torch.cat([pf._stage_propagate(zs[k]) for pf in pfs], 0)
+                for pf in pfs:
+                    pf._recv.copy_(full)
+                    pf._stage_resample()
+            for pf in pfs:
+                pf.class_probabilities()
+
+        for k in range(5):
+            step(k)
+        torch.cuda.synchronize()
+        for pf in pfs:
+            pf.stage_times()
+            pf.enable_timing(True)
+        rows = [0] * n
+        for k in range(steps):
+            step(5 + k)
+            for r, pf in enumerate(pfs):
+                rows[r] += pf.dynamics_rows()
+        torch.cuda.synchronize()
+        per = []
+        for pf in pfs:
+            pf.enable_timing(False)
+            st = pf.stage_times()
+            per.append({k: v[0] / max(v[1], 1) for k, v in st.items()})
+        tot = [sum(p.values()) for p in per]
+        worst = max(range(n), key=lambda r: tot[r])
+        print(f"[shard_order={order}] N={n}: P_total={P}, GPU ms per step per rank: max {max(tot):.3f} min {min(tot):.3f} "
+              f"(rank {worst}: dyn_gemm {per[worst]['dyn_gemm']:.3f} obs_gemm {per[worst]['obs_gemm']:.3f} "
+              f"switch {per[worst]['switch']:.3f} resample {per[worst]['resample']:.3f}); "
+              f"dyn rows per rank (mean over steps): {[r // steps for r in rows]}", flush=True)
+        del pfs
+
+
 if __name__ == "__main__":
-    main()
+    ranks_mode() if "--ranks" in sys.argv else main()
