@@ -221,6 +221,7 @@ struct gpmdm_pf {
   // observation upload through two pinned slots (a pageable hipMemcpyAsync is staged by the
   // runtime and stalls the launching thread); each slot's event guards its reuse
   double* zpin[2] = {nullptr, nullptr};
+  double* rpin = nullptr;             // pinned read-out landing buffer (F x (C + d + 1))
   hipEvent_t zev[2] = {nullptr, nullptr};
   int zslot = 0;
   double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *sobs = nullptr;
@@ -260,6 +261,7 @@ struct gpmdm_pf {
     dfree(owner);
     for (auto& r : recs) { pool.push_back(r.a); pool.push_back(r.b); }
     for (auto ev : pool) (void)hipEventDestroy(ev);
+    if (rpin) (void)hipHostFree(rpin);
     for (int k = 0; k < 2; ++k) {
       if (zpin[k]) (void)hipHostFree(zpin[k]);
       if (zev[k]) (void)hipEventDestroy(zev[k]);
@@ -562,6 +564,10 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
       delete pf;
       return fail(GPMDM_E_NOMEM, "pinned observation buffer");
     }
+  }
+  if (hipHostMalloc((void**)&pf->rpin, sizeof(double) * F * (C + d + 1)) != hipSuccess) {
+    delete pf;
+    return fail(GPMDM_E_NOMEM, "pinned read-out buffer");
   }
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, m->obs.tiles(pf->nloc)};
   if (hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess ||
@@ -1000,11 +1006,10 @@ int gpmdm_pf_read(gpmdm_pf_t pf, double* post, double* mean, double* lik, void* 
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;
   const int nr = m->C + m->d + 1;
-  std::vector<double> buf((size_t)pf->F * nr);
-  HIPCHK(hipMemcpyAsync(buf.data(), pf->readout, sizeof(double) * buf.size(), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(pf->rpin, pf->readout, sizeof(double) * pf->F * nr, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   for (int f = 0; f < pf->F; ++f) {
-    const double* b = buf.data() + (size_t)f * nr;
+    const double* b = pf->rpin + (size_t)f * nr;
     if (post) std::memcpy(post + (size_t)f * m->C, b, sizeof(double) * m->C);
     if (mean) std::memcpy(mean + (size_t)f * m->d, b + m->C, sizeof(double) * m->d);
     if (lik) lik[f] = b[m->C + m->d];
