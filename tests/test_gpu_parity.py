@@ -414,17 +414,18 @@ def test_tiny_model_and_particle_counts(P):
         assert nrel(pf.current_state_mean().numpy(), r.mean) < 1e-6, k
 
 
-@pytest.mark.parametrize("world,rng_mode,order", [(4, "philox", True), (8, "philox", True), (8, "philox", False),
-                                                  (3, "torch", True)])
-def test_logical_shards_match_one_rank(m2, world, rng_mode, order):
+@pytest.mark.parametrize("world,rng_mode,order,P", [(4, "philox", True, 10_007), (8, "philox", True, 10_007),
+                                                    (8, "philox", False, 10_007), (3, "torch", True, 10_007),
+                                                    (8, "philox", True, 400_003)])
+def test_logical_shards_match_one_rank(m2, world, rng_mode, order, P):
     """results at R ranks equal the single-rank filter, with R logical shards
     on one GPU and the all-gather done in-process.  Philox draws at 4 and 8 ranks; the
     replay stream (torch generator) at 3 ranks, every rank drawing the same full streams
     in the reference's order (gpmdm_amd.replay).  P = 10007 (uneven shards).  Philox ranks
-    run with and without ancestor-ordered shards (``shard_order``)."""
+    run with and without ancestor-ordered shards (``shard_order``); P = 400003 at 8 ranks
+    exercises the bucket pass at bench scale and the guide-table resample search."""
     from gpmdm_amd import GPMDM_PF, _lib, replay
     T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
-    P = 10_007
     Y = m2.get_Y()
     torch.manual_seed(4)
     ref = GPMDM_PF(m2, T, P, rng=rng_mode, seed=91)
