@@ -34,6 +34,14 @@ from . import _lib, replay
 from .model import GPMDM
 
 
+def _as_f64_vector(z) -> np.ndarray:
+    """The observation as a contiguous float64 vector (the reference casts it with
+    torch.tensor(z, dtype=float64), gpmdm_pf.py:123; float32 -> float64 is exact)."""
+    if isinstance(z, np.ndarray):
+        return np.ascontiguousarray(z, dtype=np.float64).reshape(-1)
+    return np.ascontiguousarray(torch.as_tensor(z, dtype=torch.float64).cpu().numpy().reshape(-1))
+
+
 class GPMDM_PF:
     def __init__(self, gpmdm: GPMDM, markov_switching_model, num_particles: int, *,
                  rng: str = "torch", seed=None, resample: str = "multinomial", process_group=None,
@@ -117,7 +125,7 @@ class GPMDM_PF:
 
     def update(self, z):
         """gpmdm_pf.py:117-135: switch classes, propagate dynamics, weight, resample."""
-        z = np.ascontiguousarray(torch.as_tensor(z, dtype=torch.float64).cpu().numpy().reshape(-1))
+        z = _as_f64_vector(z)
         if z.shape[0] != self.observation_dim:
             raise ValueError(f"observation must have {self.observation_dim} values, got {z.shape[0]}")
         lib, h, s = _lib.load(), self._h, self._stream()
@@ -146,7 +154,7 @@ class GPMDM_PF:
         uniforms P (multinomial) or 1 (systematic).  Requires rng='torch'."""
         if self._rng != "torch":
             raise ValueError("explicit draws need rng='torch' (replay mode)")
-        z = np.ascontiguousarray(torch.as_tensor(z, dtype=torch.float64).cpu().numpy().reshape(-1))
+        z = _as_f64_vector(z)
         lib, h, s = _lib.load(), self._h, self._stream()
         P, C, d = self._num_particles, self.num_classes, self.latent_dim
         E = np.ascontiguousarray(exp_draws, dtype=np.float64).reshape(P, C)
@@ -200,15 +208,16 @@ class GPMDM_PF:
 
     def class_probabilities(self) -> torch.Tensor:
         """gpmdm_pf.py:224-248."""
-        return torch.tensor(self._read()[0], dtype=torch.float64)
+        return torch.from_numpy(self._read()[0].copy())
 
     def get_most_likely_class(self) -> int:
-        """gpmdm_pf.py:250-254."""
-        return int(torch.argmax(self.class_probabilities()).item())
+        """gpmdm_pf.py:250-254 (argmax, first maximum as torch.argmax; numpy on the cached
+        read-out: no tensor round trip in the per-frame loop)."""
+        return int(np.argmax(self._read()[0]))
 
     def current_state_mean(self) -> torch.Tensor:
         """gpmdm_pf.py:256-262."""
-        return torch.tensor(self._read()[1], dtype=torch.float64)
+        return torch.from_numpy(self._read()[1].copy())
 
     def predict(self) -> torch.Tensor:
         """Dynamics-only one-step prediction of the latent mean: the average over the
