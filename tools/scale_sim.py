@@ -7,7 +7,7 @@ switch / grouping / normalise / resample / read-out kernels grow with N -- and o
 collective itself is missing, so the result is the compute floor of each rank's step.
 
     python tools/scale_sim.py [steps] [N,N,...]
-    python tools/scale_sim.py --ranks [--no-order] [steps] [N,N,...]
+    python tools/scale_sim.py --ranks [--no-order] [--per-rank=P] [steps] [N,N,...]
 
 --ranks runs all N ranks on the one GPU, one after another, with the real exchange done
 in-process (the data every rank sees is exactly what an N-GPU run sees), and reports each
@@ -66,6 +66,7 @@ def main():
 def ranks_mode():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     order = "--no-order" not in sys.argv
+    per_rank = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--per-rank=")), 100_000)
     steps = int(args[0]) if args else 20
     bench.WORKLOAD = bench.workload(2)
     from gpmdm_amd import GPMDM_PF, synthetic
@@ -75,7 +76,7 @@ def ranks_mode():
     zs = data.observation_stream(steps + 5, seed=1)
     ns = [int(x) for x in args[1].split(",")] if len(args) > 1 else [1, 2, 4, 8]
     for n in ns:
-        P = 100_000 * n
+        P = per_rank * n
         pfs = [GPMDM_PF(model, T, P, rng="philox", seed=11, shard=(n, r) if n > 1 else None,
                         shard_order=order) for r in range(n)]
 
