@@ -57,6 +57,7 @@ _SIGS = {
     "gpmdm_pf_stage_times": (c_int, [c_void_p, _dp, _i64p]),
     "gpmdm_pf_set_dedup": (c_int, [c_void_p, c_int]),
     "gpmdm_pf_set_shard_order": (c_int, [c_void_p, c_int]),
+    "gpmdm_pf_timing_stages": (c_int, [c_void_p, ctypes.c_uint]),
     "gpmdm_pf_dyn_rows": (c_int, [c_void_p, _i64p, c_void_p]),
     "gpmdm_gp_factor": (c_int, [c_int, _dp, c_int64, c_int32, _dp, _dp, c_double, c_double, c_double,
                                 _dp, c_int64, _dp, _dp]),

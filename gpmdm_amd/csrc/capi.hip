@@ -276,9 +276,10 @@ struct gpmdm_pf {
     (void)hipEventCreateWithFlags(&x, hipEventDisableSystemFence);
     return x;
   }
-  void mark_begin(hipStream_t s, hipEvent_t& a) {
+  unsigned timing_mask = (1u << GPMDM_N_STAGES) - 1;   // gpmdm_pf_timing_stages
+  void mark_begin(hipStream_t s, int stage, hipEvent_t& a) {
     a = nullptr;
-    if (timing) { a = ev(); (void)hipEventRecord(a, s); }
+    if (timing && (timing_mask >> stage & 1u)) { a = ev(); (void)hipEventRecord(a, s); }
   }
   void mark_end(hipStream_t s, int stage, hipEvent_t a) {
     if (!timing || !a) return;
@@ -690,7 +691,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
     HIPCHK(hipMemcpyAsync(pf->E, E, sizeof(double) * pf->P * C, hipMemcpyHostToDevice, s));
   }
   hipEvent_t t0;
-  pf->mark_begin(s, t0);
+  pf->mark_begin(s, GPMDM_STAGE_SWITCH, t0);
   if (pf->dedup && pf->nloc > 0)
     HIPCHK(hipMemsetAsync(pf->owner, 0xff, sizeof(unsigned) * C * pf->P, s));
   SwitchArgs sa{};
@@ -801,7 +802,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
   if (nl > 0) {
     // ---- dynamics GP per class (segments of at most kMaxSeg classes per launch) ----
     hipEvent_t t0;
-    pf->mark_begin(s, t0);
+    pf->mark_begin(s, GPMDM_STAGE_DYN_GEMM, t0);
     for (int c0 = 0; c0 < C; c0 += kMaxSeg) {
       const int ns = std::min(kMaxSeg, C - c0);
       TileParams tp{};
@@ -836,7 +837,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
       launch_gp_tile(tp, d, true, s);
     }
     pf->mark_end(s, GPMDM_STAGE_DYN_GEMM, t0);
-    pf->mark_begin(s, t0);
+    pf->mark_begin(s, GPMDM_STAGE_DYN_FINISH, t0);
     DynFinishArgs fa{};
     fa.n_out = nl;
     fa.Pf = pf->Pf;
@@ -867,7 +868,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     pf->mark_end(s, GPMDM_STAGE_DYN_FINISH, t0);
 
     // ---- observation GP + likelihood over particles [lo, hi) ----
-    pf->mark_begin(s, t0);
+    pf->mark_begin(s, GPMDM_STAGE_OBS_GEMM, t0);
     TileParams tp{};
     tp.seg[0] = m->obs.seg();
     tp.n_seg = 1;
@@ -889,7 +890,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     tp.Pf = pf->Pf;
     launch_gp_tile(tp, d, false, s);
     pf->mark_end(s, GPMDM_STAGE_OBS_GEMM, t0);
-    pf->mark_begin(s, t0);
+    pf->mark_begin(s, GPMDM_STAGE_OBS_FINISH, t0);
     ObsFinishArgs oa{};
     oa.n_out = nl;
     oa.n_parts = m->obs.n_parts();
@@ -970,7 +971,7 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
     HIPCHK(hipMemcpyAsync(pf->U, uniforms, sizeof(double) * (sys ? 1 : pf->P), hipMemcpyHostToDevice, s));
   }
   hipEvent_t t0;
-  pf->mark_begin(s, t0);
+  pf->mark_begin(s, GPMDM_STAGE_RESAMPLE, t0);
   launch_normalise(norm_args(pf), s);
   ResampleArgs ra = resample_args(pf);
   ra.U = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->U : nullptr;
@@ -1088,6 +1089,12 @@ int gpmdm_pf_dyn_rows(gpmdm_pf_t pf, int64_t* rows, void* stream) {
 int gpmdm_pf_enable_timing(gpmdm_pf_t pf, int enable) {
   CHECK(pf, "null handle");
   pf->timing = enable != 0;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_timing_stages(gpmdm_pf_t pf, unsigned mask) {
+  CHECK(pf, "null handle");
+  pf->timing_mask = mask & ((1u << GPMDM_N_STAGES) - 1);
   return GPMDM_OK;
 }
 

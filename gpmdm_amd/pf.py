@@ -258,8 +258,16 @@ class GPMDM_PF:
         _lib.check(_lib.load().gpmdm_pf_dyn_rows(self._h, _lib.i64ptr(r), self._stream()), "dyn_rows")
         return int(r[0])
 
-    def enable_timing(self, on: bool = True):
-        _lib.check(_lib.load().gpmdm_pf_enable_timing(self._h, 1 if on else 0))
+    def enable_timing(self, on: bool = True, stages=None):
+        """Record per-stage HIP events (``stages``: names from ``_lib.STAGES``; default all).
+        Each recorded stage adds two event records to the stream."""
+        lib = _lib.load()
+        names = _lib.STAGES if stages is None else tuple(stages)
+        mask = 0
+        for n in names:
+            mask |= 1 << _lib.STAGES.index(n)
+        _lib.check(lib.gpmdm_pf_timing_stages(self._h, mask))
+        _lib.check(lib.gpmdm_pf_enable_timing(self._h, 1 if on else 0))
 
     def stage_times(self) -> dict:
         ms = np.zeros(len(_lib.STAGES))

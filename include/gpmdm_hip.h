@@ -172,6 +172,9 @@ int gpmdm_pf_export(gpmdm_pf_t pf, double* states, int64_t* classes, double* ll,
 #define GPMDM_STAGE_RESAMPLE 5
 #define GPMDM_N_STAGES 6
 int gpmdm_pf_enable_timing(gpmdm_pf_t pf, int enable);
+/* Which stages record events while timing is on: bit (1 << GPMDM_STAGE_*) per stage,
+ * default all.  Each recorded stage adds two event records to the stream. */
+int gpmdm_pf_timing_stages(gpmdm_pf_t pf, unsigned mask);
 int gpmdm_pf_stage_times(gpmdm_pf_t pf, double* ms, int64_t* launches);
 
 /* Ancestor de-duplication of the dynamics GP (default on).  After a resample, offspring of
