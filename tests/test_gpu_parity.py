@@ -504,3 +504,23 @@ def test_empty_class_segments(m2, fx_config2):
         assert nrel(st["states"], r.states) < 1e-6
         post = pf.class_probabilities().numpy()
         assert post[1] == 0.0 and abs(post[0] - 1.0) < 1e-15
+
+
+def test_stage_selective_timing(m2):
+    """gpmdm_pf_timing_stages: with only the observation-GP stage selected, each step records
+    exactly that stage (the bench's timed region); all stages by default."""
+    from gpmdm_amd import GPMDM_PF
+    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
+    Y = m2.get_Y()
+    pf = GPMDM_PF(m2, T, 3000, rng="philox", seed=3)
+    pf.enable_timing(True, stages=("obs_gemm",))
+    for k in range(3):
+        pf.update(Y[k])
+    st = pf.stage_times()
+    assert st["obs_gemm"][1] == 3 and st["obs_gemm"][0] > 0.0, st
+    assert all(n == 0 for k, (ms, n) in st.items() if k != "obs_gemm"), st
+    pf.enable_timing(True)
+    pf.update(Y[3])
+    st = pf.stage_times()
+    pf.enable_timing(False)
+    assert all(n == 1 for ms, n in st.values()), st
