@@ -3,7 +3,7 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config {2,3,4,5}]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Workload (BASELINE.json configs[1]): N=2000 training latents, D=62, d=3, C=2 classes,
+Workload (BASELINE.json configs[1]): N=2000 training latents, D=62, d=3, C=2 classes, 500 frames,
 P=100,000 particles per GPU (weak scaling: P_total = 100k x GPUs), synthetic model and
 observation stream.  One step = ``update(z)`` + ``class_probabilities()``
 + ``current_state_mean()``, the notebook's per-frame loop (test_gpmdm_pf.ipynb:197-201),
@@ -142,13 +142,16 @@ def cpu_baseline(data, budget_s=12.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed frames (default: 500, configs[1]'s 500 frames; 20 for configs 3 and 5)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 4, 5))
     args = ap.parse_args()
     global WORKLOAD
     WORKLOAD = workload(args.config)
+    if args.steps is None:
+        args.steps = 20 if args.config in (3, 5) else 500
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -249,6 +252,7 @@ def main():
         "config": {"workload": f"configs[{WORKLOAD['cfg'] - 1}]: N={N} D={D} d={d} C={model.n_classes}, "
                                f"P={P_local} particles per GPU, philox draws, multinomial resampling",
                    "N": N, "D": D, "d": d, "C": model.n_classes, "P_per_gpu": P_local, "P_total": P_total,
+                   "frames": args.warmup + args.steps,
                    "parallelism": f"particles sharded over {world} GPU(s), one all-gather per step"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
