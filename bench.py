@@ -86,6 +86,11 @@ def obs_kernel_flops(N, D, bk=16):
     return algorithmic, dense_form, executed
 
 
+def obs_model_bytes(N, D):
+    """Algorithmic model bytes of the observation GP: the non-zeros of triu(R) and K^-1 Y."""
+    return 8.0 * (N * (N + 1) / 2 + N * D)
+
+
 def pmc_traffic():
     """HBM bytes per launch of the obs tile kernel from the committed PMC summary."""
     p = ROOT / "profiles" / "pmc_summary.json"
@@ -236,6 +241,8 @@ def main():
     obs_ms, obs_n = stages["obs_gemm"]
     obs_launch_s = obs_ms / max(obs_n, 1) / 1e3
     achieved = alg * P_local / obs_launch_s / 1e12
+    traffic = pmc_traffic() if WORKLOAD["cfg"] == 2 else None
+    b_image = obs_model_bytes(N, D)
     rec = {
         "metric": METRIC,
         "value": P_total * args.steps / elapsed,
@@ -256,7 +263,14 @@ def main():
                    "parallelism": f"particles sharded over {world} GPU(s), one all-gather per step"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
-                     "traffic": pmc_traffic() if WORKLOAD["cfg"] == 2 else None,
+                     "traffic": traffic,
+                     "traffic_GBps": traffic / obs_launch_s / 1e9 if traffic else None,
+                     "traffic_note": ("HBM/MALL bytes per launch from the committed rocprofv3 PMC passes "
+                                      "(profiles/pmc_summary.json); the algorithmic bytes are triu(R) and K^-1 Y "
+                                      f"({b_image / 1e6:.1f} MB) plus the particles; each XCD re-streams B panels "
+                                      "once per round of concurrently resident tiles (L2 hit 97%), which costs "
+                                      "nothing measurable: the kernel is FP64-MFMA bound at a few % of HBM "
+                                      "bandwidth (DESIGN.md §3)") if traffic else None,
                      "kernel": f"k_gp_tile<{d},false> (observation GP)",
                      "flops_per_particle_algorithmic": alg, "flops_per_particle_executed": executed,
                      "flops_per_particle_dense_form": dense,
