@@ -694,8 +694,16 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   pf->mark_begin(s, GPMDM_STAGE_SWITCH, t0);
   if (pf->dedup && pf->nloc > 0)
     HIPCHK(hipMemsetAsync(pf->owner, 0xff, sizeof(unsigned) * C * pf->P, s));
+  // Multi-rank Philox filters switch and group only their own slice (the classes of the
+  // other particles arrive with the all-gather); otherwise all P (replay draws are indexed
+  // by the global class grouping).
+  const bool sl = pf->n_ranks > 1 && pf->rng_mode == GPMDM_RNG_PHILOX;
+  const long long base = sl ? pf->lo : 0, nsw = sl ? pf->nloc : pf->P;
+  const int nbs = (int)std::max<long long>(cdiv(nsw, 256), 1);
   SwitchArgs sa{};
   sa.P = pf->P;
+  sa.base = base;
+  sa.n = nsw;
   sa.Pf = pf->Pf;
   sa.F = pf->F;
   sa.C = C;
@@ -717,12 +725,13 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   sa.own = pf->own_order();
   launch_switch(sa, s);
   ScanArgs sc{};
-  sc.nb = pf->nb;
+  sc.nb = nbs;
   sc.C = C;
   sc.pt = m->dyn[0].geo.pt();
-  sc.lo = pf->lo;
-  sc.hi = pf->hi;
+  sc.lo = sl ? 0 : pf->lo;
+  sc.hi = sl ? pf->nloc : pf->hi;
   sc.own = pf->own_order();
+  sc.base = base;
   sc.blockcounts = pf->blockcounts;
   sc.cls_new = pf->cls_new;
   sc.blockoff = pf->blockoff;
@@ -735,6 +744,8 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   launch_scan_counts(sc, s);
   GroupArgs ga{};
   ga.P = pf->P;
+  ga.base = base;
+  ga.n = nsw;
   ga.C = C;
   ga.cls_new = pf->cls_new;
   ga.class_start = pf->class_start();
@@ -748,7 +759,8 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
     la.Pf = pf->Pf;
     la.lo = pf->lo;
     la.hi = pf->hi;
-    la.nb = pf->nb;
+    la.npos = nsw;
+    la.nb = nbs;
     la.C = C;
     la.pt = m->dyn[0].geo.pt();
     la.perm = pf->perm;

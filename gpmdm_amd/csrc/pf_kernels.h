@@ -19,6 +19,8 @@ __device__ __forceinline__ uint2 filter_key(unsigned seed_lo, unsigned seed_hi, 
 
 struct SwitchArgs {
   long long P;                    // all particles (F * Pf)
+  long long base, n;              // positions [base, base + n) of the ownership order are switched
+                                  // (all: 0, P; a multi-rank Philox rank: its slice)
   long long Pf;                   // particles per filter
   int C, F;
   unsigned frame, seed_lo, seed_hi;
@@ -40,10 +42,11 @@ struct SwitchArgs {
 };
 
 struct ScanArgs {
-  int nb, C;
+  int nb, C;                      // nb: blocks of k_switch's histogram
   int pt;                         // particles per dynamics-GP tile (seg_tile_start unit)
   long long lo, hi;               // this rank's particle slice (positions of the own order)
   const int* own;                 // ownership order (nullptr: identity)
+  long long base;                 // position pos of the grouped range is particle own[base + pos]
   const int* blockcounts;
   const int* cls_new;
   int* blockoff;                  // nb x C
@@ -57,6 +60,7 @@ struct ScanArgs {
 
 struct GroupArgs {
   long long P;
+  long long base, n;              // as SwitchArgs
   int C;
   const int* cls_new;
   const int* class_start;
@@ -67,7 +71,8 @@ struct GroupArgs {
 
 // Leader compaction over the class-grouped positions (ancestor de-duplication).
 struct LeadArgs {
-  long long P, Pf, lo, hi;
+  long long P, Pf, lo, hi;        // P: all particles (key stride)
+  long long npos;                 // grouped positions (P, or the rank's slice)
   int nb, C;
   int pt;                         // particles per dynamics-GP tile
   const int* perm;                // grouped position -> particle

@@ -27,12 +27,13 @@ __global__ __launch_bounds__(kB) void k_switch(SwitchArgs a) {
   __shared__ int hist[kMaxClasses];
   const int tid = threadIdx.x;
   if (tid < a.C) hist[tid] = 0;
-  const long long i = (long long)blockIdx.x * kB + tid;     // position in the ownership order
+  const long long t = (long long)blockIdx.x * kB + tid;
+  const long long i = a.base + t;                   // position in the ownership order
   long long dkey = -1;                              // de-duplication key (owner index)
   unsigned pid = 0;                                 // this thread's particle
-  if (a.gmax_reset && i < a.F) a.gmax_reset[i] = ord_enc(-INFINITY);
+  if (a.gmax_reset && t < a.F) a.gmax_reset[t] = ord_enc(-INFINITY);
   __syncthreads();
-  if (i < a.P) {
+  if (t < a.n) {
     const long long p = OWN ? (long long)a.own[i] : i;
     pid = (unsigned)p;
     const int c0 = a.cls[p];
@@ -126,7 +127,8 @@ __global__ __launch_bounds__(1024) void k_scan_counts(ScanArgs a) {
     const long long bb = bound / kB;
     const long long start = bb * kB;
     if (tid < kB && start + tid < bound) {
-      const int cc = a.cls_new[a.own ? a.own[start + tid] : start + tid];
+      const long long q = a.base + start + tid;
+      const int cc = a.cls_new[a.own ? a.own[q] : q];
       atomicAdd(which ? &hi_cnt[cc] : &lo_cnt[cc], 1);
     }
     __syncthreads();
@@ -160,8 +162,9 @@ template <bool OWN>
 __global__ __launch_bounds__(kB) void k_group(GroupArgs a) {
   __shared__ int wcount[kB / 64][kMaxClasses];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const long long i = (long long)blockIdx.x * kB + tid;   // position in the ownership order
-  const long long p = i < a.P ? (OWN ? (long long)a.own[i] : i) : -1;
+  const long long t = (long long)blockIdx.x * kB + tid;
+  const long long i = a.base + t;                         // position in the ownership order
+  const long long p = t < a.n ? (OWN ? (long long)a.own[i] : i) : -1;
   const int c = p >= 0 ? a.cls_new[p] : -1;
   int rank = 0;
   for (int k = 0; k < a.C; ++k) {
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(kB) void k_group(GroupArgs a) {
 // tables keep their meaning.  Per-particle arithmetic is independent of which rows share a
 // tile, so the results are bitwise those of the undeduplicated path.
 __device__ __forceinline__ int lead_flag(const LeadArgs& a, long long pos) {
-  if (pos >= a.P) return 0;
+  if (pos >= a.npos) return 0;
   const long long p = a.perm[pos];
   // only this rank's slice registered owners, so owner == p also means "p is in the slice"
   const long long f = p / a.Pf;
@@ -206,7 +209,7 @@ __global__ __launch_bounds__(kB) void k_lead_flags(LeadArgs a) {
   __syncthreads();
   int base = 0;
   for (int v = 0; v < w; ++v) base += wc[v];
-  if (pos < a.P) a.lflag_scan[pos] = ((base + excl) << 1) | lf;
+  if (pos < a.npos) a.lflag_scan[pos] = ((base + excl) << 1) | lf;
   if (tid == 0) {
     int t = 0;
     for (int v = 0; v < kB / 64; ++v) t += wc[v];
@@ -246,7 +249,7 @@ __global__ __launch_bounds__(1024) void k_lead_tables(LeadArgs a) {
   if (tid == 1023) total = part[1023];
   __syncthreads();
   if (tid == 0) {
-    auto row = [&](long long x) { return x >= a.P ? total : a.lblock[x / kB] + (a.lflag_scan[x] >> 1); };
+    auto row = [&](long long x) { return x >= a.npos ? total : a.lblock[x / kB] + (a.lflag_scan[x] >> 1); };
     int ts = 0;
     for (int c = 0; c < a.C; ++c) {
       const int b0 = row(a.seg_pos_begin[c]), e0 = row(a.seg_pos_end[c]);
@@ -262,7 +265,7 @@ __global__ __launch_bounds__(1024) void k_lead_tables(LeadArgs a) {
 
 __global__ __launch_bounds__(kB) void k_lead_compact(LeadArgs a) {
   const long long pos = (long long)blockIdx.x * kB + threadIdx.x;
-  if (pos >= a.P) return;
+  if (pos >= a.npos) return;
   const int v = a.lflag_scan[pos];
   if (!(v & 1)) return;
   const long long p = a.perm[pos];
@@ -614,18 +617,18 @@ static inline unsigned nblk(long long n, int b) { return (unsigned)((n + b - 1) 
 
 void launch_switch(const SwitchArgs& a, hipStream_t s) {
   if (a.own)
-    hipLaunchKernelGGL(k_switch<true>, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+    hipLaunchKernelGGL(k_switch<true>, dim3(nblk(a.n > 0 ? a.n : 1, kB)), dim3(kB), 0, s, a);
   else
-    hipLaunchKernelGGL(k_switch<false>, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+    hipLaunchKernelGGL(k_switch<false>, dim3(nblk(a.n > 0 ? a.n : 1, kB)), dim3(kB), 0, s, a);
 }
 void launch_scan_counts(const ScanArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, a);
 }
 void launch_group(const GroupArgs& a, hipStream_t s) {
   if (a.own)
-    hipLaunchKernelGGL(k_group<true>, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+    hipLaunchKernelGGL(k_group<true>, dim3(nblk(a.n > 0 ? a.n : 1, kB)), dim3(kB), 0, s, a);
   else
-    hipLaunchKernelGGL(k_group<false>, dim3(nblk(a.P, kB)), dim3(kB), 0, s, a);
+    hipLaunchKernelGGL(k_group<false>, dim3(nblk(a.n > 0 ? a.n : 1, kB)), dim3(kB), 0, s, a);
 }
 void launch_lead(const LeadArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_lead_flags, dim3((unsigned)a.nb), dim3(kB), 0, s, a);
