@@ -195,7 +195,8 @@ def main():
     T = torch.from_numpy(synthetic.markov_matrix(WORKLOAD["C"]))
     torch.manual_seed(11)
     pf = GPMDM_PF(model, T, P_total, rng="philox", seed=11, process_group=group)
-    zs = data.observation_stream(args.warmup + args.steps, seed=1)
+    n_breakdown = min(args.steps, 10)
+    zs = data.observation_stream(args.warmup + args.steps + n_breakdown, seed=1)
     log(f"[bench] rank {rank}/{world} setup {time.perf_counter() - t_setup:.1f}s, P_total={P_total}")
 
     def one(k):
@@ -223,8 +224,8 @@ def main():
     stages = pf.stage_times()
     # per-stage breakdown from a separate, untimed pass (every stage's events on)
     pf.enable_timing(True)
-    for k in range(min(args.steps, 10)):
-        one(args.warmup + k)
+    for k in range(n_breakdown):            # the stream's next frames (no jump back in time)
+        one(args.warmup + args.steps + k)
     torch.cuda.synchronize()
     pf.enable_timing(False)
     breakdown = pf.stage_times()
