@@ -77,8 +77,11 @@ def ranks_mode():
     ns = [int(x) for x in args[1].split(",")] if len(args) > 1 else [1, 2, 4, 8]
     for n in ns:
         P = per_rank * n
-        pfs = [GPMDM_PF(model, T, P, rng="philox", seed=11, shard=(n, r) if n > 1 else None,
-                        shard_order=order) for r in range(n)]
+        pfs = []
+        for r in range(n):                  # same initial particles on every rank (torch draws)
+            torch.manual_seed(11)
+            pfs.append(GPMDM_PF(model, T, P, rng="philox", seed=11, shard=(n, r) if n > 1 else None,
+                                shard_order=order))
 
         def step(k):
             if n == 1:
