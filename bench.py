@@ -16,10 +16,19 @@ Prints ONE JSON line (rank 0) with the contract fields plus:
                 achieved = algorithmic FLOPs per launch (triangular form N(N+1) + 2N + 2ND
                 per particle; SURVEY §8(d)'s dense 2N^2 + 2ND is reported beside it) / mean
                 launch time from HIP events on the launch stream; traffic = HBM bytes per
-                launch from the committed rocprofv3 PMC summary (profiles/), or null
-  cpu_baseline  the CPU oracle (numpy fp64, BLAS threads stated) on a bounded sample
+                launch of the same kernel from the committed rocprofv3 PMC passes of this
+                bench command (profiles/r02_pmc_summary.json; its "commit" field names the
+                build it measured -- the driver's bench run has no profiler attached), or null
+  cpu_baseline  the CPU oracle (numpy fp64) on this configuration's own particle count
+                for N <= 2000 (a bounded sample of frames), a 1000-particle sample above;
+                cores = BLAS threads it ran on, with nproc and torch's thread count beside
   stages_ms_per_step  per-stage device time from a separate 10-step pass after the timed
                 region (inside it only the roofline kernel records events: 2 per step)
+  nodedup       the same step with ancestor de-duplication off (every particle's dynamics
+                GP evaluated, as the reference does): ms/step, throughput and stages -- the
+                headline's dynamics stage is cheap partly because resampling collapses the
+                cloud onto few ancestors; this line does not depend on that
+  ess_last      effective sample size 1 / sum w^2 of the last timed step's weights
 """
 from __future__ import annotations
 
@@ -91,20 +100,27 @@ def obs_model_bytes(N, D):
     return 8.0 * (N * (N + 1) / 2 + N * D)
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the obs tile kernel from the committed PMC summary."""
-    p = ROOT / "profiles" / "pmc_summary.json"
-    if not p.exists():
-        return None
-    try:
-        j = json.loads(p.read_text())
-        return j.get("obs_gemm_hbm_bytes_per_launch")
-    except Exception:
-        return None
+def pmc_traffic(cfg):
+    """(HBM bytes per launch of the obs tile kernel, source note) from the committed
+    rocprofv3 PMC summary of this bench command (tools/pmc_passes.sh + tools/pmc_summary.py)."""
+    for name in ("r02_pmc_summary.json", "pmc_summary.json"):
+        p = ROOT / "profiles" / name
+        if not p.exists():
+            continue
+        try:
+            j = json.loads(p.read_text())
+        except Exception:
+            continue
+        key = "obs_gemm_hbm_bytes_per_launch" if cfg == 2 else f"config{cfg}_obs_gemm_hbm_bytes_per_launch"
+        if j.get(key) is not None:
+            return j[key], (f"profiles/{name}: rocprofv3 --pmc passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950 "
+                            f"correction) of bench.py --config {cfg} at commit {j.get('commit', 'unrecorded')}")
+    return None, None
 
 
-def cpu_baseline(data, budget_s=12.0):
-    """The numpy oracle on the same workload shape, bounded sample (P_sample particles)."""
+def cpu_baseline(data, budget_s=20.0):
+    """The numpy oracle on the same workload: this configuration's own particle count when
+    N <= 2000 (configs 1, 2, 4: a few frames of P = 100k / 125k), 1000 particles above."""
     from oracle import gpmdm_oracle as O
     from gpmdm_amd import synthetic
     import torch
@@ -113,6 +129,7 @@ def cpu_baseline(data, budget_s=12.0):
         cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
     except Exception:
         cores = os.cpu_count() or 1
+    torch_threads = torch.get_num_threads()
     w = WORKLOAD
     from sklearn.decomposition import PCA
     Y = np.concatenate([y for c in data.sequences for y in c]).astype(np.float64)
@@ -125,7 +142,8 @@ def cpu_baseline(data, budget_s=12.0):
                       x_log_lambdas=np.log(hp["x_lambdas_init"]), x_log_sigma_n=np.log(0.1),
                       x_log_lin_coeff=np.log(hp["x_lin_coeff_init"])).precompute()
     T = synthetic.markov_matrix(w["C"])
-    Ps = 2000 if N <= 2000 else 200
+    Ps = w["P_per_gpu"] if N <= 2000 else 1000
+    Ps -= Ps % w["C"]
     rng = np.random.RandomState(0)
     parts = [rng.randint(0, m.X_for_class(c).shape[0], Ps // w["C"]) for c in range(w["C"])]
     s, c = O.init_particles(m, Ps, parts)
@@ -136,12 +154,14 @@ def cpu_baseline(data, budget_s=12.0):
         s, c = r.states, r.classes
         steps += 1
         el = time.perf_counter() - t0
-        if el > budget_s or steps >= 50:
+        if el > budget_s or steps >= (3 if Ps >= 100_000 else 50):
             break
-    del torch
     return {"value": Ps * steps / el, "unit": "particle-steps/s", "cores": int(cores), "kind": "port",
-            "sample": f"oracle (numpy fp64 restatement) N={N} D={w['D']} d={w['d']} C={w['C']}, P={Ps} particles x {steps} steps "
-                      f"in {el:.1f} s"}
+            "nproc": os.cpu_count(), "torch_threads": int(torch_threads),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "sample": f"oracle (numpy fp64 restatement of gpmdm_pf.py's step, BLAS on {cores} threads) N={N} "
+                      f"D={w['D']} d={w['d']} C={w['C']}, P={Ps} particles x {steps} frames in {el:.1f} s "
+                      f"(model precompute excluded)"}
 
 
 def main():
@@ -196,7 +216,7 @@ def main():
     torch.manual_seed(11)
     pf = GPMDM_PF(model, T, P_total, rng="philox", seed=11, process_group=group)
     n_breakdown = min(args.steps, 10)
-    zs = data.observation_stream(args.warmup + args.steps + n_breakdown, seed=1)
+    zs = data.observation_stream(args.warmup + args.steps + n_breakdown + 64, seed=1)
     log(f"[bench] rank {rank}/{world} setup {time.perf_counter() - t_setup:.1f}s, P_total={P_total}")
 
     def one(k):
@@ -235,6 +255,37 @@ def main():
         elapsed = float(t.item())
     post = pf.class_probabilities().numpy()
     dyn_rows = pf.dynamics_rows()
+    w_last = pf.export_state()["w"]
+    ess = float(1.0 / np.sum(w_last * w_last))
+    # the same step without ancestor de-duplication (every particle's dynamics GP evaluated)
+    n_nd = min(args.steps, 20)
+    pf_nd = GPMDM_PF(model, T, P_total, rng="philox", seed=11, process_group=group, dedup=False)
+    for k in range(3):
+        pf_nd.update(zs[k])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t_nd = time.perf_counter()
+    for k in range(n_nd):
+        pf_nd.update(zs[3 + k])
+        pf_nd.get_most_likely_class()
+        pf_nd.class_probabilities()
+        pf_nd.current_state_mean()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el_nd = time.perf_counter() - t_nd
+    if dist is not None:
+        t = torch.tensor([el_nd], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_nd = float(t.item())
+    pf_nd.enable_timing(True)
+    for k in range(min(n_nd, 10)):
+        pf_nd.update(zs[3 + n_nd + k])
+    torch.cuda.synchronize()
+    pf_nd.enable_timing(False)
+    nd_stages = pf_nd.stage_times()
+    del pf_nd
 
     N, D, d = model.X.shape[0], model.D, model.d
     P_local = P_total // world
@@ -242,7 +293,7 @@ def main():
     obs_ms, obs_n = stages["obs_gemm"]
     obs_launch_s = obs_ms / max(obs_n, 1) / 1e3
     achieved = alg * P_local / obs_launch_s / 1e12
-    traffic = pmc_traffic() if WORKLOAD["cfg"] == 2 else None
+    traffic, traffic_src = pmc_traffic(WORKLOAD["cfg"])
     b_image = obs_model_bytes(N, D)
     rec = {
         "metric": METRIC,
@@ -266,11 +317,11 @@ def main():
                      "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
                      "traffic": traffic,
                      "traffic_GBps": traffic / obs_launch_s / 1e9 if traffic else None,
-                     "traffic_note": ("HBM/MALL bytes per launch from the committed rocprofv3 PMC passes "
-                                      "(profiles/pmc_summary.json); the algorithmic bytes are triu(R) and K^-1 Y "
+                     "traffic_source": traffic_src,
+                     "traffic_note": ("HBM/MALL bytes per launch; the algorithmic bytes are triu(R) and K^-1 Y "
                                       f"({b_image / 1e6:.1f} MB) plus the particles; each XCD re-streams B panels "
-                                      "once per round of concurrently resident tiles (L2 hit 97%), which costs "
-                                      "nothing measurable: the kernel is FP64-MFMA bound at a few % of HBM "
+                                      "once per round of concurrently resident tiles, which costs nothing "
+                                      "measurable: the kernel is FP64-MFMA bound at a few % of HBM "
                                       "bandwidth (DESIGN.md §3)") if traffic else None,
                      "kernel": f"k_gp_tile<{d},false> (observation GP)",
                      "flops_per_particle_algorithmic": alg, "flops_per_particle_executed": executed,
@@ -279,6 +330,12 @@ def main():
                      "dense_form_equivalent_tflops": dense * P_local / obs_launch_s / 1e12,
                      "launch_ms": obs_launch_s * 1e3},
         "stages_ms_per_step": {k: v[0] / max(v[1], 1) for k, v in breakdown.items()},
+        "nodedup": {"ms_per_step": el_nd / n_nd * 1e3, "value": P_total * n_nd / el_nd, "steps": n_nd,
+                    "stages_ms_per_step": {k: v[0] / max(v[1], 1) for k, v in nd_stages.items()},
+                    "note": "dedup=False: the dynamics GP runs on every particle (the reference's work); "
+                            "bitwise the same filter as the headline's"},
+        "ess_last": ess,
+        "ess_frac_last": ess / P_total,
         "posterior_last": [float(x) for x in post],
         "dyn_rows_last": {"evaluated": dyn_rows, "particles": P_local,
                           "note": "dynamics GP rows of the last step: one per distinct (ancestor, class) "

@@ -13,11 +13,17 @@ from pathlib import Path
 
 LIB_PATH = Path(__file__).resolve().parent / "libgpmdm_hip.so"
 
+GPMDM_OK = 0
+GPMDM_E_INVALID = -1
+GPMDM_E_HIP = -2
+GPMDM_E_NOMEM = -3
+GPMDM_E_STATE = -4
 GPMDM_RNG_REPLAY = 0
 GPMDM_RNG_PHILOX = 1
 GPMDM_RESAMPLE_MULTINOMIAL = 0
 GPMDM_RESAMPLE_SYSTEMATIC = 1
 STAGES = ("switch", "dyn_gemm", "dyn_finish", "obs_gemm", "obs_finish", "resample")
+HEALTH = ("obs_var_nonpositive", "obs_ll_nonfinite", "dyn_var_nonpositive", "dyn_state_nonfinite")
 
 _dp = POINTER(c_double)
 _i64p = POINTER(c_int64)
@@ -59,6 +65,10 @@ _SIGS = {
     "gpmdm_pf_set_shard_order": (c_int, [c_void_p, c_int]),
     "gpmdm_pf_timing_stages": (c_int, [c_void_p, ctypes.c_uint]),
     "gpmdm_pf_dyn_rows": (c_int, [c_void_p, _i64p, c_void_p]),
+    "gpmdm_pf_frame": (c_int, [c_void_p, _i64p]),
+    "gpmdm_pf_set_model": (c_int, [c_void_p, c_void_p]),
+    "gpmdm_pf_health": (c_int, [c_void_p, _i64p, c_int, c_void_p]),
+    "gpmdm_pf_predict": (c_int, [c_void_p, _dp, c_void_p]),
     "gpmdm_gp_factor": (c_int, [c_int, _dp, c_int64, c_int32, _dp, _dp, c_double, c_double, c_double,
                                 _dp, c_int64, _dp, _dp]),
     "gpmdm_spd_inverse": (c_int, [c_int, c_void_p, c_int64, _dp, c_void_p]),

@@ -45,17 +45,22 @@ class GPMDM_PF_Bank:
         self._num_particles = int(num_particles)
         if self._num_filters < 1 or self._num_particles < 1:
             raise ValueError("num_filters and num_particles must be positive")
-        if seed is None:
-            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        self._seed = int(seed)
         self._group = process_group
         if process_group is not None:
             import torch.distributed as dist
             world, rank = dist.get_world_size(process_group), dist.get_rank(process_group)
         elif shard is not None:                   # (world, rank) without a process group
             world, rank = int(shard[0]), int(shard[1])
+            if world > 1 and seed is None:
+                raise ValueError("shard= needs an explicit seed (identical on every rank)")
         else:
             world, rank = 1, 0
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        if process_group is not None and world > 1:   # one seed for the whole bank: rank 0's
+            from .distributed import broadcast_array
+            seed = int(broadcast_array(np.array([seed], dtype=np.int64), process_group, self.device)[0])
+        self._seed = int(seed)
         self._world, self._rank = world, rank
         self._f_lo, self._f_hi = shard_range(self._num_filters, world, rank)
         self._h = None
@@ -69,6 +74,7 @@ class GPMDM_PF_Bank:
                 _lib.GPMDM_RESAMPLE_MULTINOMIAL if resample == "multinomial" else _lib.GPMDM_RESAMPLE_SYSTEMATIC,
                 ctypes.byref(h)), "GPMDM_PF_Bank")
             self._h = h
+            self._model_gen = gpmdm.generation
             _lib.check(_lib.load().gpmdm_pf_set_dedup(h, 1 if dedup else 0), "dedup")
             self._init_particles()
 
@@ -82,6 +88,12 @@ class GPMDM_PF_Bank:
 
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _sync_model(self):
+        """Rebind to the GPMDM's current device image (see GPMDM_PF._sync_model)."""
+        if self._h is not None and self._gpmdm.generation != self._model_gen:
+            _lib.check(_lib.load().gpmdm_pf_set_model(self._h, self._gpmdm.handle), "rebind to the rebuilt model")
+            self._model_gen = self._gpmdm.generation
 
     # ---- state ----------------------------------------------------------------------
     def _init_particles(self):
@@ -109,6 +121,7 @@ class GPMDM_PF_Bank:
         Fl, P, d = self.local_filters, self._num_particles, self.latent_dim
         states = np.ascontiguousarray(states, dtype=np.float64).reshape(Fl * P, d)
         classes = np.ascontiguousarray(classes, dtype=np.int64).reshape(Fl * P)
+        self._sync_model()
         _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "load_state")
         self._readout = None
 
@@ -141,6 +154,7 @@ class GPMDM_PF_Bank:
         if self._h is None:
             return
         Z = np.ascontiguousarray(Z)
+        self._sync_model()
         lib, h, s = _lib.load(), self._h, self._stream()
         _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
         _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(Z), None, s), "propagate")
@@ -174,6 +188,14 @@ class GPMDM_PF_Bank:
         """(F_local,): gpmdm_pf.py:215-222 per filter (a sum of exponentials, as there)."""
         return torch.tensor(self._read()[2], dtype=torch.float64)
 
+    def predict(self) -> torch.Tensor:
+        """(F_local, d): GPMDM_PF.predict per filter (gpmdm_pf_predict)."""
+        out = np.zeros((self.local_filters, self.latent_dim))
+        if self._h is not None:
+            self._sync_model()
+            _lib.check(_lib.load().gpmdm_pf_predict(self._h, _lib.dptr(out), self._stream()), "predict")
+        return torch.from_numpy(out)
+
     def gather_readouts(self) -> dict:
         """All filters' read-outs on every rank (one all-gather of F x (C + d + 1))."""
         post, mean, lik = self._read()
@@ -194,6 +216,14 @@ class GPMDM_PF_Bank:
                     log_likelihood=torch.tensor(full[:, C + d]))
 
     # ---- properties -----------------------------------------------------------------
+    @property
+    def frame(self) -> int:
+        """Resamples done so far (every filter of the bank steps together)."""
+        f = np.zeros(1, dtype=np.int64)
+        if self._h is not None:
+            _lib.check(_lib.load().gpmdm_pf_frame(self._h, _lib.i64ptr(f)), "frame")
+        return int(f[0])
+
     @property
     def num_filters(self):
         return self._num_filters

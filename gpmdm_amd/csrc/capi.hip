@@ -1,6 +1,7 @@
 // C ABI of libgpmdm_hip.so (include/gpmdm_hip.h): model and particle-filter handles,
 // device memory layout, and the per-frame launch sequence.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -161,6 +162,10 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
 
 // =====================================================================================
 struct gpmdm_model {
+  // Reference count: the caller's handle plus one per filter built on the model, so a
+  // filter keeps the device image it was built on alive until it is destroyed or rebound
+  // (gpmdm_pf_set_model) even after the caller rebuilt the model (GPMDM.set_latents).
+  std::atomic<int> refs{1};
   int device = 0;
   long long N = 0;
   int D = 0, d = 0, C = 0;
@@ -192,6 +197,10 @@ struct gpmdm_model {
     return GPMDM_OK;
   }
 };
+
+static void model_release(gpmdm_model* m) {
+  if (m && m->refs.fetch_sub(1) == 1) delete m;
+}
 
 struct gpmdm_pf {
   gpmdm_model* m = nullptr;
@@ -226,6 +235,11 @@ struct gpmdm_pf {
   int zslot = 0;
   double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *sobs = nullptr;
   int nparts_dyn_max = 0;
+  // failure detection: kHealth* counters, device, zeroed at create
+  unsigned* health = nullptr;
+  // predict(): per-particle dynamics-GP means, lazily allocated
+  double *pred_q = nullptr, *pred_mu = nullptr, *pred_mu_p = nullptr, *pred_out = nullptr;
+  size_t pred_q_cap = 0;
   double *z = nullptr, *E = nullptr, *normals = nullptr, *U = nullptr;
   unsigned long long* gmax = nullptr;
   double *e = nullptr, *local = nullptr, *blocksum = nullptr, *blockoffw = nullptr, *total = nullptr,
@@ -251,7 +265,8 @@ struct gpmdm_pf {
 
   ~gpmdm_pf() {
     double* ds[] = {T, X, X_prop, ll, qdyn, mudyn, qobs, sobs, z, E, normals, U,
-                    e, local, blocksum, blockoffw, total, cum, partials, readout};
+                    e, local, blocksum, blockoffw, total, cum, partials, readout,
+                    pred_q, pred_mu, pred_mu_p, pred_out};
     for (double* p : ds) dfree(p);
     int* is[] = {cls, cls_new, perm, ridx, blockcounts, blockoff, small, obs_tab,
                  slot, lflag, lblock, ltab, lperm, guide, own};
@@ -259,6 +274,7 @@ struct gpmdm_pf {
     dfree(own_tmp);
     dfree(gmax);
     dfree(owner);
+    dfree(health);
     for (auto& r : recs) { pool.push_back(r.a); pool.push_back(r.b); }
     for (auto ev : pool) (void)hipEventDestroy(ev);
     if (rpin) (void)hipHostFree(rpin);
@@ -266,6 +282,7 @@ struct gpmdm_pf {
       if (zpin[k]) (void)hipHostFree(zpin[k]);
       if (zev[k]) (void)hipEventDestroy(zev[k]);
     }
+    model_release(m);
   }
 
   hipEvent_t ev() {
@@ -376,7 +393,7 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
 }
 
 int gpmdm_model_destroy(gpmdm_model_t m) {
-  delete m;
+  model_release(m);   // freed once the last filter built on it is gone
   return GPMDM_OK;
 }
 
@@ -494,6 +511,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   HIPCHK(hipSetDevice(m->device));
   auto* pf = new gpmdm_pf();
   pf->m = m;
+  m->refs.fetch_add(1);   // released by ~gpmdm_pf
   pf->P = P;
   pf->Pf = Pf;
   pf->F = (int)F;
@@ -553,6 +571,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   ALLOC(guide, guide_buckets_used(Pf) > 0 ? F * (guide_buckets(Pf) + 3) : 1);
   ALLOC(partials, F * pf->nbf * (C + 1 + d));
   ALLOC(readout, F * (C + d + 1));
+  ALLOC(health, kHealthN);
   if (n_ranks > 1 && rng_mode == GPMDM_RNG_PHILOX) {
     pf->own_tmp_bytes = std::max<size_t>(ancestor_order_temp_bytes(P), 1);
     ALLOC(own, P);
@@ -572,7 +591,8 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   }
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, m->obs.tiles(pf->nloc)};
   if (hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(pf->T, T, sizeof(double) * C * C, hipMemcpyHostToDevice) != hipSuccess) {
+      hipMemcpy(pf->T, T, sizeof(double) * C * C, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(pf->health, 0, sizeof(unsigned) * kHealthN) != hipSuccess) {
     delete pf;
     return fail(GPMDM_E_HIP, "upload of particle-filter tables failed");
   }
@@ -876,6 +896,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
       fa.anc = pf->ridx;
       fa.P = pf->P;
     }
+    fa.health = pf->health;
     launch_dyn_finish(fa, s);
     pf->mark_end(s, GPMDM_STAGE_DYN_FINISH, t0);
 
@@ -920,6 +941,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     oa.ll = pf->ll;
     oa.ll_offset = pf->lo;
     oa.own = pf->own_order();
+    oa.health = pf->health;
     launch_obs_finish(oa, s);
     pf->mark_end(s, GPMDM_STAGE_OBS_FINISH, t0);
   }
@@ -1127,6 +1149,150 @@ int gpmdm_pf_stage_times(gpmdm_pf_t pf, double* ms, int64_t* launches) {
   pf->recs.clear();
   if (ms) std::memcpy(ms, acc, sizeof(acc));
   if (launches) std::memcpy(launches, n, sizeof(n));
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_frame(gpmdm_pf_t pf, int64_t* frame) {
+  CHECK(pf && frame, "null argument");
+  *frame = pf->frame;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
+  CHECK(pf && m, "null argument");
+  if (pf->switched || pf->propagated) return fail(GPMDM_E_STATE, "set_model inside a step");
+  gpmdm_model* old = pf->m;
+  if (m == old) return GPMDM_OK;
+  CHECK(m->C == old->C && m->d == old->d && m->D == old->D,
+        "the new model's (C, d, D) differ from the filter's");
+  CHECK(m->device == old->device, "the new model lives on another device");
+  HIPCHK(hipSetDevice(m->device));
+  // buffers shaped by the model's column blocks
+  int maxparts = 0;
+  for (auto& g : m->dyn) maxparts = std::max(maxparts, g.n_parts());
+  const long long nl = std::max(pf->nloc, 1ll);
+  double *qdyn = nullptr, *qobs = nullptr, *sobs = nullptr;
+  int rc = dalloc(&qdyn, (size_t)maxparts * nl);
+  if (!rc) rc = dalloc(&qobs, (size_t)m->obs.n_parts() * nl);
+  if (!rc) rc = dalloc(&sobs, (size_t)m->obs.n_j * nl);
+  const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, m->obs.tiles(pf->nloc)};
+  if (!rc && hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess)
+    rc = fail(GPMDM_E_HIP, "upload of the observation tile table");
+  if (rc) {
+    dfree(qdyn);
+    dfree(qobs);
+    dfree(sobs);
+    return rc;
+  }
+  HIPCHK(hipDeviceSynchronize());    // launches in flight may still read the old buffers
+  dfree(pf->qdyn);
+  dfree(pf->qobs);
+  dfree(pf->sobs);
+  dfree(pf->pred_q);
+  pf->pred_q_cap = 0;
+  pf->qdyn = qdyn;
+  pf->qobs = qobs;
+  pf->sobs = sobs;
+  pf->nparts_dyn_max = maxparts;
+  m->refs.fetch_add(1);
+  pf->m = m;
+  model_release(old);
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_health(gpmdm_pf_t pf, int64_t* counts, int reset, void* stream) {
+  CHECK(pf, "null handle");
+  HIPCHK(hipSetDevice(pf->m->device));
+  hipStream_t s = (hipStream_t)stream;
+  unsigned h[kHealthN];
+  HIPCHK(hipMemcpyAsync(h, pf->health, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (counts)
+    for (int k = 0; k < kHealthN; ++k) counts[k] = h[k];
+  if (reset) HIPCHK(hipMemsetAsync(pf->health, 0, sizeof(h), s));
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_predict(gpmdm_pf_t pf, double* mean, void* stream) {
+  CHECK(pf && mean, "null argument");
+  if (!pf->initialised) return fail(GPMDM_E_STATE, "particle filter not initialised");
+  if (pf->switched || pf->propagated) return fail(GPMDM_E_STATE, "predict inside a step");
+  gpmdm_model* m = pf->m;
+  HIPCHK(hipSetDevice(m->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int C = m->C, d = m->d;
+  const long long P = pf->P;
+  const size_t qn = (size_t)pf->nparts_dyn_max * P;
+  if (pf->pred_q_cap < qn) {
+    dfree(pf->pred_q);
+    TRY(dalloc(&pf->pred_q, qn));
+    pf->pred_q_cap = qn;
+  }
+  if (!pf->pred_mu) {
+    TRY(dalloc(&pf->pred_mu, (size_t)P * d));
+    TRY(dalloc(&pf->pred_mu_p, (size_t)P * d));
+    TRY(dalloc(&pf->pred_out, (size_t)pf->F * d));
+  }
+  // group the current particles by their current class (the grouping tables are the
+  // switch's; the next switch rebuilds them)
+  const int nbs = (int)cdiv(P, 256);
+  launch_class_hist(pf->cls, P, C, pf->blockcounts, s);
+  ScanArgs sc{};
+  sc.nb = nbs;
+  sc.C = C;
+  sc.pt = m->dyn[0].geo.pt();
+  sc.lo = 0;
+  sc.hi = P;
+  sc.blockcounts = pf->blockcounts;
+  sc.cls_new = pf->cls;
+  sc.blockoff = pf->blockoff;
+  sc.class_start = pf->class_start();
+  sc.counts = pf->counts();
+  sc.seg_pos_begin = pf->seg_begin();
+  sc.seg_pos_end = pf->seg_end();
+  sc.seg_out_base = pf->seg_out();
+  sc.seg_tile_start = pf->seg_tiles();
+  launch_scan_counts(sc, s);
+  GroupArgs ga{};
+  ga.P = P;
+  ga.n = P;
+  ga.C = C;
+  ga.cls_new = pf->cls;
+  ga.class_start = pf->class_start();
+  ga.blockoff = pf->blockoff;
+  ga.perm = pf->perm;
+  launch_group(ga, s);
+  // each class's dynamics-GP mean (gpmdm.py:1032-1068), rows in grouped order
+  for (int c0 = 0; c0 < C; c0 += kMaxSeg) {
+    const int ns = std::min(kMaxSeg, C - c0);
+    TileParams tp{};
+    int njm = 0;
+    for (int k = 0; k < ns; ++k) {
+      tp.seg[k] = m->dyn[c0 + k].seg();
+      njm = std::max(njm, m->dyn[c0 + k].n_j);
+    }
+    tp.n_seg = ns;
+    tp.geo = m->dyn[c0].geo;
+    tp.tiles_ub = (int)(cdiv(P, tp.geo.pt()) + ns);
+    tp.n_j_max = njm;
+    tp.seg_pos_begin = pf->seg_begin() + c0;
+    tp.seg_pos_end = pf->seg_end() + c0;
+    tp.seg_out_base = pf->seg_out() + c0;
+    tp.seg_tile_start = pf->seg_tiles() + c0;
+    tp.perm = pf->perm;
+    tp.X = pf->X;
+    fill_tile_common(tp, m, true);
+    tp.qpart = pf->pred_q;
+    tp.ld_q = P;
+    tp.mu = pf->pred_mu;
+    tp.ld_mu = d;
+    launch_gp_tile(tp, d, true, s);
+  }
+  launch_predict_mean(pf->perm, pf->pred_mu, pf->pred_mu_p, pf->pred_out, P, pf->Pf, pf->F, d, s);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(pf->rpin, pf->pred_out, sizeof(double) * pf->F * d, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::memcpy(mean, pf->rpin, sizeof(double) * pf->F * d);
   return GPMDM_OK;
 }
 

@@ -8,6 +8,17 @@ namespace gpmdm {
 constexpr int kMaxClasses = 32;
 constexpr int kMaxReadout = kMaxClasses + 1 + kMaxD;
 
+// Failure-detection counters (gpmdm_pf_health).  The filter keeps the
+// reference's arithmetic -- a non-positive variance gives NaN log-likelihoods or states,
+// as gpmdm_pf.py:167-168, 188-192 do -- and counts each event, per particle and step.
+enum HealthCounter : int {
+  kHealthObsVar = 0,      // observation-GP vc = 1 - k^T K_y^-1 k <= 0 (or NaN)
+  kHealthObsLL = 1,       // non-finite log-likelihood
+  kHealthDynVar = 2,      // dynamics-GP vc <= 0 (or NaN)
+  kHealthDynState = 3,    // non-finite propagated state
+  kHealthN = 4
+};
+
 // Filter banks: F independent filters of Pf particles each, stored filter-major
 // (particle g = f * Pf + p).  The Philox key of filter f is seed + f and the counters use
 // the in-filter index p, so filter f of a bank draws exactly what a single filter seeded
@@ -114,6 +125,7 @@ struct DynFinishArgs {
   const int* slot;                // nullptr: row = output index o
   const int* anc;
   long long P;
+  unsigned* health;               // kHealth* counters (PF) or nullptr
 };
 
 struct ObsFinishArgs {
@@ -135,6 +147,7 @@ struct ObsFinishArgs {
   const double* spart;            // [J][ld_q] for J in [jm0, n_j), or nullptr
   int jm0, n_j;
   double sum_log_il2;             // sum_j log il2_j
+  unsigned* health;               // kHealth* counters (PF) or nullptr
 };
 
 // Normalisation and resampling run per filter: grid (nb, F), nb blocks of 256 per filter.
@@ -206,6 +219,12 @@ void launch_obs_finish(const ObsFinishArgs& a, hipStream_t s);
 void launch_normalise(const NormArgs& a, hipStream_t s);
 void launch_resample(const ResampleArgs& a, hipStream_t s);
 void launch_pack(const PackArgs& a, hipStream_t s);
+// predict(): per-block class histogram of `cls` (blockcounts nb x C, nb = ceil(P / 256))
+void launch_class_hist(const int* cls, long long P, int C, int* blockcounts, hipStream_t s);
+// predict(): rows of mu (grouped order, perm: row -> particle) scattered to particle order,
+// then per filter the mean over its Pf particles (fixed-order reduction) into out (F x d)
+void launch_predict_mean(const int* perm, const double* mu, double* mu_p, double* out, long long P,
+                         long long Pf, int F, int d, hipStream_t s);
 void launch_unpack(const PackArgs& a, hipStream_t s);
 
 }  // namespace gpmdm

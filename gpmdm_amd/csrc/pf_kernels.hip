@@ -276,6 +276,14 @@ __global__ __launch_bounds__(kB) void k_lead_compact(LeadArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
+// Failure counters: one atomic per wave for the lanes that saw the event (events are rare;
+// a collapsed or indefinite model can make every particle bad, hence the ballot).
+__device__ __forceinline__ void count_event(unsigned* ctr, bool bad) {
+  const unsigned long long b = __ballot(bad);
+  if (b && (int)(threadIdx.x & 63) == __ffsll((long long)b) - 1) atomicAdd(ctr, (unsigned)__popcll(b));
+}
+
+// ---------------------------------------------------------------------------------
 // out index o -> class segment
 __device__ __forceinline__ int seg_of(const int* seg_out_base, int n_seg, int total, int o) {
   int c = 0;
@@ -309,6 +317,7 @@ __global__ __launch_bounds__(kB) void k_dyn_finish(DynFinishArgs a) {
     for (int j = 0; j < d; ++j) a.var_out[o * d + j] = vc * a.il2[j];
     return;
   }
+  bool bad_state = false;
   // torch.normal(mean, std) = eps * std + mean (gpmdm_pf.py:167-168)
   for (int j = 0; j < d; j += 2) {
     double e0, e1 = 0.0;
@@ -326,8 +335,18 @@ __global__ __launch_bounds__(kB) void k_dyn_finish(DynFinishArgs a) {
       e0 = rr * cs;
       e1 = rr * sn;
     }
-    a.X_out[p * d + j] = e0 * sqrt(vc * a.il2[j]) + a.mu[r * a.ld_mu + j];
-    if (j + 1 < d) a.X_out[p * d + j + 1] = e1 * sqrt(vc * a.il2[j + 1]) + a.mu[r * a.ld_mu + j + 1];
+    const double x0 = e0 * sqrt(vc * a.il2[j]) + a.mu[r * a.ld_mu + j];
+    a.X_out[p * d + j] = x0;
+    bad_state |= !isfinite(x0);
+    if (j + 1 < d) {
+      const double x1 = e1 * sqrt(vc * a.il2[j + 1]) + a.mu[r * a.ld_mu + j + 1];
+      a.X_out[p * d + j + 1] = x1;
+      bad_state |= !isfinite(x1);
+    }
+  }
+  if (a.health) {
+    count_event(a.health + kHealthDynVar, !(vc > 0.0));
+    count_event(a.health + kHealthDynState, bad_state);
   }
 }
 
@@ -376,7 +395,12 @@ __global__ __launch_bounds__(kB) void k_obs_ll(ObsFinishArgs a) {
   double S = 0.0;
   for (int k = a.jm0; k < a.n_j; ++k) S += a.spart[(long long)k * a.ld_q + o];
   const double vc = 1.0 - q;                           // k(x*,x*) = 1 (gpmdm.py:991)
-  a.ll[a.own ? a.own[a.ll_offset + o] : a.ll_offset + o] = -0.5 * S / vc - a.D * log(vc) - a.sum_log_il2 - a.ll_const;
+  const double llv = -0.5 * S / vc - a.D * log(vc) - a.sum_log_il2 - a.ll_const;
+  a.ll[a.own ? a.own[a.ll_offset + o] : a.ll_offset + o] = llv;
+  if (a.health) {
+    count_event(a.health + kHealthObsVar, !(vc > 0.0));
+    count_event(a.health + kHealthObsLL, !isfinite(llv));
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -613,7 +637,58 @@ __global__ __launch_bounds__(kB) void k_unpack(PackArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
+// predict(): class histogram of the current classes (k_switch's histogram without a switch)
+__global__ __launch_bounds__(kB) void k_class_hist(const int* cls, long long P, int C, int* blockcounts) {
+  __shared__ int hist[kMaxClasses];
+  const int tid = threadIdx.x;
+  if (tid < C) hist[tid] = 0;
+  __syncthreads();
+  const long long p = (long long)blockIdx.x * kB + tid;
+  if (p < P) atomicAdd(&hist[cls[p]], 1);
+  __syncthreads();
+  if (tid < C) blockcounts[(long long)blockIdx.x * C + tid] = hist[tid];
+}
+
+__global__ __launch_bounds__(kB) void k_predict_scatter(const int* perm, const double* mu, double* mu_p,
+                                                        long long P, int d) {
+  const long long o = (long long)blockIdx.x * kB + threadIdx.x;
+  if (o >= P) return;
+  const long long p = perm[o];
+  for (int j = 0; j < d; ++j) mu_p[p * d + j] = mu[o * d + j];
+}
+
+// One workgroup per filter: mean over the filter's particles, thread-strided partial sums
+// combined in a fixed order.
+__global__ __launch_bounds__(kB) void k_predict_mean(const double* mu_p, double* out, long long Pf, int d) {
+  __shared__ double red[kB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long f = blockIdx.x;
+  for (int j = 0; j < d; ++j) {
+    double s = 0.0;
+    for (long long p = tid; p < Pf; p += kB) s += mu_p[(f * Pf + p) * d + j];
+    s = wave_sum(s);
+    if (lane == 0) red[w] = s;
+    __syncthreads();
+    if (tid == 0) {
+      double t = 0.0;
+      for (int v = 0; v < kB / 64; ++v) t += red[v];
+      out[f * d + j] = t / (double)Pf;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------
 static inline unsigned nblk(long long n, int b) { return (unsigned)((n + b - 1) / b); }
+
+void launch_class_hist(const int* cls, long long P, int C, int* blockcounts, hipStream_t s) {
+  hipLaunchKernelGGL(k_class_hist, dim3(nblk(P, kB)), dim3(kB), 0, s, cls, P, C, blockcounts);
+}
+void launch_predict_mean(const int* perm, const double* mu, double* mu_p, double* out, long long P,
+                         long long Pf, int F, int d, hipStream_t s) {
+  hipLaunchKernelGGL(k_predict_scatter, dim3(nblk(P, kB)), dim3(kB), 0, s, perm, mu, mu_p, P, d);
+  hipLaunchKernelGGL(k_predict_mean, dim3((unsigned)F), dim3(kB), 0, s, mu_p, out, Pf, d);
+}
 
 void launch_switch(const SwitchArgs& a, hipStream_t s) {
   if (a.own)

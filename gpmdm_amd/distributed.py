@@ -9,7 +9,36 @@ torch's current stream, the same stream the library launches on.
 """
 from __future__ import annotations
 
+import hashlib
+
+import numpy as np
 import torch
+
+
+def _comm_device(group, device):
+    """Tensors of a collective live on the GPU for nccl (RCCL), on the host for gloo."""
+    import torch.distributed as dist
+    return device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+
+
+def broadcast_array(a: np.ndarray, group=None, device=None) -> np.ndarray:
+    """Rank 0's copy of ``a`` (same shape and dtype on every rank) on every rank."""
+    import torch.distributed as dist
+    t = torch.from_numpy(np.ascontiguousarray(a).copy()).to(_comm_device(group, device))
+    dist.broadcast(t, src=dist.get_global_rank(group or dist.group.WORLD, 0), group=group)
+    return t.cpu().numpy()
+
+
+def identical_on_all_ranks(blob: bytes, group=None, device=None) -> bool:
+    """True when every rank passed the same bytes (64-bit digest, min == max over ranks)."""
+    import torch.distributed as dist
+    h = int.from_bytes(hashlib.blake2b(blob, digest_size=8).digest(), "little", signed=True)
+    dev = _comm_device(group, device)
+    lo = torch.tensor([h], dtype=torch.int64, device=dev)
+    hi = lo.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    return int(lo.item()) == int(hi.item())
 
 
 def shard_range(P: int, world: int, rank: int):

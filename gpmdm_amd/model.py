@@ -3,8 +3,11 @@
 Mirrors ``/root/reference/gpmdm/gpmdm.py`` (class GPMDM, lines 18-1414) for construction,
 data registry, latent initialisation, kernel-inverse precompute, persistence and the two
 predictive maps; the predictive maps and everything per frame run in libgpmdm_hip.so.
-Training (``train_adam`` / ``gpdm_loss``, gpmdm.py:550-885) is out of scope:
-hyperparameters are passed in, or loaded from a saved model.
+Training (``gpdm_loss`` / ``train_adam``, gpmdm.py:550-885) runs
+on the model's GPU in ``gpmdm_amd/training.py`` and re-uploads the device model when it
+finishes; ``set_training_mode`` (gpmdm.py:247-279) selects which parameters the loss
+functions treat as trainable (``_trainable``), and the ``flg_train_*`` constructor flags
+are recorded there as the reference records them in ``flg_trainable_list``.
 
 Precompute follows the reference recipe (gpmdm.py:1284-1305) on class blocks only:
 ``U = chol(K, upper)``, ``R = U^-1``, ``K^-1 = R R^T``.  The library keeps ``R`` (upper
@@ -83,8 +86,10 @@ class GPMDM:
 
     Constructor arguments are those of the reference (gpmdm.py:96-109).  ``dtype`` must be
     float64 (the reference default, required for parity: SURVEY.md §8(c)).  ``device`` is
-    the GPU the model lives on (default ``cuda:0``); ``flg_train_*`` are accepted and
-    ignored (no training here).
+    the GPU the model lives on (default: the current HIP device, as torch's ``"cuda"``
+    resolves it); ``flg_train_*`` record which parameters training updates (gpmdm.py:
+    96-107, 239-279; ``train_adam`` itself trains every parameter, as the reference's
+    does after ``set_training_mode('all')``).
     """
 
     def __init__(self, D, d, n_classes, dyn_target, dyn_back_step,
@@ -100,9 +105,12 @@ class GPMDM:
         if dyn_target not in ("full", "delta") or dyn_back_step not in (1, 2):
             raise ValueError("target must be either 'full' or 'delta' \n back_step must be either 1 or 2")
         self.dtype = dtype
-        self.device = torch.device("cuda", 0) if device is None else torch.device(device)
-        if self.device.type != "cuda":
+        dev = torch.device("cuda") if device is None else torch.device(device)
+        if dev.type != "cuda":
             raise ValueError("gpmdm_amd runs on the GPU: device must be a cuda (HIP) device")
+        if dev.index is None:   # "cuda": the current device (torch.cuda.set_device), as torch resolves it
+            dev = torch.device("cuda", torch.cuda.current_device() if torch.cuda.is_available() else 0)
+        self.device = dev
         self.D, self.d, self.n_classes = int(D), int(d), int(n_classes)
         self.dyn_target, self.dyn_back_step = dyn_target, int(dyn_back_step)
         f64 = dict(dtype=torch.float64)
@@ -126,6 +134,12 @@ class GPMDM:
         # 2 64x512, 3 32x512); env override for A/B runs
         self.tile_shape = int(os.environ.get("GPMDM_TILE_SHAPE", "0"))
         self._trainable = {}        # set_training_mode (gpmdm.py:247-279); empty = all
+        flags = dict(y_lambdas=flg_train_y_lambdas, y_lengthscales=flg_train_y_lengthscales,
+                     y_sigma_n=flg_train_y_sigma_n, x_lambdas=flg_train_x_lambdas,
+                     x_lengthscales=flg_train_x_lengthscales, x_sigma_n=flg_train_x_sigma_n,
+                     x_lin_coeff=flg_train_x_lin_coeff)
+        self.flg_trainable_list = [k for k, v in flags.items() if v]
+        self.generation = 0         # bumped by every device upload (filters rebind to it)
 
     # ---- reference API: data registry (gpmdm.py:239-309) -------------------------
     def set_evaluation_mode(self):
@@ -305,7 +319,7 @@ class GPMDM:
         """The same factors through gpmdm_gp_factor (device Gram matrix, rocSOLVER potrf +
         trtri, rocBLAS trmm), one GP block at a time."""
         lib = _lib.load()
-        dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        dev_index = self.device.index
 
         def factor(X, log_ls, lin_c2, a, b, c, B, what):
             X = np.ascontiguousarray(X, dtype=np.float64)
@@ -371,9 +385,10 @@ class GPMDM:
         desc.x_inv_lambda2 = arr((torch.exp(self.x_log_lambdas) ** -2).numpy())
         handle = ctypes.c_void_p()
         self._release()
-        _lib.check(lib.gpmdm_model_create(ctypes.byref(desc), self.device.index or 0, ctypes.byref(handle)),
+        _lib.check(lib.gpmdm_model_create(ctypes.byref(desc), self.device.index, ctypes.byref(handle)),
                    "gpmdm_model_create")
         self._handle = handle
+        self.generation += 1
 
     def _release(self):
         if getattr(self, "_handle", None) is not None and self._handle.value:

@@ -10,7 +10,13 @@ every per-frame computation runs in the HIP library.  Extra keyword options:
 * ``seed``: Philox key (default: drawn from torch's generator);
 * ``resample='multinomial'`` (reference, gpmdm_pf.py:211) or ``'systematic'``;
 * ``process_group``: a ``torch.distributed`` group to shard particles over (one process
-  per GPU; one all-gather of the packed particle rows per frame);
+  per GPU; one all-gather of the packed particle rows per frame).  The Philox seed and
+  the initial particles are broadcast from the group's rank 0, so every rank holds the
+  same replicated filter whatever its local torch RNG state; replay mode (``rng='torch'``)
+  consumes the host generator on every rank and therefore requires identical torch RNG
+  states on all ranks (checked at construction: ``ValueError`` otherwise);
+* ``shard=(world, rank)``: sharding with a caller-driven exchange (``exchange=`` or the
+  staged calls); a Philox filter then needs an explicit ``seed`` (nothing to broadcast);
 * ``dedup`` (default True): evaluate the dynamics GP once per distinct (resampling
   ancestor, new class) pair -- offspring of one ancestor hold bit-identical states -- and
   share the result; bitwise identical to ``dedup=False`` (every particle evaluated).
@@ -58,9 +64,6 @@ class GPMDM_PF:
             raise ValueError("resample must be 'multinomial' or 'systematic'")
         self._rng = rng
         self._resample_mode = resample
-        if seed is None:
-            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if rng == "philox" else 0
-        self._seed = int(seed)
         self._group = process_group
         self._exchange_fn = exchange
         if process_group is not None:
@@ -68,8 +71,22 @@ class GPMDM_PF:
             self._world, self._rank = dist.get_world_size(process_group), dist.get_rank(process_group)
         elif shard is not None:                 # (world, rank) with a caller-driven exchange
             self._world, self._rank = int(shard[0]), int(shard[1])
+            if self._world > 1 and rng == "philox" and seed is None:
+                raise ValueError("shard= with rng='philox' needs an explicit seed (identical on every rank)")
         else:
             self._world, self._rank = 1, 0
+        self._collective = process_group is not None and self._world > 1
+        if self._collective and rng == "torch":
+            from .distributed import identical_on_all_ranks
+            if not identical_on_all_ranks(torch.get_rng_state().numpy().tobytes(), process_group, self.device):
+                raise ValueError("rng='torch' on several ranks needs identical torch RNG states "
+                                 "(torch.manual_seed with the same seed on every rank)")
+        if seed is None:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if rng == "philox" else 0
+        if self._collective and rng == "philox":
+            from .distributed import broadcast_array
+            seed = int(broadcast_array(np.array([seed], dtype=np.int64), process_group, self.device)[0])
+        self._seed = int(seed)
         lib = _lib.load()
         T = np.ascontiguousarray(self._markov_switching_model.numpy(), dtype=np.float64)
         h = ctypes.c_void_p()
@@ -80,6 +97,7 @@ class GPMDM_PF:
             _lib.GPMDM_RESAMPLE_MULTINOMIAL if resample == "multinomial" else _lib.GPMDM_RESAMPLE_SYSTEMATIC,
             self._world, self._rank, ctypes.byref(h)), "GPMDM_PF")
         self._h = h
+        self._model_gen = gpmdm.generation
         _lib.check(lib.gpmdm_pf_set_dedup(h, 1 if dedup else 0), "dedup")
         _lib.check(lib.gpmdm_pf_set_shard_order(h, 1 if shard_order else 0), "shard_order")
         self._readout = None
@@ -103,6 +121,14 @@ class GPMDM_PF:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
+    def _sync_model(self):
+        """The reference filter reads its GPMDM's current state on every call
+        (gpmdm_pf.py:164, 183): after the model was rebuilt (set_latents, train_adam,
+        a reload into the same object) rebind the device filter to the new image."""
+        if self._gpmdm.generation != self._model_gen:
+            _lib.check(_lib.load().gpmdm_pf_set_model(self._h, self._gpmdm.handle), "rebind to the rebuilt model")
+            self._model_gen = self._gpmdm.generation
+
     def _divide_into_n_parts(self, x: int, n: int) -> list:
         """gpmdm_pf.py:287-292."""
         g, r = divmod(x, n)
@@ -117,6 +143,11 @@ class GPMDM_PF:
         states = np.concatenate([self._gpmdm.get_X_for_class(c).numpy()[idx[c]] for c in range(self.num_classes)], 0)
         classes = np.concatenate([np.full(counts[c], c, dtype=np.int64) for c in range(self.num_classes)])
         states = np.ascontiguousarray(states, dtype=np.float64)
+        if self._collective:                    # one replicated filter: rank 0's particles
+            from .distributed import broadcast_array
+            states = np.ascontiguousarray(broadcast_array(states, self._group, self.device))
+            classes = np.ascontiguousarray(broadcast_array(classes, self._group, self.device))
+        self._sync_model()
         _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "init")
         self._readout = None
 
@@ -128,6 +159,7 @@ class GPMDM_PF:
         z = _as_f64_vector(z)
         if z.shape[0] != self.observation_dim:
             raise ValueError(f"observation must have {self.observation_dim} values, got {z.shape[0]}")
+        self._sync_model()
         lib, h, s = _lib.load(), self._h, self._stream()
         P, C, d = self._num_particles, self.num_classes, self.latent_dim
         if self._rng == "torch":
@@ -155,6 +187,7 @@ class GPMDM_PF:
         if self._rng != "torch":
             raise ValueError("explicit draws need rng='torch' (replay mode)")
         z = _as_f64_vector(z)
+        self._sync_model()
         lib, h, s = _lib.load(), self._h, self._stream()
         P, C, d = self._num_particles, self.num_classes, self.latent_dim
         E = np.ascontiguousarray(exp_draws, dtype=np.float64).reshape(P, C)
@@ -181,6 +214,7 @@ class GPMDM_PF:
     # staged update for callers that drive the exchange themselves (tests, schedulers)
     def _stage_propagate(self, z):
         z = np.ascontiguousarray(torch.as_tensor(z, dtype=torch.float64).cpu().numpy().reshape(-1))
+        self._sync_model()
         lib, h, s = _lib.load(), self._h, self._stream()
         _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
         _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), None, s), "propagate")
@@ -221,17 +255,29 @@ class GPMDM_PF:
 
     def predict(self) -> torch.Tensor:
         """Dynamics-only one-step prediction of the latent mean: the average over the
-        current particles of each particle's class dynamics-GP mean (gpmdm.py:1032-1068).
-        Does not change the filter state and draws no random numbers."""
-        st = self.export_state()
-        X, cls = st["states"], st["classes"]
-        acc = np.zeros(self.latent_dim)
-        for c in range(self.num_classes):
-            m = cls == c
-            if m.any():
-                mu, _ = self._gpmdm.map_x_dynamics_for_class(torch.as_tensor(X[m]), c)
-                acc += mu.cpu().numpy().sum(0)
-        return torch.tensor(acc / X.shape[0], dtype=torch.float64)
+        current particles of each particle's class dynamics-GP mean (gpmdm.py:1032-1068),
+        computed on the device (gpmdm_pf_predict: class grouping, the dynamics GP tiles,
+        a fixed-order mean).  Does not change the filter state and draws no random numbers."""
+        self._sync_model()
+        out = np.zeros(self.latent_dim)
+        _lib.check(_lib.load().gpmdm_pf_predict(self._h, _lib.dptr(out), self._stream()), "predict")
+        return torch.from_numpy(out)
+
+    @property
+    def frame(self) -> int:
+        """Resamples done so far: the Philox counter of the next step's draws."""
+        f = np.zeros(1, dtype=np.int64)
+        _lib.check(_lib.load().gpmdm_pf_frame(self._h, _lib.i64ptr(f)), "frame")
+        return int(f[0])
+
+    def health(self, reset: bool = False) -> dict:
+        """Failure counters since creation (or the last reset), per particle and step
+        (SURVEY.md §5): non-positive observation / dynamics variances and non-finite
+        log-likelihoods / states.  The arithmetic is the reference's (NaN propagates);
+        these counts say when it happened."""
+        n = np.zeros(len(_lib.HEALTH), dtype=np.int64)
+        _lib.check(_lib.load().gpmdm_pf_health(self._h, _lib.i64ptr(n), 1 if reset else 0, self._stream()), "health")
+        return {k: int(v) for k, v in zip(_lib.HEALTH, n)}
 
     # ---- introspection (tests, checkpoint of the filter state) --------------------
     def export_state(self) -> dict:
@@ -246,6 +292,7 @@ class GPMDM_PF:
 
     def load_state(self, states, classes):
         """Set the particle states/classes (e.g. a reference pre-step state)."""
+        self._sync_model()
         states = np.ascontiguousarray(states, dtype=np.float64).reshape(self._num_particles, self.latent_dim)
         classes = np.ascontiguousarray(classes, dtype=np.int64).reshape(self._num_particles)
         _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "load_state")

@@ -64,12 +64,16 @@ def _inverse_and_logdet(K):
         return torch.cholesky_inverse(L), 2.0 * torch.sum(torch.log(torch.diagonal(L)))
     import ctypes
     from . import _lib
+    if n > 46340:                       # the library's own bound (rocBLAS int32 indexing of n*n)
+        raise ValueError(f"gpmdm_spd_inverse: n={n} exceeds 46340")
     A = K.detach().contiguous().clone()
     ld = ctypes.c_double()
     rc = _lib.load().gpmdm_spd_inverse(A.device.index or 0, ctypes.c_void_p(A.data_ptr()), n, ctypes.byref(ld),
                                        ctypes.c_void_p(torch.cuda.current_stream(A.device).cuda_stream))
-    if rc != 0:
+    if rc == _lib.GPMDM_E_INVALID:      # not positive definite: NaN, as the reference's cholesky_ex
         A.fill_(float("nan"))
+    else:                               # HIP / rocSOLVER failure, out of memory, n too large: raise
+        _lib.check(rc, "gpmdm_spd_inverse")
     return A, torch.tensor(ld.value, dtype=K.dtype, device=K.device)
 
 

@@ -197,6 +197,33 @@ int gpmdm_pf_dyn_rows(gpmdm_pf_t pf, int64_t* rows, void* stream);
  * de-duplication.  Every rank must make the same call, outside switch..resample. */
 int gpmdm_pf_set_shard_order(gpmdm_pf_t pf, int enable);
 
+/* Frames (resamples) this handle has done: the Philox counter of the next step's draws
+ * (rng_mode GPMDM_RNG_PHILOX; oracle/philox.py restates the draws). */
+int gpmdm_pf_frame(gpmdm_pf_t pf, int64_t* frame);
+
+/* Rebind a filter to another model of the same (C, d, D) on the same device -- the
+ * reference filter reads its GPMDM's current state on every call (gpmdm_pf.py:164, 183),
+ * so a retrained / re-initialised model (GPMDM.set_latents, train_adam) must reach the
+ * filter.  Models are reference counted: a filter keeps the model it was built on (or
+ * last rebound to) alive, so gpmdm_model_destroy never leaves a filter dangling.  Not
+ * between switch and resample. */
+int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t model);
+
+/* Failure detection.  The filter keeps the reference's arithmetic: a
+ * non-positive predictive variance gives NaN log-likelihoods / states as it does in
+ * gpmdm_pf.py:167-168, 188-192.  Each event is counted on the device (per particle and
+ * step) and read here: counts[0] observation-GP variance <= 0, [1] non-finite
+ * log-likelihood, [2] dynamics-GP variance <= 0, [3] non-finite propagated state.
+ * Synchronises `stream`; reset != 0 zeroes the counters afterwards. */
+#define GPMDM_HEALTH_N 4
+int gpmdm_pf_health(gpmdm_pf_t pf, int64_t* counts, int reset, void* stream);
+
+/* GPMDM_PF.predict() (BASELINE.json north_star): the one-step dynamics-GP prediction of
+ * the latent mean, (1/P) sum_p mu_{c_p}(x_p) with mu_c = map_x_dynamics_for_class's mean
+ * (gpmdm.py:1032-1068) over the current particles and classes.  No state change, no draws.
+ * mean: F x d host (F = 1 for a single filter).  Synchronises `stream`. */
+int gpmdm_pf_predict(gpmdm_pf_t pf, double* mean, void* stream);
+
 /* Device-side GP factor: the recipe of _precompute_kernel_inverses
  * (gpmdm.py:1284-1305) for one GP block -- the observation GP, or one class block of the
  * dynamics GP (the reference's full masked matrix has exact zeros off the class blocks):

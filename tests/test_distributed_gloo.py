@@ -65,3 +65,38 @@ def test_shard_ranges_cover():
             r = [shard_range(P, world, k) for k in range(world)]
             assert r[0][0] == 0 and r[-1][1] == P
             assert all(r[k][1] == r[k + 1][0] for k in range(world - 1))
+
+
+def _bcast_worker(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gpmdm_amd.distributed import broadcast_array, identical_on_all_ranks
+        a = np.arange(12, dtype=np.float64).reshape(3, 4) * (rank + 1)
+        b = broadcast_array(a)
+        seed = broadcast_array(np.array([1000 + rank], dtype=np.int64))
+        same = identical_on_all_ranks(b"abc")
+        differ = identical_on_all_ranks(bytes([rank]))
+        out_q.put((rank, b, int(seed[0]), same, differ))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_broadcast_and_consistency_check_two_ranks():
+    """The helpers GPMDM_PF(process_group=...) uses so every rank holds one replicated
+    filter: rank 0's seed / particles broadcast, and the replay-mode RNG-state check."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bcast_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, b, seed, same, differ in res:
+        assert np.array_equal(b, np.arange(12, dtype=np.float64).reshape(3, 4)), rank
+        assert seed == 1000 and same and not differ

@@ -1,0 +1,127 @@
+"""GPU parity at the large BASELINE.json configurations (VERDICT r01 "missing" #1).
+
+* configs[2]: N=10000, D=128, d=8, C=5 (5 sequences of 400 frames per class);
+* configs[4]: N=20000, D=256, d=16, C=8 (5 x 500 per class; block-diagonal K_x);
+* configs[3]: N=2000, D=62, d=3 with P = 1,000,000 sharded over 8 ranks.
+
+The models are the SURVEY §8(d) synthetic generator at full size (PCA latents, unit
+lengthscales / lambdas / linear coefficients, sigma_n = 0.1), the same models
+``bench.py --config 3|5`` runs, built through the product path (device precompute:
+rocSOLVER potrf + trtri, ``gpmdm_gp_factor``).  The checker is the CPU oracle
+(``oracle/gpmdm_oracle.py``) on the GPU box's host cores, with the observation GP
+factored by Cholesky solves (``precompute("cholesky")``: the explicit-inverse recipe is
+O(N^3) three times over and would dominate the run at N = 2 x 10^4; the two agree to
+4e-10 at N = 2000, tests/test_oracle_golden.py).  Checks (reference semantics
+gpmdm.py:923-963, 1032-1068; gpmdm_pf.py:137-262):
+
+* predictive maps at 500 query points: means 1e-8, variances 1e-6 normwise;
+* one resynced filter step at P = 2000 with explicit draws (update_with_draws): classes
+  exact, states 1e-6, weights 1e-5, posterior 1e-6 abs, state mean 1e-6;
+* configs[3]: 8 logical shards of P = 10^6 on one GPU, bitwise equal to one rank.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import nrel, product_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _synthetic(cfg):
+    from gpmdm_amd import GPMDM, synthetic
+    from oracle import gpmdm_oracle as O
+    c = synthetic.CONFIGS[cfg]
+    data = synthetic.make_sequences(c["C"], c["S"], c["L"], c["D"], c["d"], seed=0)
+    hp = synthetic.default_hyperparameters(c["D"], c["d"], 0.1)
+    m = GPMDM(D=c["D"], d=c["d"], n_classes=c["C"], dyn_target="full", dyn_back_step=1, **hp)
+    for k in range(c["C"]):
+        for y in data.sequences[k]:
+            m.add_data(y, k)
+    m.init_X()
+    lp = {k: (getattr(m, k).numpy() if getattr(m, k).dim() else float(getattr(m, k)))
+          for k in ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n", "x_log_lengthscales",
+                    "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff")}
+    om = O.OracleModel(X=m.X.numpy().copy(), Y=m.get_Y().astype(np.float64),
+                       seq_lengths=[[c["L"]] * c["S"]] * c["C"], **lp).precompute("cholesky")
+    return m, om, data, c
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_large_config_maps_and_step_vs_oracle(cfg):
+    from gpmdm_amd import GPMDM_PF, synthetic
+    from oracle import gpmdm_oracle as O
+    m, om, data, c = _synthetic(cfg)
+    C, d = c["C"], c["d"]
+    assert m.X.shape[0] == C * c["S"] * c["L"]
+    rng = np.random.RandomState(100 + cfg)
+    X = m.X.numpy()
+    xs = X[rng.randint(0, X.shape[0], 500)] + 0.05 * rng.randn(500, d)
+    mu, var = m.map_x_to_y(torch.tensor(xs))
+    omu, ovar = om.map_x_to_y(xs)
+    assert nrel(mu.numpy(), omu) < 1e-8
+    assert nrel(var.numpy(), ovar) < 1e-6
+    for k in range(C):
+        mu, var = m.map_x_dynamics_for_class(torch.tensor(xs), k)
+        omu, ovar = om.map_x_dynamics_for_class(xs, k)
+        assert nrel(mu.numpy(), omu) < 1e-8, k
+        assert nrel(var.numpy(), ovar) < 1e-6, k
+    # one resynced filter step from a spread-out cloud (two warm-up steps on the device)
+    P = 2000
+    T = synthetic.markov_matrix(C)
+    pf = GPMDM_PF(m, torch.tensor(T), P, rng="torch")
+    torch.manual_seed(cfg)
+    zs = data.observation_stream(3, seed=1)
+    pf.update(zs[0])
+    pf.update(zs[1])
+    st0 = pf.export_state()
+    E = rng.exponential(size=(P, C))
+    cls1 = O.switch_classes(st0["classes"], T, E)
+    nrm = rng.randn(P, d)
+    u = rng.rand(P)
+    pf.update_with_draws(zs[2], E, nrm, u)
+    r = O.step(om, T, st0["states"], st0["classes"], zs[2], E, nrm, u)
+    st = pf.export_state()
+    assert np.array_equal(cls1, r.classes_switched)
+    assert np.array_equal(st["resample_idx"], r.resample_idx)
+    assert np.array_equal(st["classes"], r.classes)
+    assert nrel(st["states"], r.states) < 1e-6
+    assert nrel(st["w"], r.w) < 1e-5
+    assert np.max(np.abs(pf.class_probabilities().numpy() - r.posterior)) < 1e-6
+    assert nrel(pf.current_state_mean().numpy(), r.mean) < 1e-6
+    assert all(v == 0 for v in pf.health().values())
+
+
+@pytest.mark.timeout(300)
+def test_config4_one_million_particles_8_shards(fx_config2):
+    """configs[3]'s real size: P = 1,000,000 over 8 ranks (125k each), N = 2000 model;
+    the 8 logical shards on one GPU (exchange in-process) are bitwise one rank, with
+    ancestor-ordered shards (the bench's multi-rank default) over 3 frames."""
+    from gpmdm_amd import GPMDM_PF
+    m = product_model(fx_config2)
+    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
+    P, world = 1_000_000, 8
+    ref = GPMDM_PF(m, T, P, rng="philox", seed=41)
+    torch.manual_seed(4)
+    init = ref.export_state()
+    ranks = [GPMDM_PF(m, T, P, rng="philox", seed=41, shard=(world, r)) for r in range(world)]
+    for pf in ranks:
+        pf.load_state(init["states"], init["classes"])
+    ref.load_state(init["states"], init["classes"])
+    Y = m.get_Y()
+    for k in range(3):
+        z = Y[500 + 7 * k]
+        ref.update(z)
+        full = torch.cat([pf._stage_propagate(z) for pf in ranks], 0)
+        for pf in ranks:
+            pf._recv.copy_(full)
+            pf._stage_resample()
+        a = ref.export_state()
+        for r, pf in enumerate(ranks):
+            b = pf.export_state()
+            for key in ("states", "classes", "ll", "resample_idx"):
+                assert np.array_equal(a[key], b[key]), (k, r, key)
+            assert np.array_equal(ref.class_probabilities().numpy(), pf.class_probabilities().numpy())
+            assert np.array_equal(ref.current_state_mean().numpy(), pf.current_state_mean().numpy())
+        del full

@@ -1,0 +1,125 @@
+"""GPU: the real process-group path -- GPMDM_PF(process_group=...) in separate processes.
+
+Two ranks are spawned on this box's GPU with the gloo backend (RCCL refuses two ranks on
+one device; gloo moves the all-gather through host memory, the library and every kernel
+are the same as with nccl).  Each rank seeds torch *differently*: the filter must still be
+one replicated filter, because the Philox seed and the initial particles are broadcast
+from rank 0 (gpmdm_amd/pf.py).  After 3 frames every rank's states, classes, ll,
+resample indices and read-outs must be bitwise equal to a single-rank filter built in
+the parent with rank 0's torch seed.  Replay mode (rng='torch') with identical torch
+seeds is bitwise as well; with different seeds it must refuse (ValueError) instead of
+silently diverging.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import product_model
+
+pytestmark = pytest.mark.gpu
+
+P = 10_001
+FRAMES = 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _obs(m):
+    Y = m.get_Y()
+    return [np.asarray(Y[200 + 5 * k], dtype=np.float64) for k in range(FRAMES)]
+
+
+def _worker(rank, world, port, rng, seeds, out_q):
+    import torch.distributed as dist
+    from conftest import load_fixture
+    from gpmdm_amd import GPMDM_PF
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = product_model(load_fixture("config2_n2000_p1000"))
+        T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
+        torch.manual_seed(seeds[rank])
+        try:
+            pf = GPMDM_PF(m, T, P, rng=rng, process_group=dist.group.WORLD)
+        except ValueError as e:
+            out_q.put((rank, "ValueError", str(e)))
+            return
+        for z in _obs(m):
+            pf.update(z)
+        st = pf.export_state()
+        out_q.put((rank, "ok", dict(states=st["states"], classes=st["classes"], ll=st["ll"],
+                                     resample_idx=st["resample_idx"],
+                                     post=pf.class_probabilities().numpy(),
+                                     mean=pf.current_state_mean().numpy(), lik=pf.log_likelihood(),
+                                     seed=pf._seed)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(rng, seeds):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, rng, seeds, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict((r, (kind, payload)) for r, kind, payload in (q.get(timeout=240) for _ in range(world)))
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    return res
+
+
+def _single(m, rng, seed_torch):
+    from gpmdm_amd import GPMDM_PF
+    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
+    torch.manual_seed(seed_torch)
+    pf = GPMDM_PF(m, T, P, rng=rng)
+    for z in _obs(m):
+        pf.update(z)
+    return pf
+
+
+@pytest.mark.timeout(400)
+@pytest.mark.parametrize("rng,seeds", [("philox", (100, 101)), ("torch", (7, 7))])
+def test_process_group_filter_matches_single_rank(fx_config2, rng, seeds):
+    res = _run(rng, seeds)
+    m = product_model(fx_config2)
+    ref = _single(m, rng, seeds[0])
+    a = ref.export_state()
+    for r in range(2):
+        kind, got = res[r]
+        assert kind == "ok", got
+        if rng == "philox":
+            assert got["seed"] == ref._seed
+        for key in ("states", "classes", "ll", "resample_idx"):
+            assert np.array_equal(a[key], got[key]), (r, key)
+        assert np.array_equal(ref.class_probabilities().numpy(), got["post"])
+        assert np.array_equal(ref.current_state_mean().numpy(), got["mean"])
+        assert ref.log_likelihood() == got["lik"]
+
+
+@pytest.mark.timeout(400)
+def test_process_group_replay_refuses_different_torch_states():
+    res = _run("torch", (7, 8))
+    for r in range(2):
+        kind, msg = res[r]
+        assert kind == "ValueError" and "identical torch RNG" in msg

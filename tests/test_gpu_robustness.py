@@ -1,0 +1,85 @@
+"""GPU: model lifetime and failure detection.
+
+* A filter outlives a rebuild of its model (``GPMDM.set_latents`` destroys the old device
+  model): models are reference counted, and the filter rebinds to the rebuilt model on
+  its next call, as the reference filter reads its GPMDM's current state
+  (gpmdm_pf.py:164, 183).  The rebound filter must equal a filter built on the new model.
+* Failure counters (``GPMDM_PF.health``): the reference's NaN propagation
+  is kept, and every non-positive variance / non-finite log-likelihood or state is
+  counted.  A deliberately inconsistent model (K_y^-1 scaled by 9: kT K^-1 k > 1) makes
+  the observation variance negative and ll NaN, as the reference would; the sigma_n = 0.01
+  stress model stays healthy in fp64 (fp32 would not).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import product_model
+
+pytestmark = pytest.mark.gpu
+
+
+def test_filter_survives_model_rebuild(fx_config1):
+    from gpmdm_amd import GPMDM_PF
+    f = fx_config1
+    m = product_model(f)
+    T = torch.tensor(f["T"])
+    pf = GPMDM_PF(m, T, 500, rng="torch")
+    torch.manual_seed(1)
+    pf.update(f["z"][0])
+    old_gen = m.generation
+    m.set_latents(m.X.numpy() * 1.01)          # destroys the old handle, uploads a new model
+    assert m.generation == old_gen + 1
+    st0 = pf.export_state()
+    rng = np.random.RandomState(2)
+    E, nrm, u = rng.exponential(size=(500, 2)), rng.randn(500, m.d), rng.rand(500)
+    pf.update_with_draws(f["z"][1], E, nrm, u)  # rebinds, then steps on the new model
+    fresh = GPMDM_PF(m, T, 500, rng="torch")
+    fresh.load_state(st0["states"], st0["classes"])
+    fresh.update_with_draws(f["z"][1], E, nrm, u)
+    a, b = pf.export_state(), fresh.export_state()
+    for key in ("states", "classes", "ll", "resample_idx"):
+        assert np.array_equal(a[key], b[key]), key
+    assert np.array_equal(pf.predict().numpy(), fresh.predict().numpy())
+    del m                                       # the filter still holds its model
+    pf.update(f["z"][2])
+    assert np.all(np.isfinite(pf.export_state()["states"]))
+
+
+def test_health_counts_indefinite_model(fx_config1, monkeypatch):
+    from gpmdm_amd import GPMDM_PF, model as model_mod
+    f = fx_config1
+    good = product_model(f)
+    orig = model_mod._chol_inv_factor
+
+    def scaled(K, what):
+        R = orig(K, what)
+        return 3.0 * R if what == "K_y" else R  # K_y^-1 -> 9 K_y^-1
+
+    monkeypatch.setattr(model_mod, "_chol_inv_factor", scaled)
+    bad = product_model(f)
+    monkeypatch.setattr(model_mod, "_chol_inv_factor", orig)
+    T = torch.tensor(f["T"])
+    P = 1000
+    for m, expect_bad in ((good, False), (bad, True)):
+        pf = GPMDM_PF(m, T, P, rng="philox", seed=3)
+        pf.update(f["z"][0])
+        h = pf.health()
+        ll = pf.export_state()["ll"]
+        if expect_bad:
+            n_neg = int(np.sum(~np.isfinite(ll)))
+            assert h["obs_var_nonpositive"] > 0 and h["obs_ll_nonfinite"] == n_neg > 0, h
+        else:
+            assert h == {k: 0 for k in h}, h
+        pf.health(reset=True)
+        assert all(v == 0 for v in pf.health().values())
+
+
+def test_stress_model_is_healthy_in_fp64(fx_stress):
+    from gpmdm_amd import GPMDM_PF
+    f = fx_stress
+    m = product_model(f)
+    pf = GPMDM_PF(m, torch.tensor(f["T"]), 5000, rng="philox", seed=12)
+    for k in range(10):
+        pf.update(f["z"][k % f["z"].shape[0]])
+    assert all(v == 0 for v in pf.health().values()), pf.health()

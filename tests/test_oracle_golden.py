@@ -118,3 +118,68 @@ def test_oracle_training_loss_matches_reference():
     assert abs(ly - f["loss_y0"]) <= 1e-9 * abs(f["loss_y0"])
     assert abs(lx - f["loss_x0"]) <= 1e-9 * abs(f["loss_x0"])
     assert abs(O.gpdm_loss(om) - f["loss0"]) <= 1e-9 * abs(f["loss0"])
+
+
+@pytest.mark.parametrize("name", ["config1_n500_p100_f200", "config2_n2000_p1000"])
+def test_cholesky_observation_oracle_matches_reference(name):
+    """precompute("cholesky") (triangular solves instead of the explicit K_y^-1 recipe; the
+    large-configuration checker) against the reference's observation-map goldens."""
+    f = load_fixture(name)
+    m = oracle_model(f)
+    mc = O.OracleModel(X=m.X, Y=m.Y, seq_lengths=m.seq_lengths, y_log_lengthscales=m.y_log_lengthscales,
+                       y_log_lambdas=m.y_log_lambdas, y_log_sigma_n=m.y_log_sigma_n,
+                       x_log_lengthscales=m.x_log_lengthscales, x_log_lambdas=m.x_log_lambdas,
+                       x_log_sigma_n=m.x_log_sigma_n, x_log_lin_coeff=m.x_log_lin_coeff,
+                       sigma_n_num_X=m.sigma_n_num_X, sigma_n_num_Y=m.sigma_n_num_Y).precompute("cholesky")
+    mu, var = mc.map_x_to_y(f["obs_xs"])
+    assert nrel(mu, f["obs_mu"]) < 1e-8
+    assert nrel(var, f["obs_var"]) < 1e-6
+    xs = f["obs_xs"] + 0.05
+    assert nrel(mc.map_x_to_y(xs)[1], m.map_x_to_y(xs)[1]) < 1e-8
+
+
+def test_philox_known_answers():
+    """oracle/philox.py against the Philox4x32-10 known-answer vectors of Salmon et al.
+    (Random123's kat_vectors: counter, key -> output)."""
+    from oracle import philox as X
+    kat = [((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+           ((0xFFFFFFFF,) * 4, (0xFFFFFFFF, 0xFFFFFFFF), (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+           ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+            (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1))]
+    for ctr, key, out in kat:
+        got = X.philox4x32_10(*[np.uint32(c) for c in ctr], *key)
+        assert tuple(int(v) for v in got) == out
+
+
+def test_philox_draw_transforms():
+    """Shapes, ranges and moments of the restated device draws; streams and frames are
+    independent; a bank's filter f equals a single filter keyed seed + f."""
+    from oracle import philox as X
+    P = 200_000
+    E = X.switch_draws(7, 3, P, 3)
+    assert E.shape == (P, 3) and np.all(E > 0) and abs(E.mean() - 1.0) < 0.01
+    nrm = X.dynamics_normals(7, 3, P, 5)
+    assert nrm.shape == (P, 5) and abs(nrm.mean()) < 0.01 and abs(nrm.std() - 1.0) < 0.01
+    u = X.resample_uniforms(7, 3, P)
+    assert np.all((u >= 0) & (u < 1)) and abs(u.mean() - 0.5) < 0.01
+    assert not np.array_equal(u, X.resample_uniforms(7, 4, P))
+    assert np.array_equal(X.resample_uniforms(7, 3, 50, f=2), X.resample_uniforms(9, 3, 50))
+    assert 0.0 <= X.systematic_u0(7, 3) < 1.0
+    # 64-bit key carry: seed + f crosses the 32-bit boundary
+    k = X.filter_key(2 ** 32 - 1, 1)
+    assert k == (0, 1)
+
+
+def test_systematic_resample_oracle():
+    """Systematic resampling: offspring counts within floor/ceil(P w_i); identical to an
+    inverse-CDF search of the stratified uniforms (s + u0) / P."""
+    rng = np.random.RandomState(3)
+    for P in (1, 7, 1000):
+        w = rng.exponential(size=P) ** 3
+        w = w / w.sum()
+        u0 = rng.rand()
+        idx = O.systematic_resample_indices(w, u0)
+        n = np.bincount(idx, minlength=P)
+        assert np.all(n >= np.floor(P * w - 1e-9)) and np.all(n <= np.ceil(P * w + 1e-9))
+        u = (np.arange(P) + u0) / P
+        assert np.array_equal(idx, O.multinomial_resample_indices(w, u))
