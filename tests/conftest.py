@@ -90,3 +90,33 @@ def fx_config2():
 @pytest.fixture(scope="session")
 def fx_stress():
     return load_fixture("stress_n500_sigma001")
+
+
+def assert_step_matches(post, r, gpu_post, gpu_mean, u, resample="multinomial", what=""):
+    """A GPU filter step (``post`` = export after it, read-outs ``gpu_post``/``gpu_mean``)
+    against the oracle's step ``r`` from the same pre-step particles and draws.
+
+    Every stage is compared given the previous one: weights against the oracle's (1e-5
+    normwise); the resample indices against the oracle's inverse-CDF search of the GPU's
+    own weights with the same uniforms (exact up to 2 last-ulp CDF ties: the device scans
+    in another association order than numpy's cumsum); post-resample states / classes and
+    the read-outs against the oracle's propagated states, switched classes and read-out
+    formulas at the GPU's indices.  (Comparing indices searched in two independently
+    computed CDFs is not a parity statement at large P: a 1e-12 relative weight
+    difference moves ~P^2 x 1e-12 / 2 slots across a boundary.)"""
+    from oracle import gpmdm_oracle as O
+    idx = post["resample_idx"]
+    assert nrel(post["w"], r.w) < 1e-5, (what, nrel(post["w"], r.w))
+    if resample == "multinomial":
+        ref_idx = O.multinomial_resample_indices(post["w"], u)
+    else:
+        ref_idx = O.systematic_resample_indices(post["w"], float(np.asarray(u).reshape(-1)[0]))
+    assert int(np.sum(ref_idx != idx)) <= 2, (what, int(np.sum(ref_idx != idx)))
+    assert np.array_equal(post["classes"], r.classes_switched[idx]), what
+    assert nrel(post["states"], r.states_propagated[idx]) < 1e-6, what
+    C = len(r.posterior)
+    ref_post = O.class_probabilities(r.ll, r.log_w, r.classes_switched[idx], C)
+    ref_mean = O.current_state_mean(r.states_propagated[idx], r.w)
+    assert np.max(np.abs(gpu_post - ref_post)) < 1e-6, what
+    assert nrel(gpu_mean, ref_mean) < 1e-6, what
+    return int(np.sum(r.resample_idx != idx))

@@ -5,10 +5,9 @@ Each step is *resynced*: the oracle starts from the GPU's own pre-step particles
 draws the frame's numbers with the restated Philox4x32-10 keyed exactly as the kernels
 key them (seed + filter, frame, particle index, stream), runs the reference step
 (``oracle.gpmdm_oracle.step``, gpmdm_pf.py:117-262) and the GPU's post-step state must
-match.  Tolerances (as tests/test_gpu_parity.py): classes exact; resample indices exact
-except at most 2 slots whose uniform falls on a last-ulp tie of the two CDFs (the device
-scans the weights in a different association order than numpy's cumsum); states 1e-6,
-weights 1e-5 normwise; posterior 1e-6 abs; state mean 1e-6 normwise.  The device's log /
+match (``conftest.assert_step_matches``: weights 1e-5 normwise; resample indices equal to
+the oracle's search of the GPU's weights with the restated uniforms, up to 2 last-ulp CDF
+ties; classes exact; states 1e-6 normwise; posterior 1e-6 abs; state mean 1e-6).  The device's log /
 sincos and numpy's may differ in the last ulp, which moves an Exp(1) or normal draw by
 ~1e-16 relative: far below every tolerance, and an argmax(T/E) flip would need a tie at
 that level.
@@ -17,7 +16,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import nrel, oracle_model, product_model
+from conftest import assert_step_matches, nrel, oracle_model, product_model
 
 pytestmark = pytest.mark.gpu
 
@@ -33,33 +32,15 @@ def om2(fx_config2):
 
 
 def _oracle_step(om, T, pre, z, seed, frame, resample, f=0):
+    """(oracle StepResult, uniforms) of one step with the restated Philox draws."""
     from oracle import gpmdm_oracle as O
     from oracle import philox as X
     P, C, d = pre["states"].shape[0], T.shape[0], pre["states"].shape[1]
     E = X.switch_draws(seed, frame, P, C, f)
     nrm = X.dynamics_normals(seed, frame, P, d, f)
     u = X.resample_uniforms(seed, frame, P, f) if resample == "multinomial" else X.systematic_u0(seed, frame, f)
-    return O.step(om, T, pre["states"], pre["classes"], z, E, nrm, u, resample=resample, normals_by_particle=True)
-
-
-def _compare(post, r, gpu_post, gpu_mean, what):
-    """post: GPU export after the step; r: oracle StepResult.  Where a resample index sits
-    on a CDF tie, the oracle's read-outs are re-derived with the GPU's indices (the
-    read-outs pair post-resample classes/states with pre-resample weights,
-    gpmdm_pf.py:233-262, so one tie can move the posterior by ~1/P)."""
-    from oracle import gpmdm_oracle as O
-    mism = post["resample_idx"] != r.resample_idx
-    assert int(mism.sum()) <= 2, (what, int(mism.sum()))
-    ok = ~mism
-    assert np.array_equal(post["classes"][ok], r.classes[ok]), what
-    assert nrel(post["states"][ok], r.states[ok]) < 1e-6, what
-    assert nrel(post["w"], r.w) < 1e-5, what
-    idx = post["resample_idx"]
-    ref_post = O.class_probabilities(r.ll, r.log_w, r.classes_switched[idx], len(r.posterior))
-    ref_mean = O.current_state_mean(r.states_propagated[idx], r.w)
-    assert np.array_equal(post["classes"], r.classes_switched[idx]), what
-    assert np.max(np.abs(gpu_post - ref_post)) < 1e-6, what
-    assert nrel(gpu_mean, ref_mean) < 1e-6, what
+    r = O.step(om, T, pre["states"], pre["classes"], z, E, nrm, u, resample=resample, normals_by_particle=True)
+    return r, u
 
 
 @pytest.mark.parametrize("resample,P", [("multinomial", 100_000), ("systematic", 20_011)])
@@ -80,8 +61,9 @@ def test_philox_steps_vs_oracle(m2, om2, fx_config2, resample, P):
         z = Y[11 + k] + 0.01
         pf.update(z)
         post = pf.export_state()
-        r = _oracle_step(om2, T, pre, z, seed, frame, resample)
-        _compare(post, r, pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), (resample, k))
+        r, u = _oracle_step(om2, T, pre, z, seed, frame, resample)
+        assert_step_matches(post, r, pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), u,
+                            resample, (resample, k))
         assert abs(pf.log_likelihood() - r.lik) <= 1e-5 * abs(r.lik)
         assert pf.health() == {k2: 0 for k2 in pf.health()}
 
@@ -104,9 +86,9 @@ def test_bank_filters_vs_oracle(m2, om2, fx_config2):
         gp, gm = bank.class_probabilities().numpy(), bank.current_state_mean().numpy()
         for f in range(F):
             pre_f = {key: pre[key][f] for key in ("states", "classes")}
-            r = _oracle_step(om2, T, pre_f, Z[f], seed, frame, "multinomial", f=f)
+            r, u = _oracle_step(om2, T, pre_f, Z[f], seed, frame, "multinomial", f=f)
             post_f = {key: post[key][f] for key in ("states", "classes", "w", "resample_idx")}
-            _compare(post_f, r, gp[f], gm[f], (k, f))
+            assert_step_matches(post_f, r, gp[f], gm[f], u, "multinomial", (k, f))
 
 
 def test_predict_device_vs_oracle(m2, om2, fx_config2):
