@@ -1,0 +1,37 @@
+"""GPU: a checkpoint written by the reference's GPMDM.save (tests/golden/make_checkpoint.py,
+after 20 steps of the reference's own train_adam) loads through GPMDM.load and its
+predictive maps match the reference's outputs for that trained model (gpmdm.py:923-963,
+1032-1068; tolerances of tests/test_gpu_parity.py), and a filter on it steps like the
+oracle built from the same parameters."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, assert_step_matches, nrel, oracle_model
+
+pytestmark = pytest.mark.gpu
+
+
+def test_reference_checkpoint_predictive_maps_and_step():
+    from gpmdm_amd import GPMDM, GPMDM_PF, synthetic
+    from oracle import gpmdm_oracle as O
+    f = dict(np.load(GOLDEN / "ref_checkpoint_config1.npz", allow_pickle=False))
+    m = GPMDM.load(GOLDEN / "ref_checkpoint_config1.pth")
+    for c in range(m.n_classes):
+        mu, var = m.map_x_dynamics_for_class(torch.tensor(f[f"dyn{c}_xs"]), c)
+        assert nrel(mu.numpy(), f[f"dyn{c}_mu"]) < 1e-8, c
+        assert nrel(var.numpy(), f[f"dyn{c}_var"]) < 1e-5, c
+    mu, var = m.map_x_to_y(torch.tensor(f["obs_xs"]))
+    assert nrel(mu.numpy(), f["obs_mu"]) < 1e-8
+    assert nrel(var.numpy(), f["obs_var"]) < 1e-6
+    om = oracle_model(f)
+    T = synthetic.markov_matrix(2)
+    P = 3000
+    pf = GPMDM_PF(m, torch.tensor(T), P, rng="torch")
+    st0 = pf.export_state()
+    rng = np.random.RandomState(3)
+    E, nrm, u = rng.exponential(size=(P, 2)), rng.randn(P, 3), rng.rand(P)
+    z = f["Y"][42] + 0.02
+    pf.update_with_draws(z, E, nrm, u)
+    r = O.step(om, T, st0["states"], st0["classes"], z, E, nrm, u)
+    assert_step_matches(pf.export_state(), r, pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), u)

@@ -54,3 +54,24 @@ def test_npz_round_trip(tmp_path):
     for k in ("y_log_lengthscales", "y_log_lambdas", "x_log_lin_coeff", "x_log_sigma_n"):
         assert torch.equal(getattr(m2, k), getattr(m, k)), k
     assert np.array_equal(m2.get_Y(), m.get_Y())
+
+
+def test_reference_written_checkpoint_loads(tmp_path):
+    """A checkpoint written by the reference's own GPMDM.save after 20 steps of its own
+    train_adam (tests/golden/make_checkpoint.py): the safe loader reproduces every saved
+    parameter bit for bit and the observation sequences; the .npz round trip keeps them."""
+    from conftest import GOLDEN
+    f = np.load(GOLDEN / "ref_checkpoint_config1.npz", allow_pickle=False)
+    m = GPMDM.load(GOLDEN / "ref_checkpoint_config1.pth", upload=False)
+    assert np.array_equal(m.X.numpy(), f["X"])
+    for k in ("y_log_lengthscales", "y_log_lambdas", "x_log_lengthscales", "x_log_lambdas", "x_log_lin_coeff"):
+        assert np.array_equal(getattr(m, k).numpy(), f[k]), k
+    for k in ("y_log_sigma_n", "x_log_sigma_n"):
+        assert float(getattr(m, k)) == float(f[k]), k
+    assert np.array_equal(m.get_Y(), f["Y"])
+    assert [[len(s) for s in c] for c in m.class_aware_observations_list] == f["seq_lengths"].tolist()
+    assert (m.D, m.d, m.n_classes, m.dyn_target, m.dyn_back_step) == (62, 3, 2, "full", 1)
+    q = tmp_path / "m.npz"
+    m.save(q)
+    m2 = GPMDM.load(q, upload=False)
+    assert np.array_equal(m2.X.numpy(), f["X"]) and np.array_equal(m2.get_Y(), f["Y"])
