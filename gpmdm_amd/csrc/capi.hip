@@ -11,6 +11,7 @@
 
 #include "../../include/gpmdm_hip.h"
 #include "common.h"
+#include "host_image.h"
 #include "pf_kernels.h"
 #include "status.h"
 
@@ -24,35 +25,17 @@ int fail(int code, const std::string& msg) {
 }
 }  // namespace gpmdm
 
+static_assert(kMaxClassesDesc == kMaxClasses, "descriptor check and kernels agree on the class limit");
+
 namespace {
 
-
-bool supported_d(int d) { return (d >= 1 && d <= 16) || d == 24 || d == 32; }
-
-constexpr double kLog2eX64 = 92.33248261689366;   // 64 / ln 2, as in gp_tile.hip
-
-// One GP's device image: scaled inputs (+ squared norms), raw inputs, and B = [R | M] in
-// MFMA-fragment order.
-//
-// Fragment layout (consumed by gp_tile.hip), for a tile shape (nw waves, each owning ntw
-// column tiles of 16; nb = 16 ntw nw columns per block): column block J stores
-// ksteps(block_kmax(J)) K-steps; each K-step holds nw waves x 256 ntw doubles, and inside a
-// wave's share the value v = 2q + e of lane l sits at q*128 + 2l + e, where
-// v = kk*ntw + nt is the B operand of MFMA sub-step kk (K=4) for column tile nt of wave w,
-// whose 16 columns are interleaved with the other waves' tiles:
-//   B[row = 16 ks + 4 kk + (l >> 4)][col = nb J + 16 (nw nt + w) + (l & 15)].
-// A lane's 4 ntw values are therefore 16-byte loads, each wave-instruction reading one
-// contiguous 1 KiB.  Rows below the diagonal of R are never stored (triangular skip).
-//
-// Dynamics images also carry H = (X~ C^2)^T B ((d+1) x cols, X~ = [Xin, 1], C^2 the linear
-// kernel's coefficients, gpmdm.py:493-506): the linear kernel's share of K* B, seeded into
-// the accumulators by MFMA.  Hf[((J kh_n + kh) nw + w) 64 ntw + ntw l + nt] =
-//   H[row = 4 kh + (l >> 4)][col = nb J + 16 (nw nt + w) + (l & 15)].
+// One GP's device image: scaled inputs (+ squared norms) and B = [R | M] (+ H for the
+// dynamics GPs) in MFMA-fragment order -- layout and packing in host_image.h.
 struct GpImage {
   int n_rows = 0, n_m = 0, n_j = 0, coff = 0;
   TileGeo geo = kGeo64x256;
-  double* Xs = nullptr;   // n_rows x d, inputs / lengthscales
-  double* Xsq = nullptr;  // n_rows
+  double* Xs = nullptr;   // row_cap(n_rows) x d, inputs / lengthscales
+  double* Xsq = nullptr;  // row_cap(n_rows)
   double* Hf = nullptr;   // dynamics only
   double* Bf = nullptr;
 
@@ -78,80 +61,35 @@ struct GpImage {
   int tiles(long long n) const { return (int)cdiv(n, geo.pt()); }
 };
 
+template <typename T>
+int upload(T** dst, const std::vector<T>& v) {
+  TRY(dalloc(dst, v.size()));
+  HIPCHK(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return GPMDM_OK;
+}
+
 int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const double* ls,
                 const double* lin_c2, const double* R, const double* M, TileGeo geo) {
-  const int nw = geo.nw, ntw = geo.ntw, nb = geo.nb(), fs = geo.fs(), ws = 256 * ntw;
+  const ImagePacker pk(n_rows, d, n_m, X, ls, lin_c2, R, M, geo);
   g.geo = geo;
   g.n_rows = n_rows;
   g.n_m = n_m;
-  g.coff = col_offset(n_rows + n_m, nb);
-  g.n_j = (int)cdiv(n_rows + n_m + g.coff, nb);
-  const int coff = g.coff;
-  const int cap = row_cap(n_rows);   // padded rows (gp_tile.h: padding rows generate K* = 0)
-  std::vector<double> xs((size_t)cap * d, 0.0), xsq(cap, kPadSq);
-  for (long long i = 0; i < n_rows; ++i) {
-    double s = 0.0;
-    for (int j = 0; j < d; ++j) {
-      const double v = X[i * d + j] / ls[j];
-      xs[i * d + j] = v;
-      s += v * v;
-    }
-    xsq[i] = s * kLog2eX64;   // pre-scaled for the kernel's exp2 (gp_tile.hip)
-  }
-  TRY(dalloc(&g.Xs, xs.size()));
-  HIPCHK(hipMemcpy(g.Xs, xs.data(), xs.size() * sizeof(double), hipMemcpyHostToDevice));
-  TRY(dalloc(&g.Xsq, xsq.size()));
-  HIPCHK(hipMemcpy(g.Xsq, xsq.data(), xsq.size() * sizeof(double), hipMemcpyHostToDevice));
-  long long total = 0;
-  for (int J = 0; J < g.n_j; ++J) total += (long long)ksteps(block_kmax(J, n_rows, nb, coff)) * fs;
-  TRY(dalloc(&g.Bf, (size_t)total));
-  auto val = [&](long long row, long long col) -> double {
-    if (row >= n_rows || col < 0) return 0.0;
-    if (col < n_rows) return row <= col ? R[row * n_rows + col] : 0.0;   // upper triangle of R
-    const long long j = col - n_rows;
-    return j < n_m ? M[row * n_m + j] : 0.0;
-  };
+  g.coff = pk.coff;
+  g.n_j = pk.n_j;
+  std::vector<double> xs, xsq, hf;
+  pk.inputs(xs, xsq);
+  TRY(upload(&g.Xs, xs));
+  TRY(upload(&g.Xsq, xsq));
   if (lin_c2) {
-    const long long n_cols = (long long)n_rows + n_m;
-    std::vector<double> H((size_t)(d + 1) * n_cols, 0.0);
-    for (long long i = 0; i < n_rows; ++i)
-      for (long long col = 0; col < n_cols; ++col) {
-        const double b = val(i, col);
-        if (b == 0.0) continue;
-        for (int k = 0; k < d; ++k) H[k * n_cols + col] += lin_c2[k] * X[i * d + k] * b;
-        H[(size_t)d * n_cols + col] += lin_c2[d] * b;
-      }
-    const int kh_n = lin_substeps(d);
-    std::vector<double> hf((size_t)g.n_j * kh_n * nw * 64 * ntw, 0.0);
-    for (int J = 0; J < g.n_j; ++J)
-      for (int kh = 0; kh < kh_n; ++kh)
-        for (int w = 0; w < nw; ++w)
-          for (int l = 0; l < 64; ++l)
-            for (int nt = 0; nt < ntw; ++nt) {
-              const int row = 4 * kh + (l >> 4);
-              const long long col = (long long)J * nb + 16 * (nw * nt + w) + (l & 15) - coff;
-              if (row <= d && col >= 0 && col < n_cols)
-                hf[(((size_t)J * kh_n + kh) * nw + w) * 64 * ntw + ntw * l + nt] = H[row * n_cols + col];
-            }
-    TRY(dalloc(&g.Hf, hf.size()));
-    HIPCHK(hipMemcpy(g.Hf, hf.data(), hf.size() * sizeof(double), hipMemcpyHostToDevice));
+    pk.linear(hf);
+    TRY(upload(&g.Hf, hf));
   }
+  TRY(dalloc(&g.Bf, (size_t)pk.total_doubles()));
   long long off = 0;
   std::vector<double> buf;
   for (int J = 0; J < g.n_j; ++J) {
-    const int nks = ksteps(block_kmax(J, n_rows, nb, coff));
-    buf.assign((size_t)nks * fs, 0.0);
-    for (int ks = 0; ks < nks; ++ks)
-      for (int w = 0; w < nw; ++w) {
-        double* dst = buf.data() + ((size_t)ks * nw + w) * ws;
-        for (int l = 0; l < 64; ++l)
-          for (int v = 0; v < 4 * ntw; ++v) {
-            const int kk = v / ntw, nt = v % ntw;
-            const long long row = (long long)ks * kBK + kk * 4 + (l >> 4);
-            const long long col = (long long)J * nb + 16 * (nw * nt + w) + (l & 15) - coff;
-            dst[(v >> 1) * 128 + 2 * l + (v & 1)] = val(row, col);
-          }
-      }
+    buf.assign((size_t)pk.block_doubles(J), 0.0);
+    pk.pack_block(J, buf.data());
     HIPCHK(hipMemcpy(g.Bf + off, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice));
     off += (long long)buf.size();
   }
@@ -313,16 +251,12 @@ const char* gpmdm_last_error(void) { return g_err.c_str(); }
 const char* gpmdm_version(void) { return "gpmdm_hip 0.1.0 (gfx950, fp64 MFMA)"; }
 
 int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* out) {
-  CHECK(desc && out, "null argument");
+  CHECK(out, "null argument");
   *out = nullptr;
-  CHECK(desc->N > 0 && desc->D > 0 && desc->C > 0, "N, D and C must be positive");
-  CHECK(supported_d(desc->d), "latent dimension d must be 1..16, 24 or 32");
-  CHECK(desc->C <= kMaxClasses, "at most 32 classes");
-  CHECK(desc->N < (1ll << 30), "N too large");
-  CHECK(desc->X && desc->obs_R && desc->obs_beta && desc->y_lengthscales && desc->y_inv_lambda2 &&
-            desc->Nc && desc->Xin && desc->dyn_R && desc->dyn_alpha && desc->x_lengthscales &&
-            desc->x_lin_coeff2 && desc->x_inv_lambda2,
-        "null array in model descriptor");
+  {
+    const std::string why = check_model_desc(desc);   // host_image.h
+    CHECK(why.empty(), why);
+  }
   HIPCHK(hipSetDevice(device));
   auto* m = new gpmdm_model();
   m->device = device;
@@ -351,17 +285,13 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
     case GPMDM_TILE_64x256: obs_geo = dyn_geo = kGeo64x256; break;
     case GPMDM_TILE_64x512: obs_geo = dyn_geo = kGeo64x512; break;
     case GPMDM_TILE_32x512: obs_geo = kGeo32x512; break;
-    default: delete m; return fail(GPMDM_E_INVALID, "tile_shape must be one of GPMDM_TILE_*");
+    default: break;   // rejected by check_model_desc
   }
   int rc = build_image(m->obs, (int)m->N, d, m->D, desc->X, desc->y_lengthscales, nullptr,
                        desc->obs_R, desc->obs_beta, obs_geo);
   if (rc) { delete m; return rc; }
   m->dyn.resize(m->C);
   for (int c = 0; c < m->C; ++c) {
-    if (desc->Nc[c] <= 0 || !desc->Xin[c] || !desc->dyn_R[c] || !desc->dyn_alpha[c]) {
-      delete m;
-      return fail(GPMDM_E_INVALID, "class " + std::to_string(c) + " has no dynamics rows");
-    }
     rc = build_image(m->dyn[c], (int)desc->Nc[c], d, d, desc->Xin[c], desc->x_lengthscales,
                      m->x_lin_c2.data(),
                      desc->dyn_R[c], desc->dyn_alpha[c], dyn_geo);

@@ -135,7 +135,6 @@ static __constant__ double kExp2Tab256[256] = {
 // exp(x) = 2^(t/64): n = rint(t), f = t - n (exact, Sterbenz), 2^(f/64) - 1 by a degree-5
 // polynomial in f (|f| <= 1/2, truncation < 2^-55), table 2^(j/64), ldexp.  No clamp is
 // needed: v_cvt_i32_f64 saturates and ldexp underflows to 0 exactly like exp().
-constexpr double kLog2eX64 = 92.33248261689366;   // 64 / ln 2 (host and device)
 
 __device__ __forceinline__ double exp2_64(double t, const double* tab) {
   const double n = __builtin_rint(t);

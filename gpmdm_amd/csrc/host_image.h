@@ -1,0 +1,146 @@
+// Host-side construction of a GP's device image and the model-descriptor checks
+// (plain C++17: no HIP; capi.hip uploads what this produces, and the host sanitizer test
+// tests/test_host_asan.py builds it with -fsanitize=address,undefined).
+//
+// Fragment layout (consumed by gp_tile.h), for a tile shape (nw waves, each owning ntw
+// column tiles of 16; nb = 16 ntw nw columns per block): column block J stores
+// ksteps(block_kmax(J)) K-steps; each K-step holds nw waves x 256 ntw doubles, and inside a
+// wave's share the value v = 2q + e of lane l sits at q*128 + 2l + e, where
+// v = kk*ntw + nt is the B operand of MFMA sub-step kk (K=4) for column tile nt of wave w,
+// whose 16 columns are interleaved with the other waves' tiles:
+//   B[row = 16 ks + 4 kk + (l >> 4)][col = nb J + 16 (nw nt + w) + (l & 15)].
+// A lane's 4 ntw values are therefore 16-byte loads, each wave-instruction reading one
+// contiguous 1 KiB.  Rows below the diagonal of R are never stored (triangular skip).
+//
+// Dynamics images also carry H = (X~ C^2)^T B ((d+1) x cols, X~ = [Xin, 1], C^2 the linear
+// kernel's coefficients, gpmdm.py:493-506): the linear kernel's share of K* B, seeded into
+// the accumulators by MFMA.  Hf[((J kh_n + kh) nw + w) 64 ntw + ntw l + nt] =
+//   H[row = 4 kh + (l >> 4)][col = nb J + 16 (nw nt + w) + (l & 15) - coff].
+#pragma once
+
+#include <cstddef>
+#include <string>
+#include <vector>
+
+#include "../../include/gpmdm_hip.h"
+#include "geometry.h"
+
+namespace gpmdm {
+
+constexpr int kMaxClassesDesc = 32;
+
+inline bool supported_d(int d) { return (d >= 1 && d <= 16) || d == 24 || d == 32; }
+
+// "" if the descriptor is usable, else the reason (gpmdm_model_create's argument checks).
+inline std::string check_model_desc(const gpmdm_model_desc* desc) {
+  if (!desc) return "null argument";
+  if (!(desc->N > 0 && desc->D > 0 && desc->C > 0)) return "N, D and C must be positive";
+  if (!supported_d(desc->d)) return "latent dimension d must be 1..16, 24 or 32";
+  if (desc->C > kMaxClassesDesc) return "at most 32 classes";
+  if (desc->N >= (1ll << 30)) return "N too large";
+  if (!(desc->X && desc->obs_R && desc->obs_beta && desc->y_lengthscales && desc->y_inv_lambda2 && desc->Nc &&
+        desc->Xin && desc->dyn_R && desc->dyn_alpha && desc->x_lengthscales && desc->x_lin_coeff2 &&
+        desc->x_inv_lambda2))
+    return "null array in model descriptor";
+  if (desc->tile_shape < GPMDM_TILE_DEFAULT || desc->tile_shape > GPMDM_TILE_32x512)
+    return "tile_shape must be one of GPMDM_TILE_*";
+  for (int c = 0; c < desc->C; ++c)
+    if (desc->Nc[c] <= 0 || desc->Nc[c] >= (1ll << 30) || !desc->Xin[c] || !desc->dyn_R[c] || !desc->dyn_alpha[c])
+      return "class " + std::to_string(c) + " has no dynamics rows";
+  return "";
+}
+
+// One GP's image, packed block by block (the device image is streamed up per block so the
+// host never holds a second copy of an N^2 matrix).
+struct ImagePacker {
+  int n_rows, d, n_m, coff, n_j;
+  TileGeo geo;
+  const double *X, *ls, *lin_c2, *R, *M;
+
+  ImagePacker(int n_rows_, int d_, int n_m_, const double* X_, const double* ls_, const double* lin_c2_,
+              const double* R_, const double* M_, TileGeo geo_)
+      : n_rows(n_rows_), d(d_), n_m(n_m_), geo(geo_), X(X_), ls(ls_), lin_c2(lin_c2_), R(R_), M(M_) {
+    coff = col_offset(n_rows + n_m, geo.nb());
+    n_j = (n_rows + n_m + coff + geo.nb() - 1) / geo.nb();
+  }
+
+  // B = [triu(R) | M] (row-major inputs R: n_rows x n_rows, M: n_rows x n_m)
+  double val(long long row, long long col) const {
+    if (row >= n_rows || col < 0) return 0.0;
+    if (col < n_rows) return row <= col ? R[row * n_rows + col] : 0.0;   // upper triangle of R
+    const long long j = col - n_rows;
+    return j < n_m ? M[row * n_m + j] : 0.0;
+  }
+
+  // Xs = X / ls (padded to row_cap rows with 0) and |Xs|^2 * 64/ln2 (padding: kPadSq).
+  void inputs(std::vector<double>& xs, std::vector<double>& xsq) const {
+    const int cap = row_cap(n_rows);
+    xs.assign((size_t)cap * d, 0.0);
+    xsq.assign((size_t)cap, kPadSq);
+    for (long long i = 0; i < n_rows; ++i) {
+      double s = 0.0;
+      for (int j = 0; j < d; ++j) {
+        const double v = X[i * d + j] / ls[j];
+        xs[i * d + j] = v;
+        s += v * v;
+      }
+      xsq[i] = s * kLog2eX64;
+    }
+  }
+
+  long long block_doubles(int J) const {
+    return (long long)ksteps(block_kmax(J, n_rows, geo.nb(), coff)) * geo.fs();
+  }
+  long long total_doubles() const {
+    long long t = 0;
+    for (int J = 0; J < n_j; ++J) t += block_doubles(J);
+    return t;
+  }
+
+  // Fragment-order B of column block J into dst[0, block_doubles(J)).
+  void pack_block(int J, double* dst) const {
+    const int nw = geo.nw, ntw = geo.ntw, nb = geo.nb(), ws = 256 * ntw;
+    const int nks = ksteps(block_kmax(J, n_rows, nb, coff));
+    for (int ks = 0; ks < nks; ++ks)
+      for (int w = 0; w < nw; ++w) {
+        double* o = dst + ((size_t)ks * nw + w) * ws;
+        for (int l = 0; l < 64; ++l)
+          for (int v = 0; v < 4 * ntw; ++v) {
+            const int kk = v / ntw, nt = v % ntw;
+            const long long row = (long long)ks * kBK + kk * 4 + (l >> 4);
+            const long long col = (long long)J * nb + 16 * (nw * nt + w) + (l & 15) - coff;
+            o[(v >> 1) * 128 + 2 * l + (v & 1)] = val(row, col);
+          }
+      }
+  }
+
+  // Dynamics GPs: H = (X~ C^2)^T B in fragment order (empty when lin_c2 is null).
+  void linear(std::vector<double>& hf) const {
+    hf.clear();
+    if (!lin_c2) return;
+    const int nw = geo.nw, ntw = geo.ntw, nb = geo.nb();
+    const long long n_cols = (long long)n_rows + n_m;
+    std::vector<double> H((size_t)(d + 1) * n_cols, 0.0);
+    for (long long i = 0; i < n_rows; ++i)
+      for (long long col = 0; col < n_cols; ++col) {
+        const double b = val(i, col);
+        if (b == 0.0) continue;
+        for (int k = 0; k < d; ++k) H[k * n_cols + col] += lin_c2[k] * X[i * d + k] * b;
+        H[(size_t)d * n_cols + col] += lin_c2[d] * b;
+      }
+    const int kh_n = lin_substeps(d);
+    hf.assign((size_t)n_j * kh_n * nw * 64 * ntw, 0.0);
+    for (int J = 0; J < n_j; ++J)
+      for (int kh = 0; kh < kh_n; ++kh)
+        for (int w = 0; w < nw; ++w)
+          for (int l = 0; l < 64; ++l)
+            for (int nt = 0; nt < ntw; ++nt) {
+              const int row = 4 * kh + (l >> 4);
+              const long long col = (long long)J * nb + 16 * (nw * nt + w) + (l & 15) - coff;
+              if (row <= d && col >= 0 && col < n_cols)
+                hf[(((size_t)J * kh_n + kh) * nw + w) * 64 * ntw + ntw * l + nt] = H[row * n_cols + col];
+            }
+  }
+};
+
+}  // namespace gpmdm

@@ -1,0 +1,128 @@
+// Host sanitizer driver for the C ABI's host-side code (gpmdm_amd/csrc/host_image.h):
+// descriptor validation and the MFMA-fragment image packing that gpmdm_model_create runs
+// before any upload.  Built and run by tests/test_host_asan.py with
+// -fsanitize=address,undefined; no HIP, no GPU.
+//
+// Packing check, independent of the layout formula: R and M are filled with distinct
+// values, so a correct image is a permutation of exactly the non-zero entries of
+// B = [triu(R) | M] plus zeros -- every distinct value must occur exactly once.
+#include <cmath>
+#include <cstdio>
+#include <map>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "host_image.h"
+
+using namespace gpmdm;
+
+static int failures = 0;
+#define EXPECT(cond, ...)                  \
+  do {                                     \
+    if (!(cond)) {                         \
+      std::printf("FAIL %s:%d ", __FILE__, __LINE__); \
+      std::printf(__VA_ARGS__);            \
+      std::printf("\n");                   \
+      ++failures;                          \
+    }                                      \
+  } while (0)
+
+static void check_packing(int n_rows, int n_m, int d, TileGeo geo, bool lin) {
+  std::mt19937_64 rng(n_rows * 131 + n_m * 7 + d);
+  std::uniform_real_distribution<double> U(-1.0, 1.0);
+  std::vector<double> X((size_t)n_rows * d), ls(d), c2(d + 1), R((size_t)n_rows * n_rows), M((size_t)n_rows * n_m);
+  for (auto& v : X) v = U(rng);
+  for (auto& v : ls) v = 0.5 + std::fabs(U(rng));
+  for (auto& v : c2) v = 0.1 + std::fabs(U(rng));
+  // distinct non-zero values: value = 1 + linear index in [R | M]
+  const long long ncols = (long long)n_rows + n_m;
+  for (long long i = 0; i < n_rows; ++i) {
+    for (long long j = 0; j < n_rows; ++j) R[i * n_rows + j] = 1.0 + (double)(i * ncols + j);
+    for (long long j = 0; j < n_m; ++j) M[i * n_m + j] = 1.0 + (double)(i * ncols + n_rows + j);
+  }
+  const ImagePacker pk(n_rows, d, n_m, X.data(), ls.data(), lin ? c2.data() : nullptr, R.data(), M.data(), geo);
+  EXPECT(pk.coff % 16 == 0 && pk.coff < geo.nb(), "coff %d", pk.coff);
+  EXPECT((long long)pk.n_j * geo.nb() >= ncols + pk.coff, "n_j %d", pk.n_j);
+  std::vector<double> img((size_t)pk.total_doubles());
+  long long off = 0;
+  for (int J = 0; J < pk.n_j; ++J) {
+    pk.pack_block(J, img.data() + off);
+    off += pk.block_doubles(J);
+  }
+  EXPECT(off == (long long)img.size(), "total %lld vs %zu", off, img.size());
+  std::map<double, int> seen;
+  for (double v : img)
+    if (v != 0.0) ++seen[v];
+  long long expected = 0;
+  for (long long i = 0; i < n_rows; ++i)
+    for (long long j = 0; j < ncols; ++j) {
+      if (j < n_rows && i > j) continue;   // strictly lower R: never stored
+      ++expected;
+      const double v = 1.0 + (double)(i * ncols + j);
+      auto it = seen.find(v);
+      EXPECT(it != seen.end() && it->second == 1, "B[%lld][%lld] stored %d times", i, j,
+             it == seen.end() ? 0 : it->second);
+    }
+  EXPECT((long long)seen.size() == expected, "%zu distinct values stored, %lld expected", seen.size(), expected);
+  std::vector<double> xs, xsq;
+  pk.inputs(xs, xsq);
+  EXPECT((int)xsq.size() == row_cap(n_rows) && xs.size() == xsq.size() * d, "input sizes");
+  for (int i = n_rows; i < (int)xsq.size(); ++i) EXPECT(xsq[i] == kPadSq, "pad row %d", i);
+  if (lin) {
+    std::vector<double> hf;
+    pk.linear(hf);
+    // H = (X~ C^2)^T triu-B: compare the sum of all entries (each H entry is stored once)
+    double ref = 0.0;
+    for (long long i = 0; i < n_rows; ++i)
+      for (long long j = 0; j < ncols; ++j) {
+        const double b = pk.val(i, j);
+        double w = c2[d];
+        for (int k = 0; k < d; ++k) w += c2[k] * X[i * d + k];
+        ref += w * b;
+      }
+    double got = 0.0;
+    for (double v : hf) got += v;
+    EXPECT(std::fabs(got - ref) <= 1e-9 * std::fabs(ref), "H sum %.17g vs %.17g", got, ref);
+  }
+}
+
+static void check_desc() {
+  std::vector<double> a(64, 1.0);
+  const double* pa = a.data();
+  const double* ptrs[2] = {pa, pa};
+  int64_t nc[2] = {3, 4};
+  gpmdm_model_desc d{};
+  EXPECT(check_model_desc(nullptr) == "null argument", "null desc");
+  d.N = 8; d.D = 5; d.d = 3; d.C = 2; d.tile_shape = 0;
+  EXPECT(check_model_desc(&d) == "null array in model descriptor", "null arrays");
+  d.X = d.obs_R = d.obs_beta = d.y_lengthscales = d.y_inv_lambda2 = pa;
+  d.x_lengthscales = d.x_lin_coeff2 = d.x_inv_lambda2 = pa;
+  d.Nc = nc; d.Xin = ptrs; d.dyn_R = ptrs; d.dyn_alpha = ptrs;
+  EXPECT(check_model_desc(&d).empty(), "valid: %s", check_model_desc(&d).c_str());
+  d.d = 17;
+  EXPECT(check_model_desc(&d).find("latent dimension") == 0, "d=17");
+  d.d = 3; d.C = 33;
+  EXPECT(check_model_desc(&d) == "at most 32 classes", "C=33");
+  d.C = 2; d.N = 0;
+  EXPECT(check_model_desc(&d).find("positive") != std::string::npos, "N=0");
+  d.N = 8; d.tile_shape = 9;
+  EXPECT(check_model_desc(&d).find("tile_shape") == 0, "tile shape");
+  d.tile_shape = 0; nc[1] = 0;
+  EXPECT(check_model_desc(&d) == "class 1 has no dynamics rows", "Nc=0");
+}
+
+int main() {
+  check_desc();
+  const TileGeo geos[] = {kGeo64x256, kGeo64x512, kGeo32x512, kGeo32x256, kGeo16x256};
+  const int shapes[][3] = {{1, 1, 1}, {7, 3, 2}, {16, 62, 3}, {17, 5, 3}, {250, 62, 3}, {513, 8, 16}, {300, 3, 8}};
+  for (const auto& g : geos)
+    for (const auto& s : shapes)
+      for (int lin = 0; lin < 2; ++lin) check_packing(s[0], s[1], s[2], g, lin != 0);
+  if (failures) {
+    std::printf("%d failures\n", failures);
+    return 1;
+  }
+  std::printf("ok\n");
+  return 0;
+}
