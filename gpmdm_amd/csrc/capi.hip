@@ -34,21 +34,18 @@ namespace {
 struct GpImage {
   int n_rows = 0, n_m = 0, n_j = 0, coff = 0;
   TileGeo geo = kGeo64x256;
-  double* Xs = nullptr;   // row_cap(n_rows) x d, inputs / lengthscales
-  double* Xsq = nullptr;  // row_cap(n_rows)
+  double* Xrec = nullptr; // row_cap(n_rows) x (d + 1) row records (host_image.h)
   double* Hf = nullptr;   // dynamics only
   double* Bf = nullptr;
 
   void release() {
-    dfree(Xs);
-    dfree(Xsq);
+    dfree(Xrec);
     dfree(Hf);
     dfree(Bf);
   }
   SegDesc seg() const {
     SegDesc s{};
-    s.Xs = Xs;
-    s.Xsq = Xsq;
+    s.Xrec = Xrec;
     s.Hf = Hf;
     s.Bf = Bf;
     s.n_rows = n_rows;
@@ -76,10 +73,9 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
   g.n_m = n_m;
   g.coff = pk.coff;
   g.n_j = pk.n_j;
-  std::vector<double> xs, xsq, hf;
-  pk.inputs(xs, xsq);
-  TRY(upload(&g.Xs, xs));
-  TRY(upload(&g.Xsq, xsq));
+  std::vector<double> rec, hf;
+  pk.records(rec);
+  TRY(upload(&g.Xrec, rec));
   if (lin_c2) {
     pk.linear(hf);
     TRY(upload(&g.Hf, hf));

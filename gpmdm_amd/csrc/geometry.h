@@ -47,11 +47,12 @@ constexpr int col_offset(int n_cols, int nb) {
   return r ? ((nb - r) / 16) * 16 : 0;
 }
 constexpr int ksteps(int kmax) { return (kmax + kBK - 1) / kBK; }
-// Rows the Xs / Xsq arrays are padded to: the K loop stages rows up to eight K-steps past
+// Rows the row records are padded to: the K loop stages rows up to eight K-steps past
 // the last one it multiplies (A/B variants included).  Padding rows have Xs = 0 and
 // |Xs|^2 = kPadSq (kernel value 0).
 constexpr int row_cap(int n_rows) { return (ksteps(n_rows) + 8) * kBK; }
-constexpr double kPadSq = 1e300;
+constexpr double kPadSq = 268435456.0;   // 2^28: exponent ~ -2^28 even x 128/ln2 scaled
+                                        // (v_cvt_i32_f64 exact, ldexp underflows to 0)
 // |Xs|^2 is stored pre-scaled by 64 / ln 2 for the tile kernel's exp2 (gp_tile.h)
 constexpr double kLog2eX64 = 92.33248261689366;
 // Dynamics linear kernel: K=4 MFMA sub-steps covering the d+1 rows of H.

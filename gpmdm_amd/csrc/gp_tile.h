@@ -61,6 +61,42 @@ static __constant__ double kExp2Tab[64] = {
     1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951
 };
 
+// 2^(j/128), j = 0..127 (correctly rounded).
+static __constant__ double kExp2Tab128[128] = {
+    1.0, 1.0054299011128027, 1.0108892860517005, 1.016378314910953,
+    1.0218971486541166, 1.0274459491187637, 1.0330248790212284, 1.0386341019613787,
+    1.0442737824274138, 1.0499440858006872, 1.0556451783605572, 1.061377227289262,
+    1.0671404006768237, 1.0729348675259756, 1.0787607977571199, 1.0846183622133092,
+    1.0905077326652577, 1.0964290818163769, 1.102382583307841, 1.1083684117236787,
+    1.1143867425958924, 1.1204377524096067, 1.1265216186082418, 1.1326385195987192,
+    1.1387886347566916, 1.1449721444318042, 1.1511892299529827, 1.1574400736337511,
+    1.1637248587775775, 1.1700437696832502, 1.1763969916502812, 1.182784710984341,
+    1.189207115002721, 1.1956643920398273, 1.202156731452703, 1.2086843236265816,
+    1.215247359980469, 1.2218460329727576, 1.22848053610687, 1.2351510639369334,
+    1.241857812073484, 1.2486009771892048, 1.255380757024691, 1.2621973503942507,
+    1.2690509571917332, 1.275941778396392, 1.2828700160787783, 1.2898358734066657,
+    1.2968395546510096, 1.3038812651919358, 1.3109612115247644, 1.318079601266064,
+    1.3252366431597413, 1.3324325470831615, 1.339667524053303, 1.3469417862329458,
+    1.3542555469368927, 1.3616090206382248, 1.3690024229745905, 1.3764359707545302,
+    1.383909881963832, 1.3914243757719262, 1.3989796725383112, 1.4065759938190154,
+    1.4142135623730951, 1.4218926021691656, 1.42961333839197, 1.4373759974489824,
+    1.4451808069770467, 1.4530279958490526, 1.460917794180647, 1.4688504333369818,
+    1.4768261459394993, 1.4848451658727524, 1.4929077282912648, 1.5010140696264256,
+    1.5091644275934228, 1.5173590411982147, 1.5255981507445384, 1.533881997840956,
+    1.5422108254079407, 1.550584877685, 1.559004400237837, 1.567469639965553,
+    1.5759808451078865, 1.5845382652524937, 1.593142151342267, 1.6017927556826934,
+    1.6104903319492543, 1.6192351351948637, 1.6280274218573478, 1.6368674497669644,
+    1.645755478153965, 1.6546917676561943, 1.6636765803267364, 1.6727101796415966,
+    1.681792830507429, 1.6909247992693053, 1.7001063537185235, 1.709337763100463,
+    1.718619298122478, 1.7279512309618377, 1.7373338352737062, 1.746767386199169,
+    1.7562521603732995, 1.7657884359332727, 1.7753764925265212, 1.785016611318935,
+    1.7947090750031072, 1.804454167806624, 1.8142521755003989, 1.8241033854070534,
+    1.8340080864093424, 1.843966568958626, 1.8539791250833855, 1.864046048397789,
+    1.8741676341103, 1.8843441790323345, 1.8945759815869656, 1.9048633418176741,
+    1.9152065613971474, 1.925605943636125, 1.9360617934922943, 1.9465744175792332,
+    1.9571441241754002, 1.9677712232331759, 1.978456026387951, 1.9891988469672663
+};
+
 // 2^(j/256), j = 0..255 (correctly rounded).
 static __constant__ double kExp2Tab256[256] = {
     1.0, 1.0027112750502025, 1.0054299011128027, 1.0081558981184175,
@@ -149,6 +185,58 @@ __device__ __forceinline__ double exp2_64(double t, const double* tab) {
   return ldexp(fma(tj, p, tj), ni >> 6);
 }
 
+// exp2_64 on a lane-replicated table: entry j of this lane's copy at tabl[j * TREP].
+template <int TREP>
+__device__ __forceinline__ double exp2_64r(double t, const double* tabl) {
+  const double n = __builtin_rint(t);
+  const double f = t - n;
+  double p = fma(f, 1.2417843701716925e-12, 5.732851688640402e-10);
+  p = fma(p, f, 2.1173137155464776e-07);
+  p = fma(p, f, 5.86490495505617e-05);
+  p = fma(p, f, 0.010830424696249145);
+  p *= f;                                                          // 2^(f/64) - 1
+  const int ni = (int)n;
+  const unsigned jj = __builtin_amdgcn_ubfe((unsigned)ni, 0u, 6u);   // ni & 63 (keeps v_lshl_add)
+  const double tj = tabl[jj * TREP];
+  return ldexp(fma(tj, p, tj), ni >> 6);
+}
+
+// Generalised table exp for the A/B variants (VAR bits 21-23): 2^(t / S) with S = 64 or 128
+// table entries, the integer part of the exponent reduced by `ioff` (a per-particle integer
+// folded out of t, see FOLD), and the final power of two applied by ldexp or by an integer
+// add to the exponent field (clamped at 2^-1022: a value below that comes out as ~2^-1022
+// instead of 0, which only ever multiplies zero-padded or negligible terms).
+// S = 128: |f| <= 1/2 in units of 1/128, 2^(f/128) - 1 = f q(f) with q a degree-3 fit
+// (least squares on Chebyshev nodes in long double; relative error 1.5e-16).
+template <int S, bool IEXP>
+__device__ __forceinline__ double exp2_gen(double t, const double* tab, int ioff) {
+  const double n = __builtin_rint(t);
+  const double f = t - n;
+  double p;
+  if constexpr (S == 128) {
+    double q = fma(f, 3.583032206604434e-11, 2.6466431146364605e-08);
+    q = fma(q, f, 1.4662262387641965e-05);
+    q = fma(q, f, 0.00541521234812427);
+    p = f * q;
+  } else {
+    p = fma(f, 1.2417843701716925e-12, 5.732851688640402e-10);
+    p = fma(p, f, 2.1173137155464776e-07);
+    p = fma(p, f, 5.86490495505617e-05);
+    p = fma(p, f, 0.010830424696249145);
+    p *= f;
+  }
+  const int ni = (int)n - ioff;
+  constexpr int SH = S == 128 ? 7 : 6;
+  const double tj = tab[ni & (S - 1)];
+  const double r = fma(tj, p, tj);
+  if constexpr (IEXP) {
+    const int e = max(ni >> SH, -1022);
+    return __hiloint2double(__double2hiint(r) + (e << 20), __double2loint(r));
+  } else {
+    return ldexp(r, ni >> SH);
+  }
+}
+
 // exp(x) for t = x 256 / ln 2 <= ~0 (the kernel-value exponent, pre-scaled like exp2_64).
 // Fewer and cheaper VALU ops than exp2_64 (FP64 VALU and FP64 MFMA share the SIMD's issue,
 // tools/microbench/mix_probe.hip): no v_rndne/v_cvt/v_ldexp.
@@ -214,6 +302,21 @@ __device__ __forceinline__ double exp2_64m(double t, const double* tab) {
 //   bit 15: A/B -- one barrier per K-step (2-slot rings) instead of one per two K-steps
 //   bit 16: A/B -- one barrier per four K-steps (8-slot rings)
 //   bit 17: particle coordinates from LDS in the generation (see PLDS)
+//   bit 18: A/B -- lane-replicated exp table (no LDS bank conflicts; one more integer
+//           VALU per value for the address) instead of one shared 64-entry table
+//           (measured: conflicts 16.4M -> 0 cycles per launch, time +0.4%)
+//   bit 19: A/B -- training rows staged from the separate Xs / Xsq arrays by global loads
+//           instead of row records by buffer loads (measured: records -1.1%)
+//   bit 20: A/B -- K loop unrolled by 4 with compile-time ring slots (LDS offsets as
+//           instruction immediates: -4.5 VALU per K-step, 2.7x code; measured: no gain)
+//   bit 21: FOLD -- |x_p / l|^2 leaves the per-value exponent: its integer part (in table
+//           units) is subtracted from the exponent as an integer, its fraction becomes a
+//           per-particle factor c_p = 2^(-frac / S) applied to the tile's rows in the
+//           epilogue (one fp64 add fewer per kernel value)
+//   bit 22: 128-entry exp table with a degree-4 polynomial (one fp64 fma fewer per value;
+//           the row records' |Xs|^2 must then be scaled by 128/ln2, TileParams::rec128)
+//   bit 23: final power of two by an integer add to the exponent field (clamped) instead
+//           of v_ldexp_f64
 //
 // Geometry: NW waves; each wave owns MT x NTW tiles of 16 x 16 (16 MT particles x 16 NTW
 // columns), so a workgroup covers PT = 16 MT particles x NB = 16 NTW NW columns.  K* costs
@@ -232,7 +335,13 @@ __device__ __forceinline__ void static_for(F&& f) {
 template <int DI, bool DYN, int VAR = 0, int NW = 4, int MT = 4, int NTW = 4>
 __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
   static_assert(MT == 1 || MT == 2 || MT == 4, "MT");
-  static_assert(NTW == 4 || NTW == 8, "NTW");
+  static_assert(NTW == 4 || NTW == 8 || NTW == 16, "NTW");
+  // B fragments in flight: BR sub-steps (a full K-step, 4, for NTW <= 8; 2 for NTW = 16,
+  // whose full K-step of fragments would not fit next to 128 accumulator VGPRs)
+  constexpr int BR = NTW >= 16 ? 2 : 4;
+  // tiles retire in groups of RG (NTW = 16: 8 phase groups instead of 16, so the K loop has
+  // 36 phase variants rather than 136; a group runs until its last tile's diagonal)
+  constexpr int RG = NTW >= 16 ? 2 : 1;
   constexpr int NT = 64 * NW;                                // threads
   constexpr int PT = 16 * MT;                                // particles per tile
   constexpr int NB = 16 * NTW * NW;                          // columns per block
@@ -262,8 +371,20 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   __shared__ double As[ASL][kBK][LDA];
   __shared__ double RX[RXS][RPT * NT];                        // row records, then padding
   constexpr bool E256 = (VAR & 256) != 0;
-  constexpr double kScale = E256 ? kLog2eX256 : kLog2eX64;
-  __shared__ double tab[E256 ? 256 : 64];
+  constexpr bool FOLD = (VAR & 2097152) != 0;
+  constexpr bool T128 = (VAR & 4194304) != 0;
+  constexpr bool IEXP = (VAR & 8388608) != 0;
+  constexpr bool GENX = FOLD || T128 || IEXP;                 // exp2_gen path
+  constexpr int TS = T128 ? 128 : 64;                         // exp table entries (GENX)
+  constexpr double kScale = E256 ? kLog2eX256 : (T128 ? 2.0 * kLog2eX64 : kLog2eX64);
+  // exp table 2^(j/64).  Production: one shared copy (lanes reading entries j and j + 32
+  // in one lane group conflict; the conflicts cost nothing measurable).  VAR bit 18:
+  // replicated TREP times, lane l reading copy l mod TREP at double (j TREP + l mod TREP),
+  // so a ds_read_b64 lane group (32 lanes, 64 banks of 4 B) hits 32 distinct bank pairs
+  // (TREP = 32; 8-wave shapes 16 so two workgroups still fit a CU's 160 KiB).
+  constexpr int TREP = (E256 || !(VAR & 262144)) ? 1 : (NW == 4 ? 32 : 16);
+  __shared__ double tab[(E256 ? 256 : (T128 ? 128 : 64)) * TREP];
+  __shared__ double csc[FOLD ? PT : 1];                       // FOLD: per-particle factor c_p
   __shared__ double qred[NW][PT];
   // VAR bit 17: particle coordinates read from LDS in the generation instead of held in
   // VGPRs (frees 2 d VGPRs: large d on the 32-particle shapes)
@@ -288,6 +409,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   if (J >= n_j) return;
   const double* __restrict__ Xs = prm.seg[c].Xs;
   const double* __restrict__ Xsq = prm.seg[c].Xsq;
+  const double* __restrict__ Xrec = prm.seg[c].Xrec;
   const double* __restrict__ Bf = prm.seg[c].Bf;
   const int n_rows = prm.seg[c].n_rows;
   const int n_m = prm.seg[c].n_m;
@@ -296,9 +418,12 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
 
   if constexpr (E256) {
     for (int i = tid; i < 256; i += NT) tab[i] = kExp2Tab256[i];
+  } else if constexpr (T128) {
+    for (int i = tid; i < 128; i += NT) tab[i] = kExp2Tab128[i];
   } else {
-    if (tid < 64) tab[tid] = kExp2Tab[tid];
+    for (int i = tid; i < 64 * TREP; i += NT) tab[i] = kExp2Tab[i / TREP];
   }
+  const double* tabl = tab + (TREP > 1 ? (tid & 63) % TREP : 0);   // this lane's copy
 
   const int seg_begin = prm.seg_pos_begin[c];
   const int pos0 = seg_begin + (t - prm.seg_tile_start[c]) * PT;
@@ -321,6 +446,12 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     a2[j] = (2.0 * kScale) * xs;
   }
   asq *= kScale;                                           // |x / l|^2 (64 / ln 2)
+  int aint = 0;                                            // FOLD: integer part of asq
+  if constexpr (FOLD) {
+    const double af = floor(asq);
+    aint = (int)af;
+    if (g == 0) csc[m] = exp2((af - asq) / (double)TS);    // 2^(-frac / S)
+  }
   if constexpr (PLDS) {
     if (g == 0) {
 #pragma unroll
@@ -366,7 +497,28 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   // Branch-free: threads past the record count load a clamped (valid) address and store it
   // to a padding slot, so no exec-mask branch splits the K-step (the compiler otherwise
   // sinks the load into the conditional store and waits for it with vmcnt(0)).
+  // Row records [Xs_i, |Xs_i|^2 64/ln2] (RW doubles per row, padded rows included) are one
+  // contiguous array: buffer loads with a per-thread constant byte offset and a wave-uniform
+  // K-step offset, no VALU address arithmetic per K-step.
+  constexpr bool RECB = !(VAR & 524288) && !E256;
+  const __amdgpu_buffer_rsrc_t rrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(T128 ? prm.rec128 : Xrec), (short)0, 0x7fffffff, 0x00020000);
+  unsigned roff[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int idx = tid + NT * k;
+    roff[k] = (unsigned)(idx < NRV ? idx : NRV - 1) * 8u;
+  }
   auto load_rows = [&](int ks, double (&rr)[RPT]) {
+    if constexpr (RECB) {
+      typedef unsigned v2u __attribute__((ext_vector_type(2)));
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(rrsrc, roff[k], ks * (NRV * 8), 0);
+        rr[k] = __builtin_bit_cast(double, (unsigned long long)x.x | ((unsigned long long)x.y << 32));
+      }
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       int idx = tid + NT * k;
@@ -391,8 +543,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   // Branch-free generation.  The row arrays are padded to row_cap(n_rows) rows with
   // |Xs|^2 = kPadSq, so the exponent of a padding row is ~ -1e300 and its kernel value is
   // exactly 0 (v_cvt_i32_f64 saturates, ldexp underflows): no masking per value.
-  auto gen_one = [&](int ks, int s) -> double {
-    const int rb = ks & (RXS - 1);
+  auto gen_one = [&](int ks, int rb, int s) -> double {
     const int r = g + NG * s;
     const double* row = &RX[rb][r * RW];
     double x;
@@ -400,6 +551,10 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       x = -(asq + 0.5 * (ks * kBK + r));
 #pragma unroll
       for (int j = 0; j < DI; ++j) x = fma(a2[j], 0.25 * j, x);
+    } else if constexpr (FOLD) {
+      x = -row[DI];                                        // asq leaves via aint / csc
+#pragma unroll
+      for (int j = 0; j < DI; ++j) x = fma(PLDS ? PA[m][j] : a2[j], row[j], x);
     } else {
       x = -(asq + row[DI]);
 #pragma unroll
@@ -407,22 +562,24 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     }
     double val;
     if constexpr (VAR & 2) val = fma(x, 1e-3, 1.0);
+    else if constexpr (GENX) val = exp2_gen<TS, IEXP>(x, tab, aint);
     else if constexpr (E256) val = exp2_256(x, tab);
     else if constexpr ((VAR & 512) != 0) val = exp2_64m(x, tab);
+    else if constexpr (TREP > 1) val = exp2_64r<TREP>(x, tabl);
     else val = exp2_64(x, tab);
     return val;                                            // padding rows: exactly 0
   };
-  auto gen = [&](int ks, double (&v)[GV]) {
+  auto gen = [&](int ks, int rb, double (&v)[GV]) {
 #pragma unroll
-    for (int s = 0; s < GV; ++s) v[s] = gen_one(ks, s);
+    for (int s = 0; s < GV; ++s) v[s] = gen_one(ks, rb, s);
   };
   // B fragments: one register set, refilled sub-step by sub-step for the next K-step right
   // after the MFMAs that consumed it (so the prefetch needs no second set of registers).
   // The address is clamped to the wave's last K-step so no branch guards the loads.
-  auto loadB_part = [&](int ks, int kk, double (&bb)[4 * NTW]) {
+  auto loadB_part = [&](int ks, int kk, int slot, double (&bb)[BR * NTW]) {
     if constexpr (VAR & 32) {
 #pragma unroll
-      for (int q = 0; q < NTW; ++q) bb[kk * NTW + q] = bb[kk * NTW + q] * 0.999 + 1e-3 * (ks & 1);
+      for (int q = 0; q < NTW; ++q) bb[slot * NTW + q] = bb[slot * NTW + q] * 0.999 + 1e-3 * (ks & 1);
       return;
     }
     const int kc = ks < ks_last ? ks : ks_last;
@@ -431,8 +588,8 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
 #pragma unroll
       for (int h = 0; h < NTW / 2; ++h) {
         const double2 x = *reinterpret_cast<const double2*>(src + 128 * h);
-        bb[kk * NTW + 2 * h + 0] = x.x;
-        bb[kk * NTW + 2 * h + 1] = x.y;
+        bb[slot * NTW + 2 * h + 0] = x.x;
+        bb[slot * NTW + 2 * h + 1] = x.y;
       }
       return;
     }
@@ -441,8 +598,8 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       typedef unsigned v4u __attribute__((ext_vector_type(4)));
       const int soff = (kc * FS + kk * (64 * NTW) + 128 * h) * 8;     // bytes, wave-uniform
       const v4u x = __builtin_amdgcn_raw_buffer_load_b128(brsrc, lane_off, soff, 0);
-      bb[kk * NTW + 2 * h + 0] = __builtin_bit_cast(double, (unsigned long long)x.x | ((unsigned long long)x.y << 32));
-      bb[kk * NTW + 2 * h + 1] = __builtin_bit_cast(double, (unsigned long long)x.z | ((unsigned long long)x.w << 32));
+      bb[slot * NTW + 2 * h + 0] = __builtin_bit_cast(double, (unsigned long long)x.x | ((unsigned long long)x.y << 32));
+      bb[slot * NTW + 2 * h + 1] = __builtin_bit_cast(double, (unsigned long long)x.z | ((unsigned long long)x.w << 32));
     }
   };
   auto store = [&](int buf, const double (&v)[GV]) {
@@ -465,14 +622,24 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   // MFMA/VALU interleave with sched_group_barrier so the generation's dependent chain
   // hides under the MFMA pipe.
   constexpr bool SPLIT = (VAR & (4096 | 8192)) != 0;
-  auto full_step = [&](auto t0c, auto t1c, int ks, double (&bb)[4 * NTW]) {
-    constexpr int T0 = decltype(t0c)::value, T1c = decltype(t1c)::value;
-    const int buf = ks & (ASL - 1);
+  // Static ring slots: with the default rings (ASL = RXS = 4) every slot a K-step touches is
+  // a function of ks & 3, so the K loop runs four K-steps per iteration with compile-time
+  // slots (SL = 0..3): LDS addresses are a constant per-lane base plus instruction
+  // immediates, no VALU address arithmetic.  Steps before the first multiple of 4 and
+  // after the last one use run-time slots (SL = -1).
+  constexpr bool STATIC = SB == 2 && ASL == 4 && RXS == 4 && (VAR & 1048576) != 0;
+  auto full_step = [&](auto t0c, auto t1c, auto slotc, int ks, double (&bb)[BR * NTW]) {
+    constexpr int T0 = decltype(t0c)::value, T1c = decltype(t1c)::value, SL = decltype(slotc)::value;
+    constexpr bool ST = SL >= 0;
+    const int buf = ST ? SL : (ks & (ASL - 1));
+    const int gslot = ST ? ((SL + LOOK) & (ASL - 1)) : ((ks + LOOK) & (ASL - 1));
+    const int rslot = ST ? ((SL + RA) & (RXS - 1)) : ((ks + RA) & (RXS - 1));
+    const int grb = ST ? ((SL + LOOK) & (RXS - 1)) : ((ks + LOOK) & (RXS - 1));
     double v[GV];
     double rr[RPT];
     if constexpr (!(VAR & 16)) {
       load_rows(ks + RA, rr);
-      if constexpr (!SPLIT) gen(ks + LOOK, v);
+      if constexpr (!SPLIT) gen(ks + LOOK, grb, v);
     }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
@@ -486,13 +653,13 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int nt = T0; nt < T1c; ++nt)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bb[kk * NTW + nt], acc[mt][nt], 0, 0, 0);
+          acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bb[(kk % BR) * NTW + nt], acc[mt][nt], 0, 0, 0);
       if constexpr (SPLIT && !(VAR & 16)) {
         constexpr int PER = 4 / GV > 0 ? 4 / GV : 1;
         if (kk % PER == 0) {
 #pragma unroll
           for (int s = 0; s < GV; ++s)
-            if (s == kk / PER) v[s] = gen_one(ks + LOOK, s);
+            if (s == kk / PER) v[s] = gen_one(ks + LOOK, grb, s);
         }
       }
       if constexpr ((VAR & 4096) != 0) {
@@ -503,21 +670,39 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
           __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // 2 VALU
         }
       }
-      loadB_part(ks + 1, kk, bb);
+      loadB_part(ks + (kk + BR) / 4, (kk + BR) % 4, kk % BR, bb);   // sub-step kk + BR
     }
     if constexpr (!(VAR & 16)) {
-      store((ks + LOOK) & (ASL - 1), v);
-      store_rows((ks + RA) & (RXS - 1), rr);
+      store(gslot, v);
+      store_rows(rslot, rr);
     }
     if constexpr (!(VAR & 8)) {
-      if (ks % SB == SB - 1) __syncthreads();
+      if constexpr (ST) {
+        if constexpr (SL % SB == SB - 1) __syncthreads();
+      } else {
+        if (ks % SB == SB - 1) __syncthreads();
+      }
     }
   };
+  // K-steps [ks, e) with tiles [T0, T1) active
+  auto run_steps = [&](auto t0c, auto t1c, int& ks, const int e, double (&bb)[BR * NTW]) {
+    using RT = std::integral_constant<int, -1>;
+    if constexpr (STATIC) {
+      for (; ks < e && (ks & 3); ++ks) full_step(t0c, t1c, RT{}, ks, bb);
+      for (; ks + 4 <= e; ks += 4) {
+        full_step(t0c, t1c, std::integral_constant<int, 0>{}, ks, bb);
+        full_step(t0c, t1c, std::integral_constant<int, 1>{}, ks + 1, bb);
+        full_step(t0c, t1c, std::integral_constant<int, 2>{}, ks + 2, bb);
+        full_step(t0c, t1c, std::integral_constant<int, 3>{}, ks + 3, bb);
+      }
+    }
+    for (; ks < e; ++ks) full_step(t0c, t1c, RT{}, ks, bb);
+  };
 
-  double bb[4 * NTW];
+  double bb[BR * NTW];
   if constexpr (VAR & 32) {
 #pragma unroll
-    for (int q = 0; q < 4 * NTW; ++q) bb[q] = 1e-3 * q + lane;
+    for (int q = 0; q < BR * NTW; ++q) bb[q] = 1e-3 * q + lane;
   }
   {
     double rr[RPT];
@@ -532,11 +717,11 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     double v[GV];
 #pragma unroll
     for (int j = 0; j < LOOK; ++j) {
-      gen(j, v);
+      gen(j, j & (RXS - 1), v);
       store(j, v);
     }
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) loadB_part(0, kk, bb);
+    for (int kk = 0; kk < BR; ++kk) loadB_part(0, kk, kk, bb);
   }
   // Drain the prologue's loads (vmcnt(0)) so that the K loop's entry carries no pending
   // loads: otherwise the waitcnt pass merges the prologue's issue order into the loop
@@ -546,13 +731,15 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
 
   int ks = 0;
   // K-steps [ks, kend[T0]) with tiles [T0, T1) active, for T0 = 0 .. T1-1
-  static_for<1, NTW + 1>([&](auto t1c) {
-    constexpr int T1c = decltype(t1c)::value;
-    if (T1 == T1c) {
-      static_for<0, T1c>([&](auto t0c) {
-        constexpr int T0 = decltype(t0c)::value;
-        const int e = kend[T0];
-        for (; ks < e; ++ks) full_step(t0c, t1c, ks, bb);
+  // (groups of RG tiles: phase T0 = g0 RG runs until the group's last tile retires)
+  static_for<1, NTW / RG + 1>([&](auto g1c) {
+    constexpr int T1c = decltype(g1c)::value * RG;
+    if ((T1 + RG - 1) / RG * RG == T1c) {
+      static_for<0, T1c / RG>([&](auto g0c) {
+        constexpr int T0 = decltype(g0c)::value * RG;
+        int e = kend[T0];
+        if constexpr (RG == 2) e = max(e, kend[T0 + 1]);
+        run_steps(std::integral_constant<int, T0>{}, std::integral_constant<int, T1c>{}, ks, e, bb);
       });
     }
   });
@@ -561,12 +748,29 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     double v[GV];
     double rr[RPT];
     load_rows(ks + RA, rr);
-    gen(ks + LOOK, v);
+    gen(ks + LOOK, (ks + LOOK) & (RXS - 1), v);
     store((ks + LOOK) & (ASL - 1), v);
     store_rows((ks + RA) & (RXS - 1), rr);
     if (ks % SB == SB - 1) __syncthreads();
   }
 
+  // FOLD: rows of V = K* B carry the per-particle factor c_p (row (l >> 4) + 4 r of tile mt)
+  double cfold[MT][4];
+  if constexpr (FOLD) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cfold[mt][r] = csc[mt * 16 + (lane >> 4) + 4 * r];
+    if constexpr (DYN) {                                   // before the linear-kernel share
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NTW; ++nt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[mt][nt][r] *= cfold[mt][r];
+    }
+  }
+  constexpr bool OFOLD = FOLD && !DYN;                     // obs: scale q and mean uses only
   if constexpr (DYN) {
     // Linear-kernel share: acc += X~ H for this block.  A fragment: lane l holds
     // x~[particle mt*16 + (l&15)][4 kh + (l>>4)]; B fragment: Hf[J][kh][w][l][nt].
@@ -615,7 +819,8 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int p = pos0 + mt * 16 + lk + 4 * r;
-              if (p < pos_end) prm.mu[(long long)(out_base + p) * prm.ld_mu + jm] = acc[mt][nt][r];
+              if (p < pos_end)
+                prm.mu[(long long)(out_base + p) * prm.ld_mu + jm] = OFOLD ? cfold[mt][r] * acc[mt][nt][r] : acc[mt][nt][r];
             }
         }
       }
@@ -641,7 +846,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
             for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const double t = zj - acc[mt][nt][r];
+                const double t = OFOLD ? fma(-cfold[mt][r], acc[mt][nt][r], zj) : zj - acc[mt][nt][r];
                 ss[mt][r] = fma(t * t, lam, ss[mt][r]);
               }
           } else {
@@ -651,7 +856,8 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
               for (int r = 0; r < 4; ++r) {
                 int p = pos0 + mt * 16 + lk + 4 * r;
                 p = p < pos_end ? p : pos0;
-                const double t = prm.z[(long long)(p / Pf) * n_m + jm] - acc[mt][nt][r];
+                const double zz = prm.z[(long long)(p / Pf) * n_m + jm];
+                const double t = OFOLD ? fma(-cfold[mt][r], acc[mt][nt][r], zz) : zz - acc[mt][nt][r];
                 ss[mt][r] = fma(t * t, lam, ss[mt][r]);
               }
           }
@@ -694,6 +900,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
         v += __shfl_xor(v, 2);
         v += __shfl_xor(v, 4);
         v += __shfl_xor(v, 8);
+        if constexpr (OFOLD) v *= cfold[mt][r] * cfold[mt][r];
         qs[mt][r] = v;
       }
     if (li == 0) {

@@ -72,19 +72,20 @@ struct ImagePacker {
     return j < n_m ? M[row * n_m + j] : 0.0;
   }
 
-  // Xs = X / ls (padded to row_cap rows with 0) and |Xs|^2 * 64/ln2 (padding: kPadSq).
-  void inputs(std::vector<double>& xs, std::vector<double>& xsq) const {
-    const int cap = row_cap(n_rows);
-    xs.assign((size_t)cap * d, 0.0);
-    xsq.assign((size_t)cap, kPadSq);
+  // Row records [Xs_i, |Xs_i|^2 * 64/ln2], Xs = X / ls: (d + 1) doubles per row, padded to
+  // row_cap(n_rows) rows with Xs = 0 and |Xs|^2 = kPadSq (kernel value exactly 0).
+  void records(std::vector<double>& rec) const {
+    const int cap = row_cap(n_rows), rw = d + 1;
+    rec.assign((size_t)cap * rw, 0.0);
+    for (int i = n_rows; i < cap; ++i) rec[(size_t)i * rw + d] = kPadSq;
     for (long long i = 0; i < n_rows; ++i) {
       double s = 0.0;
       for (int j = 0; j < d; ++j) {
         const double v = X[i * d + j] / ls[j];
-        xs[i * d + j] = v;
+        rec[i * rw + j] = v;
         s += v * v;
       }
-      xsq[i] = s * kLog2eX64;
+      rec[i * rw + d] = s * kLog2eX64;
     }
   }
 

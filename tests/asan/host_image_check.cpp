@@ -65,10 +65,15 @@ static void check_packing(int n_rows, int n_m, int d, TileGeo geo, bool lin) {
              it == seen.end() ? 0 : it->second);
     }
   EXPECT((long long)seen.size() == expected, "%zu distinct values stored, %lld expected", seen.size(), expected);
-  std::vector<double> xs, xsq;
-  pk.inputs(xs, xsq);
-  EXPECT((int)xsq.size() == row_cap(n_rows) && xs.size() == xsq.size() * d, "input sizes");
-  for (int i = n_rows; i < (int)xsq.size(); ++i) EXPECT(xsq[i] == kPadSq, "pad row %d", i);
+  std::vector<double> rec;
+  pk.records(rec);
+  EXPECT(rec.size() == (size_t)row_cap(n_rows) * (d + 1), "record size");
+  for (int i = n_rows; i < row_cap(n_rows); ++i) EXPECT(rec[(size_t)i * (d + 1) + d] == kPadSq, "pad row %d", i);
+  for (int i = 0; i < n_rows; ++i) {
+    double s2 = 0.0;
+    for (int j = 0; j < d; ++j) s2 += (X[(size_t)i * d + j] / ls[j]) * (X[(size_t)i * d + j] / ls[j]);
+    EXPECT(std::fabs(rec[(size_t)i * (d + 1) + d] - s2 * kLog2eX64) <= 1e-12 * (1.0 + s2 * kLog2eX64), "row %d", i);
+  }
   if (lin) {
     std::vector<double> hf;
     pk.linear(hf);

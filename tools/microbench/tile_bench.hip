@@ -36,7 +36,17 @@ int main(int argc, char** argv) {
     hXsq[i] = s;
   }
   for (auto& v : hX) v = 2.0 * nd(rng);
-  double *Xs, *Xsq, *X, *q, *mu;
+  std::vector<double> hRec((size_t)cap * (d + 1));
+  for (int i = 0; i < cap; ++i) {
+    for (int j = 0; j < d; ++j) hRec[(size_t)i * (d + 1) + j] = hXs[(size_t)i * d + j];
+    hRec[(size_t)i * (d + 1) + d] = hXsq[i];
+  }
+  double *Xs, *Xsq, *Xrec, *Xrec128, *X, *q, *mu;
+  CK(hipMalloc(&Xrec, hRec.size() * 8));
+  CK(hipMemcpy(Xrec, hRec.data(), hRec.size() * 8, hipMemcpyHostToDevice));
+  for (int i = 0; i < cap; ++i) hRec[(size_t)i * (d + 1) + d] *= 2.0;   // |Xs|^2 x 128/ln2 (VAR bit 22)
+  CK(hipMalloc(&Xrec128, hRec.size() * 8));
+  CK(hipMemcpy(Xrec128, hRec.data(), hRec.size() * 8, hipMemcpyHostToDevice));
   CK(hipMalloc(&Xs, cap * d * 8)); CK(hipMalloc(&Xsq, cap * 8));
   CK(hipMalloc(&X, (size_t)P * d * 8)); CK(hipMalloc(&q, (size_t)P * (N + D + 4095) / 256 * 8)); CK(hipMalloc(&mu, (size_t)P * D * 8));
     CK(hipMemcpy(Xs, hXs.data(), cap * d * 8, hipMemcpyHostToDevice));
@@ -44,7 +54,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(X, hX.data(), (size_t)P * d * 8, hipMemcpyHostToDevice));
   // geometries: {waves, particle tiles MT, column tiles per wave NTW}
   struct Geo { int nw, mt, ntw; };
-  const Geo geos[] = {{4, 4, 4}, {8, 4, 4}, {4, 2, 8}};
+  const Geo geos[] = {{4, 4, 4}, {8, 4, 4}, {4, 2, 8}, {4, 1, 16}};
   const int NGEO = sizeof(geos) / sizeof(geos[0]);
   TileParams pp[NGEO];
   int* tabs;
@@ -65,7 +75,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(B, hB.data(), total * 8, hipMemcpyHostToDevice));
     TileParams& p = pp[v];
     p = TileParams{};
-    p.seg[0].Xs = Xs; p.seg[0].Xsq = Xsq; p.seg[0].Bf = B;
+    p.seg[0].Xs = Xs; p.seg[0].Xsq = Xsq; p.seg[0].Xrec = Xrec; p.seg[0].Bf = B;
+    p.rec128 = Xrec128;
     p.seg[0].n_rows = N; p.seg[0].n_m = D; p.seg[0].n_j = n_j; p.seg[0].coff = coff;
     p.n_seg = 1; p.tiles_ub = ntiles; p.n_j_max = n_j; p.geo = TileGeo{nw, geos[v].mt, geos[v].ntw};
     int* tab = tabs + 8 * v;
@@ -85,8 +96,12 @@ int main(int argc, char** argv) {
               {launch_var<0, 4, 2, 8>, 2, "32x512 (VGPR coords)"}, {launch_var<131072, 4, 2, 8>, 2, "32x512 LDS coords"},
               {launch_var<131072, 8>, 1, "64x512 LDS coords"}};
 #else
-  V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512"}, {launch_var<131072, 4, 2, 8>, 2, "32x512 LDS coords"},
-              {launch_var<0, 4>, 0, "64x256"}};
+  V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512 production"},
+              {launch_var<4194304, 4, 2, 8>, 2, "32x512 T128"},
+              {launch_var<0, 4, 1, 16>, 3, "16x1024"},
+              {launch_var<4194304, 4, 1, 16>, 3, "16x1024 T128"},
+              {launch_var<16, 4, 1, 16>, 3, "16x1024 no gen"},
+              {launch_var<16, 4, 2, 8>, 2, "32x512 no gen"}};
 #endif
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
   std::vector<std::vector<float>> t(NV);
