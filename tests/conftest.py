@@ -92,7 +92,7 @@ def fx_stress():
     return load_fixture("stress_n500_sigma001")
 
 
-def assert_step_matches(post, r, gpu_post, gpu_mean, u, resample="multinomial", what=""):
+def assert_step_matches(post, r, gpu_post, gpu_mean, u, resample="multinomial", what="", w_tol=1e-5):
     """A GPU filter step (``post`` = export after it, read-outs ``gpu_post``/``gpu_mean``)
     against the oracle's step ``r`` from the same pre-step particles and draws.
 
@@ -106,7 +106,7 @@ def assert_step_matches(post, r, gpu_post, gpu_mean, u, resample="multinomial", 
     difference moves ~P^2 x 1e-12 / 2 slots across a boundary.)"""
     from oracle import gpmdm_oracle as O
     idx = post["resample_idx"]
-    assert nrel(post["w"], r.w) < 1e-5, (what, nrel(post["w"], r.w))
+    assert nrel(post["w"], r.w) < w_tol, (what, nrel(post["w"], r.w))
     if resample == "multinomial":
         ref_idx = O.multinomial_resample_indices(post["w"], u)
     else:

@@ -16,7 +16,8 @@ gpmdm.py:923-963, 1032-1068; gpmdm_pf.py:137-262):
 
 * predictive maps at 500 query points: means 1e-8, variances 1e-6 normwise;
 * one resynced filter step at P = 2000 with explicit draws (update_with_draws): switched
-  classes exact, then ``conftest.assert_step_matches`` (weights 1e-5, resample indices of
+  classes exact, then ``conftest.assert_step_matches`` (weights 1e-4 -- see the test --,
+  resample indices of
   the GPU's weights exact up to 2 CDF ties, states 1e-6, posterior 1e-6 abs, mean 1e-6);
 * configs[3]: 8 logical shards of P = 10^6 on one GPU, bitwise equal to one rank.
 """
@@ -85,8 +86,12 @@ def test_large_config_maps_and_step_vs_oracle(cfg):
     r = O.step(om, T, st0["states"], st0["classes"], zs[2], E, nrm, u)
     st = pf.export_state()
     assert np.array_equal(cls1, r.classes_switched)
+    # weights 1e-4: at N = 10^4 / 2 x 10^4 the variance 1 - k^T K^-1 k (cond(K_y) ~ 1e6, vc ~
+    # 1e-2) carries ~1e-8 relative rounding in any fp64 evaluation, the log-likelihood
+    # (|ll| ~ 500) ~1e-5 absolute, so the normalised weights differ at ~1e-5 between two
+    # correct fp64 evaluations (measured 0.3-1.6e-5 GPU vs oracle across boxes)
     assert_step_matches(st, r, pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), u,
-                        what=f"config {cfg}")
+                        what=f"config {cfg}", w_tol=1e-4)
     assert all(v == 0 for v in pf.health().values())
 
 

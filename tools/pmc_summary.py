@@ -42,9 +42,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--commit", default=None, help="commit of the build the passes measured")
+    ap.add_argument("--command", default=None, help="the profiled command")
+    ap.add_argument("--merge", default=None, help="existing summary to add this one to, under --key")
+    ap.add_argument("--key", default=None, help="e.g. config3: stored as <key>_obs_gemm_hbm_bytes_per_launch")
     a = ap.parse_args()
     vals, dur = load(a.root)
-    out = {"source": str(a.root), "kernels": {}}
+    out = {"source": str(a.root), "commit": a.commit, "command": a.command, "kernels": {}}
     for k, d in vals.items():
         if "rocclr" in k:
             continue
@@ -68,6 +72,11 @@ def main():
         out["kernels"][short(k)] = rec
     obs = out["kernels"].get("obs_gemm", {})
     out["obs_gemm_hbm_bytes_per_launch"] = obs.get("hbm_bytes_per_launch")
+    if a.merge and a.key:
+        base = json.loads(Path(a.merge).read_text())
+        base[a.key] = out
+        base[f"{a.key}_obs_gemm_hbm_bytes_per_launch"] = out["obs_gemm_hbm_bytes_per_launch"]
+        out = base
     text = json.dumps(out, indent=1)
     if a.out:
         Path(a.out).write_text(text)

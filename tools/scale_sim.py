@@ -13,7 +13,24 @@ collective itself is missing, so the result is the compute floor of each rank's 
 in-process (the data every rank sees is exactly what an N-GPU run sees), and reports each
 rank's GPU time per step from its stage events (kernels only, no host gaps) and its
 dynamics-GP rows; the slowest rank bounds the N-GPU step.
+
+The RCCL all-gather is modelled, not measured (one GPU here): every rank receives the
+(N-1)/N share of P_total x (d+2) doubles.  Two bounds per N: a ring on one xGMI link per
+GPU (153 GB/s) and the ring's chunks spread over min(N-1, 7) links (RCCL's channels use
+distinct links on the fully connected 8-GPU node).  The modelled step adds the all-gather
+to the slowest rank's compute (no overlap) -- the weak-scaling figure the N-GPU bench would
+show with the collective on the critical path.
 """
+
+XGMI_LINK_GBPS = 153.0
+
+
+def allgather_ms(P_total, width, n):
+    """(one-link ring, multi-link) all-gather time in ms for P_total rows of `width` doubles."""
+    if n == 1:
+        return 0.0, 0.0
+    recv = (n - 1) / n * P_total * width * 8.0
+    return recv / (XGMI_LINK_GBPS * 1e9) * 1e3, recv / (XGMI_LINK_GBPS * 1e9 * min(n - 1, 7)) * 1e3
 import sys
 import time
 from pathlib import Path
@@ -113,10 +130,14 @@ def ranks_mode():
             per.append({k: v[0] / max(v[1], 1) for k, v in st.items()})
         tot = [sum(p.values()) for p in per]
         worst = max(range(n), key=lambda r: tot[r])
+        ag1, agm = allgather_ms(P, model.d + 2, n)
         print(f"[shard_order={order}] N={n}: P_total={P}, GPU ms per step per rank: max {max(tot):.3f} min {min(tot):.3f} "
               f"(rank {worst}: dyn_gemm {per[worst]['dyn_gemm']:.3f} obs_gemm {per[worst]['obs_gemm']:.3f} "
               f"switch {per[worst]['switch']:.3f} resample {per[worst]['resample']:.3f}); "
-              f"dyn rows per rank (mean over steps): {[r // steps for r in rows]}", flush=True)
+              f"dyn rows per rank (mean over steps): {[r // steps for r in rows]}; "
+              f"modelled all-gather {ag1:.3f} ms (1 link) / {agm:.3f} ms ({min(max(n - 1, 1), 7)} links) -> "
+              f"step {max(tot) + ag1:.3f} / {max(tot) + agm:.3f} ms, "
+              f"{P * 1e3 / (max(tot) + ag1):.3e} / {P * 1e3 / (max(tot) + agm):.3e} particle-steps/s", flush=True)
         del pfs
 
 
