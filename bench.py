@@ -95,6 +95,13 @@ def obs_kernel_flops(N, D, bk=16):
     return algorithmic, dense_form, executed
 
 
+def dyn_row_flops(model):
+    """Algorithmic FLOPs of one dynamics-GP row (triangular R_c^T k plus the mean weights),
+    averaged over the classes."""
+    rows = model._class_dynamics_rows()
+    return sum(n * (n + 1.0) + 2.0 * n * model.d for n in rows) / len(rows)
+
+
 def obs_model_bytes(N, D):
     """Algorithmic model bytes of the observation GP: the non-zeros of triu(R) and K^-1 Y."""
     return 8.0 * (N * (N + 1) / 2 + N * D)
@@ -332,8 +339,11 @@ def main():
         "stages_ms_per_step": {k: v[0] / max(v[1], 1) for k, v in breakdown.items()},
         "nodedup": {"ms_per_step": el_nd / n_nd * 1e3, "value": P_total * n_nd / el_nd, "steps": n_nd,
                     "stages_ms_per_step": {k: v[0] / max(v[1], 1) for k, v in nd_stages.items()},
-                    "note": "dedup=False: the dynamics GP runs on every particle (the reference's work); "
-                            "bitwise the same filter as the headline's"},
+                    "dyn_gemm_tflops": dyn_row_flops(model) * P_local / max(nd_stages["dyn_gemm"][0] / max(nd_stages["dyn_gemm"][1], 1), 1e-9) / 1e9,
+                    "note": "dedup=False: the dynamics GP runs on every particle (the reference's work) on "
+                            "the wide dynamics tiles; the same filter as the headline's up to summation order; "
+                            "dyn_gemm_tflops = algorithmic N_c(N_c+1) + 2 N_c d FLOP per row (class mean) / "
+                            "launch time"},
         "ess_last": ess,
         "ess_frac_last": ess / P_total,
         "posterior_last": [float(x) for x in post],

@@ -22,6 +22,7 @@ GPMDM_RNG_REPLAY = 0
 GPMDM_RNG_PHILOX = 1
 GPMDM_RESAMPLE_MULTINOMIAL = 0
 GPMDM_RESAMPLE_SYSTEMATIC = 1
+DYN_TILES = {"auto": 0, "narrow": 1, "wide": 2}
 STAGES = ("switch", "dyn_gemm", "dyn_finish", "obs_gemm", "obs_finish", "resample")
 HEALTH = ("obs_var_nonpositive", "obs_ll_nonfinite", "dyn_var_nonpositive", "dyn_state_nonfinite")
 
@@ -63,6 +64,7 @@ _SIGS = {
     "gpmdm_pf_stage_times": (c_int, [c_void_p, _dp, _i64p]),
     "gpmdm_pf_set_dedup": (c_int, [c_void_p, c_int]),
     "gpmdm_pf_set_shard_order": (c_int, [c_void_p, c_int]),
+    "gpmdm_pf_set_dyn_tiles": (c_int, [c_void_p, c_int]),
     "gpmdm_pf_timing_stages": (c_int, [c_void_p, ctypes.c_uint]),
     "gpmdm_pf_dyn_rows": (c_int, [c_void_p, _i64p, c_void_p]),
     "gpmdm_pf_frame": (c_int, [c_void_p, _i64p]),

@@ -33,7 +33,7 @@ from .model import GPMDM
 class GPMDM_PF_Bank:
     def __init__(self, gpmdm: GPMDM, markov_switching_model, num_filters: int, num_particles: int, *,
                  seed=None, resample: str = "multinomial", process_group=None, shard=None,
-                 dedup: bool = True):
+                 dedup: bool = True, dyn_tiles: str = "auto"):
         self._gpmdm = gpmdm
         self._gpmdm.set_evaluation_mode()
         self._T = torch.as_tensor(markov_switching_model).type(torch.float64)
@@ -76,6 +76,9 @@ class GPMDM_PF_Bank:
             self._h = h
             self._model_gen = gpmdm.generation
             _lib.check(_lib.load().gpmdm_pf_set_dedup(h, 1 if dedup else 0), "dedup")
+            if dyn_tiles not in _lib.DYN_TILES:
+                raise ValueError("dyn_tiles must be 'auto', 'narrow' or 'wide'")
+            _lib.check(_lib.load().gpmdm_pf_set_dyn_tiles(h, _lib.DYN_TILES[dyn_tiles]), "dyn_tiles")
             self._init_particles()
 
     def __del__(self):

@@ -29,6 +29,10 @@ static_assert(kMaxClassesDesc == kMaxClasses, "descriptor check and kernels agre
 
 namespace {
 
+// Rows from which a dynamics-GP predictive map uses the wide tile image (a throughput
+// problem; below, the narrow tiles' shorter K loops win)
+constexpr long long kWideRows = 4096;
+
 // One GP's device image: scaled inputs (+ squared norms) and B = [R | M] (+ H for the
 // dynamics GPs) in MFMA-fragment order -- layout and packing in host_image.h.
 struct GpImage {
@@ -106,7 +110,16 @@ struct gpmdm_model {
   std::vector<double> X;              // host copy, N x d
   std::vector<double> y_ls, x_ls, x_lin_c2, x_il2, y_il2;
   GpImage obs;
-  std::vector<GpImage> dyn;
+  std::vector<GpImage> dyn;           // narrow tiles (16x256): de-duplicated rows, small maps
+  std::vector<GpImage> dynw;          // wide tiles (the observation GP's shape): every particle
+                                      // (dedup off, predict), large maps; empty = same as dyn
+  const std::vector<GpImage>& dyn_set(bool wide) const { return wide && !dynw.empty() ? dynw : dyn; }
+  int dyn_parts_max() const {
+    int mx = 0;
+    for (auto& g : dyn) mx = std::max(mx, g.n_parts());
+    for (auto& g : dynw) mx = std::max(mx, g.n_parts());
+    return mx;
+  }
   double* y_il2_dev = nullptr;
   double* y_lam2_dev = nullptr;   // 1 / il2 = exp(y_log_lambdas)^2
   double sum_log_il2 = 0.0;
@@ -118,6 +131,7 @@ struct gpmdm_model {
   ~gpmdm_model() {
     obs.release();
     for (auto& g : dyn) g.release();
+    for (auto& g : dynw) g.release();
     dfree(y_il2_dev);
     dfree(y_lam2_dev);
     dfree(tab);
@@ -145,6 +159,8 @@ struct gpmdm_pf {
   unsigned seed_lo = 0, seed_hi = 0, frame = 0;
   bool initialised = false, switched = false, propagated = false;
   bool dedup = true;                  // ancestor de-duplication of the dynamics GP
+  int dyn_tiles = GPMDM_DYN_TILES_AUTO;   // gpmdm_pf_set_dyn_tiles
+  bool wide_dyn() const { return dyn_tiles == GPMDM_DYN_TILES_WIDE || (dyn_tiles == GPMDM_DYN_TILES_AUTO && !dedup); }
   // device state
   double *T = nullptr, *X = nullptr, *X_prop = nullptr, *ll = nullptr;
   int *cls = nullptr, *cls_new = nullptr, *perm = nullptr, *ridx = nullptr;
@@ -274,12 +290,17 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
   // others there: config 5, d = 16, 0.79 of FP64 peak vs 0.70 for 64x256).  The dynamics
   // GPs run few rows (ancestor de-duplication) against short triangular blocks: their time
   // is the K loop of the heaviest blocks, which narrow particle tiles shorten (64 -> 32 ->
-  // 16 particles: dyn GEMM 0.215 -> 0.163 -> 0.150 ms per step at config 2).
+  // 16 particles: dyn GEMM 0.215 -> 0.163 -> 0.150 ms per step at config 2).  Evaluating
+  // every particle (de-duplication off, GPMDM_PF.predict, large predictive maps) is a
+  // throughput problem like the observation GP's, so the dynamics GPs get a second image in
+  // the observation GP's shape (half the kernel-value generation per MFMA of 16x256 and
+  // 40% fewer generated rows; config 2, 100k rows: see DESIGN.md §3).
   TileGeo obs_geo = d <= 12 ? kGeo32x512 : kGeo64x512, dyn_geo = kGeo16x256;
+  TileGeo dynw_geo = obs_geo;
   switch (desc->tile_shape) {
     case GPMDM_TILE_DEFAULT: break;
-    case GPMDM_TILE_64x256: obs_geo = dyn_geo = kGeo64x256; break;
-    case GPMDM_TILE_64x512: obs_geo = dyn_geo = kGeo64x512; break;
+    case GPMDM_TILE_64x256: obs_geo = dyn_geo = dynw_geo = kGeo64x256; break;
+    case GPMDM_TILE_64x512: obs_geo = dyn_geo = dynw_geo = kGeo64x512; break;
     case GPMDM_TILE_32x512: obs_geo = kGeo32x512; break;
     default: break;   // rejected by check_model_desc
   }
@@ -287,11 +308,18 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
                        desc->obs_R, desc->obs_beta, obs_geo);
   if (rc) { delete m; return rc; }
   m->dyn.resize(m->C);
+  const bool two = dynw_geo.nw != dyn_geo.nw || dynw_geo.mt != dyn_geo.mt || dynw_geo.ntw != dyn_geo.ntw;
+  if (two) m->dynw.resize(m->C);
   for (int c = 0; c < m->C; ++c) {
     rc = build_image(m->dyn[c], (int)desc->Nc[c], d, d, desc->Xin[c], desc->x_lengthscales,
                      m->x_lin_c2.data(),
                      desc->dyn_R[c], desc->dyn_alpha[c], dyn_geo);
     if (rc) { delete m; return rc; }
+    if (two) {
+      rc = build_image(m->dynw[c], (int)desc->Nc[c], d, d, desc->Xin[c], desc->x_lengthscales,
+                       m->x_lin_c2.data(), desc->dyn_R[c], desc->dyn_alpha[c], dynw_geo);
+      if (rc) { delete m; return rc; }
+    }
   }
   rc = dalloc(&m->y_il2_dev, m->D);
   if (rc) { delete m; return rc; }
@@ -381,7 +409,7 @@ int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, doubl
   CHECK(Xs && mu && var, "null buffer");
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipSetDevice(m->device));
-  const GpImage& g = m->dyn[c];
+  const GpImage& g = m->dyn_set(n >= kWideRows)[c];
   const int nparts = g.n_parts();
   TRY(m->ensure_q((size_t)nparts * n));
   const int tab[5] = {0, (int)n, 0, 0, g.tiles(n)};
@@ -453,8 +481,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   pf->nb = (int)cdiv(P, 256);
   pf->nbf = (int)cdiv(Pf, 256);
   const int C = m->C, d = m->d, D = m->D;
-  int maxparts = 0;
-  for (auto& g : m->dyn) maxparts = std::max(maxparts, g.n_parts());
+  const int maxparts = m->dyn_parts_max();
   pf->nparts_dyn_max = maxparts;
   const long long nl = std::max(pf->nloc, 1ll);
   int rc = 0;
@@ -673,7 +700,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   ScanArgs sc{};
   sc.nb = nbs;
   sc.C = C;
-  sc.pt = m->dyn[0].geo.pt();
+  sc.pt = m->dyn_set(pf->wide_dyn())[0].geo.pt();   // tile unit of the dynamics pass
   sc.lo = sl ? 0 : pf->lo;
   sc.hi = sl ? pf->nloc : pf->hi;
   sc.own = pf->own_order();
@@ -708,7 +735,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
     la.npos = nsw;
     la.nb = nbs;
     la.C = C;
-    la.pt = m->dyn[0].geo.pt();
+    la.pt = m->dyn_set(pf->wide_dyn())[0].geo.pt();
     la.perm = pf->perm;
     la.cls_new = pf->cls_new;
     la.anc = pf->ridx;
@@ -759,6 +786,8 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
   const long long nl = pf->nloc;
   if (nl > 0) {
     // ---- dynamics GP per class (segments of at most kMaxSeg classes per launch) ----
+    // narrow tiles for the de-duplicated rows, the wide image when every particle is evaluated
+    const std::vector<GpImage>& dset = m->dyn_set(pf->wide_dyn());
     hipEvent_t t0;
     pf->mark_begin(s, GPMDM_STAGE_DYN_GEMM, t0);
     for (int c0 = 0; c0 < C; c0 += kMaxSeg) {
@@ -766,11 +795,11 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
       TileParams tp{};
       int njm = 0;
       for (int k = 0; k < ns; ++k) {
-        tp.seg[k] = m->dyn[c0 + k].seg();
-        njm = std::max(njm, m->dyn[c0 + k].n_j);
+        tp.seg[k] = dset[c0 + k].seg();
+        njm = std::max(njm, dset[c0 + k].n_j);
       }
       tp.n_seg = ns;
-      tp.geo = m->dyn[c0].geo;           // tile starts computed on the device in units of pt
+      tp.geo = dset[c0].geo;           // tile starts computed on the device in units of pt
       tp.tiles_ub = (int)(cdiv(nl, tp.geo.pt()) + ns);
       tp.n_j_max = njm;
       if (pf->dedup) {                  // one row per (ancestor, class) leader
@@ -807,7 +836,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     fa.seg_out_base = pf->seg_out();
     fa.seg_pos_begin = pf->seg_begin();
     fa.perm = pf->perm;
-    for (int c = 0; c < C; ++c) fa.n_parts[c] = m->dyn[c].n_parts();
+    for (int c = 0; c < C; ++c) fa.n_parts[c] = dset[c].n_parts();
     fa.qpart = pf->qdyn;
     fa.ld_q = nl;
     fa.mu = pf->mudyn;
@@ -1023,6 +1052,15 @@ int gpmdm_pf_set_dedup(gpmdm_pf_t pf, int enable) {
   return GPMDM_OK;
 }
 
+int gpmdm_pf_set_dyn_tiles(gpmdm_pf_t pf, int mode) {
+  CHECK(pf, "null handle");
+  CHECK(mode == GPMDM_DYN_TILES_AUTO || mode == GPMDM_DYN_TILES_NARROW || mode == GPMDM_DYN_TILES_WIDE,
+        "mode must be GPMDM_DYN_TILES_*");
+  if (pf->switched) return fail(GPMDM_E_STATE, "set_dyn_tiles between switch and propagate");
+  pf->dyn_tiles = mode;
+  return GPMDM_OK;
+}
+
 int gpmdm_pf_set_shard_order(gpmdm_pf_t pf, int enable) {
   CHECK(pf, "null handle");
   if (pf->switched || pf->propagated) return fail(GPMDM_E_STATE, "set_shard_order inside a step");
@@ -1094,8 +1132,7 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
   CHECK(m->device == old->device, "the new model lives on another device");
   HIPCHK(hipSetDevice(m->device));
   // buffers shaped by the model's column blocks
-  int maxparts = 0;
-  for (auto& g : m->dyn) maxparts = std::max(maxparts, g.n_parts());
+  const int maxparts = m->dyn_parts_max();
   const long long nl = std::max(pf->nloc, 1ll);
   double *qdyn = nullptr, *qobs = nullptr, *sobs = nullptr;
   int rc = dalloc(&qdyn, (size_t)maxparts * nl);
@@ -1166,7 +1203,7 @@ int gpmdm_pf_predict(gpmdm_pf_t pf, double* mean, void* stream) {
   ScanArgs sc{};
   sc.nb = nbs;
   sc.C = C;
-  sc.pt = m->dyn[0].geo.pt();
+  sc.pt = m->dyn_set(true)[0].geo.pt();
   sc.lo = 0;
   sc.hi = P;
   sc.blockcounts = pf->blockcounts;
@@ -1194,11 +1231,11 @@ int gpmdm_pf_predict(gpmdm_pf_t pf, double* mean, void* stream) {
     TileParams tp{};
     int njm = 0;
     for (int k = 0; k < ns; ++k) {
-      tp.seg[k] = m->dyn[c0 + k].seg();
-      njm = std::max(njm, m->dyn[c0 + k].n_j);
+      tp.seg[k] = m->dyn_set(true)[c0 + k].seg();
+      njm = std::max(njm, m->dyn_set(true)[c0 + k].n_j);
     }
     tp.n_seg = ns;
-    tp.geo = m->dyn[c0].geo;
+    tp.geo = m->dyn_set(true)[c0].geo;
     tp.tiles_ub = (int)(cdiv(P, tp.geo.pt()) + ns);
     tp.n_j_max = njm;
     tp.seg_pos_begin = pf->seg_begin() + c0;

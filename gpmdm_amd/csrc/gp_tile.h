@@ -939,6 +939,8 @@ void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
   if (dyn) {
     if (g.nw == 8)
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 8>), grid, dim3(512), 0, stream, p);
+    else if (g.mt == 2 && g.ntw == 8)
+      hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 2, 8>), grid, dim3(256), 0, stream, p);
     else if (g.mt == 2)
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 2, 4>), grid, dim3(256), 0, stream, p);
     else if (g.mt == 1)

@@ -19,10 +19,14 @@ every per-frame computation runs in the HIP library.  Extra keyword options:
   staged calls); a Philox filter then needs an explicit ``seed`` (nothing to broadcast);
 * ``dedup`` (default True): evaluate the dynamics GP once per distinct (resampling
   ancestor, new class) pair -- offspring of one ancestor hold bit-identical states -- and
-  share the result; bitwise identical to ``dedup=False`` (every particle evaluated).
+  share the result; bitwise identical to ``dedup=False`` (every particle evaluated) with
+  the same dynamics tile shape (``dyn_tiles``).
 * ``shard_order`` (default True; multi-rank philox filters): each rank evaluates a slice of
   the particles ordered by resampling ancestor rather than a slice of particle indices, so
   de-duplication keeps ~1/R of the distinct keys per rank; bitwise identical either way.
+* ``dyn_tiles`` (``'auto'``): tile shape of the dynamics-GP pass (``gpmdm_pf_set_dyn_tiles``):
+  narrow tiles for de-duplicated rows, wide ones when every particle is evaluated; the
+  shapes differ only in floating-point summation order.
 
 Reference quirks kept for parity: log variance counted twice in the
 log-likelihood, float32 ``ln 2pi``, non-recursive weights, read-outs pairing
@@ -51,7 +55,8 @@ def _as_f64_vector(z) -> np.ndarray:
 class GPMDM_PF:
     def __init__(self, gpmdm: GPMDM, markov_switching_model, num_particles: int, *,
                  rng: str = "torch", seed=None, resample: str = "multinomial", process_group=None,
-                 shard=None, exchange=None, dedup: bool = True, shard_order: bool = True):
+                 shard=None, exchange=None, dedup: bool = True, shard_order: bool = True,
+                 dyn_tiles: str = "auto"):
         self._gpmdm = gpmdm
         self._gpmdm.set_evaluation_mode()
         self._markov_switching_model = torch.as_tensor(markov_switching_model).type(self.dtype)
@@ -100,6 +105,9 @@ class GPMDM_PF:
         self._model_gen = gpmdm.generation
         _lib.check(lib.gpmdm_pf_set_dedup(h, 1 if dedup else 0), "dedup")
         _lib.check(lib.gpmdm_pf_set_shard_order(h, 1 if shard_order else 0), "shard_order")
+        if dyn_tiles not in _lib.DYN_TILES:
+            raise ValueError("dyn_tiles must be 'auto', 'narrow' or 'wide'")
+        _lib.check(lib.gpmdm_pf_set_dyn_tiles(h, _lib.DYN_TILES[dyn_tiles]), "dyn_tiles")
         self._readout = None
         if self._world > 1:
             w, lo, hi = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()

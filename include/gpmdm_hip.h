@@ -188,6 +188,16 @@ int gpmdm_pf_stage_times(gpmdm_pf_t pf, double* ms, int64_t* launches);
 int gpmdm_pf_set_dedup(gpmdm_pf_t pf, int enable);
 int gpmdm_pf_dyn_rows(gpmdm_pf_t pf, int64_t* rows, void* stream);
 
+/* Tile shape of the dynamics-GP pass.  AUTO (default): narrow 16x256 tiles for the few
+ * de-duplicated rows (short K loops), the observation GP's wide shape when every particle
+ * is evaluated (dedup off: a throughput problem).  NARROW / WIDE force one; the two differ
+ * only in floating-point summation order (the de-duplication test forces NARROW on both
+ * filters to check bitwise identity).  Not between switch and propagate. */
+#define GPMDM_DYN_TILES_AUTO 0
+#define GPMDM_DYN_TILES_NARROW 1
+#define GPMDM_DYN_TILES_WIDE 2
+int gpmdm_pf_set_dyn_tiles(gpmdm_pf_t pf, int mode);
+
 /* Ancestor-ordered shards (multi-rank philox filters; default on).  After each resample the
  * particles are put in a stable order of their resampling ancestor's bucket (256 contiguous
  * ancestor ranges; identical on every rank) and rank r evaluates positions [lo, hi) of that

@@ -4,7 +4,9 @@ Offspring of one resampling ancestor hold bit-identical states, so the dynamics 
 (gpmdm.py:1032-1068) is evaluated once per distinct (ancestor, new class) key.  The bar is
 bitwise identity with the undeduplicated path (every particle evaluated, as the
 reference's _propogate_dynamics does, gpmdm_pf.py:153-168) for states, classes,
-log-likelihoods and resample indices, frame after frame.
+log-likelihoods and resample indices, frame after frame (both filters on the same
+dynamics tile shape: the default picks wide tiles without de-duplication, which differ
+only in summation order -- test_wide_dynamics_tiles_vs_narrow).
 """
 import numpy as np
 import pytest
@@ -27,7 +29,7 @@ def _pair(m, T, P, frames, zs, **kw):
     pfs = []
     for dd in (True, False):
         torch.manual_seed(5)
-        pfs.append(GPMDM_PF(m, T, P, dedup=dd, **kw))
+        pfs.append(GPMDM_PF(m, T, P, dedup=dd, dyn_tiles="narrow", **kw))
     rows = []
     for k in range(frames):
         st = torch.get_rng_state()          # replay mode: both filters see the same draws
@@ -72,7 +74,7 @@ def test_dedup_bitwise_sharded_and_many_classes():
         pfs = []
         for shard in ((2, 0), (2, 1)):
             torch.manual_seed(3)
-            pfs.append(GPMDM_PF(m, T, P, rng="philox", seed=5, shard=shard, dedup=dd))
+            pfs.append(GPMDM_PF(m, T, P, rng="philox", seed=5, shard=shard, dedup=dd, dyn_tiles="narrow"))
         hist = []
         for k in range(4):
             sends = [pf._stage_propagate(Y[k]) for pf in pfs]
@@ -92,10 +94,42 @@ def test_dedup_bank(m2):
     from gpmdm_amd import GPMDM_PF_Bank
     T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
     Y = m2.get_Y()
-    banks = [GPMDM_PF_Bank(m2, T, 3, 2000, seed=8, dedup=dd) for dd in (True, False)]
+    banks = [GPMDM_PF_Bank(m2, T, 3, 2000, seed=8, dedup=dd, dyn_tiles="narrow") for dd in (True, False)]
     for k in range(4):
         z = np.stack([Y[10 + k], Y[200 + k], Y[400 + k]])
         for b in banks:
             b.update(z)
         assert np.array_equal(banks[0].class_probabilities().numpy(), banks[1].class_probabilities().numpy())
         assert np.array_equal(banks[0].current_state_mean().numpy(), banks[1].current_state_mean().numpy())
+
+
+def test_wide_dynamics_tiles_vs_narrow(m2, fx_config2):
+    """dedup=False runs the dynamics GP on the wide (observation-GP-shaped) tile image by
+    default: one resynced step from the same particles and draws as the narrow tiles and as
+    the oracle -- states within 1e-12 of the narrow path (summation order only), everything
+    against the oracle at the parity tolerances."""
+    from conftest import assert_step_matches, oracle_model
+    from gpmdm_amd import GPMDM_PF
+    from oracle import gpmdm_oracle as O
+    T = np.array([[0.9, 0.1], [0.1, 0.9]])
+    P = 30_000
+    rng = np.random.RandomState(17)
+    om = oracle_model(fx_config2)
+    Y = m2.get_Y()
+    torch.manual_seed(2)
+    warm = GPMDM_PF(m2, torch.tensor(T), P, rng="torch")
+    warm.update(Y[30])
+    st0 = warm.export_state()
+    E, nrm, u = rng.exponential(size=(P, 2)), rng.randn(P, m2.d), rng.rand(P)
+    out = {}
+    for tiles in ("narrow", "wide"):
+        pf = GPMDM_PF(m2, torch.tensor(T), P, rng="torch", dedup=False, dyn_tiles=tiles)
+        pf.load_state(st0["states"], st0["classes"])
+        pf.update_with_draws(Y[31], E, nrm, u)
+        out[tiles] = (pf.export_state(), pf.class_probabilities().numpy(), pf.current_state_mean().numpy())
+    a, b = out["narrow"][0], out["wide"][0]
+    same = a["resample_idx"] == b["resample_idx"]
+    assert int((~same).sum()) <= 2
+    assert np.max(np.abs(a["states"][same] - b["states"][same])) <= 1e-12 * np.max(np.abs(a["states"]))
+    r = O.step(om, T, st0["states"], st0["classes"], Y[31], E, nrm, u)
+    assert_step_matches(b, r, out["wide"][1], out["wide"][2], u, what="wide")
