@@ -251,8 +251,10 @@ def main():
     stages = pf.stage_times()
     # per-stage breakdown from a separate, untimed pass (every stage's events on)
     pf.enable_timing(True)
+    bd_rows = 0
     for k in range(n_breakdown):            # the stream's next frames (no jump back in time)
         one(args.warmup + args.steps + k)
+        bd_rows += pf.dynamics_rows()       # rows the dynamics GP evaluated this frame
     torch.cuda.synchronize()
     pf.enable_timing(False)
     breakdown = pf.stage_times()
@@ -348,8 +350,12 @@ def main():
         "ess_frac_last": ess / P_total,
         "posterior_last": [float(x) for x in post],
         "dyn_rows_last": {"evaluated": dyn_rows, "particles": P_local,
-                          "note": "dynamics GP rows of the last step: one per distinct (ancestor, class) "
-                                  "key (bitwise-identical ancestor de-duplication, DESIGN.md §3)"},
+                          "breakdown_mean": bd_rows / max(n_breakdown, 1),
+                          "dyn_gemm_tflops": dyn_row_flops(model) * bd_rows
+                          / max(breakdown["dyn_gemm"][0], 1e-9) / 1e9,
+                          "note": "dynamics GP rows: one per distinct (ancestor, class) key (bitwise-"
+                                  "identical ancestor de-duplication, DESIGN.md §3); breakdown_mean and "
+                                  "dyn_gemm_tflops over the stage-breakdown pass"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
