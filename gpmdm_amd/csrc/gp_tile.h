@@ -317,6 +317,7 @@ __device__ __forceinline__ double exp2_64m(double t, const double* tab) {
 //           the row records' |Xs|^2 must then be scaled by 128/ln2, TileParams::rec128)
 //   bit 23: final power of two by an integer add to the exponent field (clamped) instead
 //           of v_ldexp_f64
+//   bit 24: three workgroups per CU (register cap 168: small shapes, e.g. 16x512, 32x384)
 //
 // Geometry: NW waves; each wave owns MT x NTW tiles of 16 x 16 (16 MT particles x 16 NTW
 // columns), so a workgroup covers PT = 16 MT particles x NB = 16 NTW NW columns.  K* costs
@@ -333,9 +334,9 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 template <int DI, bool DYN, int VAR = 0, int NW = 4, int MT = 4, int NTW = 4>
-__global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
+__global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1)) void k_gp_tile(const TileParams prm) {
   static_assert(MT == 1 || MT == 2 || MT == 4, "MT");
-  static_assert(NTW == 4 || NTW == 8 || NTW == 16, "NTW");
+  static_assert(NTW == 4 || NTW == 6 || NTW == 8 || NTW == 16, "NTW");
   // B fragments in flight: BR sub-steps (a full K-step, 4, for NTW <= 8; 2 for NTW = 16,
   // whose full K-step of fragments would not fit next to 128 accumulator VGPRs)
   constexpr int BR = NTW >= 16 ? 2 : 4;

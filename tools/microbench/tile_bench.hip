@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(X, hX.data(), (size_t)P * d * 8, hipMemcpyHostToDevice));
   // geometries: {waves, particle tiles MT, column tiles per wave NTW}
   struct Geo { int nw, mt, ntw; };
-  const Geo geos[] = {{4, 4, 4}, {8, 4, 4}, {4, 2, 8}, {4, 1, 16}};
+  const Geo geos[] = {{4, 4, 4}, {8, 4, 4}, {4, 2, 8}, {4, 1, 16}, {4, 1, 8}, {4, 2, 6}};
   const int NGEO = sizeof(geos) / sizeof(geos[0]);
   TileParams pp[NGEO];
   int* tabs;
@@ -97,10 +97,10 @@ int main(int argc, char** argv) {
               {launch_var<131072, 8>, 1, "64x512 LDS coords"}};
 #else
   V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512 production"},
-              {launch_var<4194304, 4, 2, 8>, 2, "32x512 T128"},
-              {launch_var<0, 4, 1, 16>, 3, "16x1024"},
-              {launch_var<4194304, 4, 1, 16>, 3, "16x1024 T128"},
-              {launch_var<16, 4, 1, 16>, 3, "16x1024 no gen"},
+              {launch_var<0, 4, 1, 8>, 4, "16x512 (2 WG/CU)"},
+              {launch_var<16777216, 4, 1, 8>, 4, "16x512 (3 WG/CU)"},
+              {launch_var<0, 4, 2, 6>, 5, "32x384 (2 WG/CU)"},
+              {launch_var<16777216, 4, 2, 6>, 5, "32x384 (3 WG/CU)"},
               {launch_var<16, 4, 2, 8>, 2, "32x512 no gen"}};
 #endif
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
