@@ -147,7 +147,8 @@ def cpu_baseline(data, budget_s=20.0):
                       y_log_lengthscales=np.log(hp["y_lengthscales_init"]), y_log_lambdas=np.log(hp["y_lambdas_init"]),
                       y_log_sigma_n=np.log(0.1), x_log_lengthscales=np.log(hp["x_lengthscales_init"]),
                       x_log_lambdas=np.log(hp["x_lambdas_init"]), x_log_sigma_n=np.log(0.1),
-                      x_log_lin_coeff=np.log(hp["x_lin_coeff_init"])).precompute()
+                      x_log_lin_coeff=np.log(hp["x_lin_coeff_init"])).precompute(
+                          "cholesky" if N > 4096 else "inverse")   # N >= 10^4: solves, not the O(N^3) inverse
     T = synthetic.markov_matrix(w["C"])
     Ps = w["P_per_gpu"] if N <= 2000 else 1000
     Ps -= Ps % w["C"]
