@@ -123,10 +123,6 @@ struct gpmdm_model {
   double* y_il2_dev = nullptr;
   double* y_lam2_dev = nullptr;   // 1 / il2 = exp(y_log_lambdas)^2
   double sum_log_il2 = 0.0;
-  // predictive-map scratch
-  int* tab = nullptr;                 // 5 ints: begin, end, out_base, tile_start[2]
-  double* qscratch = nullptr;
-  size_t qcap = 0;
 
   ~gpmdm_model() {
     obs.release();
@@ -134,15 +130,6 @@ struct gpmdm_model {
     for (auto& g : dynw) g.release();
     dfree(y_il2_dev);
     dfree(y_lam2_dev);
-    dfree(tab);
-    dfree(qscratch);
-  }
-  int ensure_q(size_t n) {
-    if (n <= qcap) return GPMDM_OK;
-    dfree(qscratch);
-    TRY(dalloc(&qscratch, n));
-    qcap = n;
-    return GPMDM_OK;
   }
 };
 
@@ -340,8 +327,6 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
       return fail(GPMDM_E_HIP, "upload lambda^2");
     }
   }
-  rc = dalloc(&m->tab, 8);
-  if (rc) { delete m; return rc; }
   *out = m;
   return GPMDM_OK;
 }
@@ -365,23 +350,26 @@ int gpmdm_predict_obs(gpmdm_model_t m, const double* Xs, int64_t n, double* mu, 
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipSetDevice(m->device));
   const int nparts = m->obs.n_parts();
-  TRY(m->ensure_q((size_t)nparts * n));
-  const int tab[5] = {0, (int)n, 0, 0, m->obs.tiles(n)};
-  HIPCHK(hipMemcpyAsync(m->tab, tab, sizeof(tab), hipMemcpyHostToDevice, s));
+  // per-call scratch on the caller's stream (stream-ordered allocation: calls on different
+  // streams never share it), freed in stream order after the finish kernel
+  double* q = nullptr;
+  HIPCHK(hipMallocAsync((void**)&q, sizeof(double) * (size_t)nparts * n, s));
   TileParams tp{};
   tp.seg[0] = m->obs.seg();
   tp.n_seg = 1;
   tp.geo = m->obs.geo;
   tp.tiles_ub = m->obs.tiles(n);
   tp.n_j_max = m->obs.n_j;
-  tp.seg_pos_begin = m->tab + 0;
-  tp.seg_pos_end = m->tab + 1;
-  tp.seg_out_base = m->tab + 2;
-  tp.seg_tile_start = m->tab + 3;
+  tp.seg_pos_begin = tp.seg_pos_end = tp.seg_out_base = tp.seg_tile_start = nullptr;   // inline table
+  tp.tab_inline[0] = 0;
+  tp.tab_inline[1] = (int)n;
+  tp.tab_inline[2] = 0;
+  tp.tab_inline[3] = 0;
+  tp.tab_inline[4] = m->obs.tiles(n);
   tp.perm = nullptr;
   tp.X = Xs;
   fill_tile_common(tp, m, false);
-  tp.qpart = m->qscratch;
+  tp.qpart = q;
   tp.ld_q = n;
   tp.mu = mu;
   tp.ld_mu = m->D;
@@ -390,7 +378,7 @@ int gpmdm_predict_obs(gpmdm_model_t m, const double* Xs, int64_t n, double* mu, 
   fa.n_out = n;
   fa.n_parts = nparts;
   fa.D = m->D;
-  fa.qpart = m->qscratch;
+  fa.qpart = q;
   fa.ld_q = n;
   fa.mu = mu;
   fa.ld_mu = m->D;
@@ -398,6 +386,7 @@ int gpmdm_predict_obs(gpmdm_model_t m, const double* Xs, int64_t n, double* mu, 
   fa.var_out = var;
   launch_obs_finish(fa, s);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipFreeAsync(q, s));
   return GPMDM_OK;
 }
 
@@ -411,22 +400,23 @@ int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, doubl
   HIPCHK(hipSetDevice(m->device));
   const GpImage& g = m->dyn_set(n >= kWideRows)[c];
   const int nparts = g.n_parts();
-  TRY(m->ensure_q((size_t)nparts * n));
-  const int tab[5] = {0, (int)n, 0, 0, g.tiles(n)};
-  HIPCHK(hipMemcpyAsync(m->tab, tab, sizeof(tab), hipMemcpyHostToDevice, s));
+  double* q = nullptr;                 // per-call scratch, stream-ordered (see gpmdm_predict_obs)
+  HIPCHK(hipMallocAsync((void**)&q, sizeof(double) * (size_t)nparts * n, s));
   TileParams tp{};
   tp.seg[0] = g.seg();
   tp.n_seg = 1;
   tp.geo = g.geo;
   tp.tiles_ub = g.tiles(n);
   tp.n_j_max = g.n_j;
-  tp.seg_pos_begin = m->tab + 0;
-  tp.seg_pos_end = m->tab + 1;
-  tp.seg_out_base = m->tab + 2;
-  tp.seg_tile_start = m->tab + 3;
+  tp.seg_pos_begin = tp.seg_pos_end = tp.seg_out_base = tp.seg_tile_start = nullptr;   // inline table
+  tp.tab_inline[0] = 0;
+  tp.tab_inline[1] = (int)n;
+  tp.tab_inline[2] = 0;
+  tp.tab_inline[3] = 0;
+  tp.tab_inline[4] = g.tiles(n);
   tp.X = Xs;
   fill_tile_common(tp, m, true);
-  tp.qpart = m->qscratch;
+  tp.qpart = q;
   tp.ld_q = n;
   tp.mu = mu;
   tp.ld_mu = m->d;
@@ -436,7 +426,7 @@ int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, doubl
   fa.n_seg = 1;
   fa.d = m->d;
   fa.n_parts[0] = nparts;
-  fa.qpart = m->qscratch;
+  fa.qpart = q;
   fa.ld_q = n;
   fa.mu = mu;
   fa.ld_mu = m->d;
@@ -446,6 +436,7 @@ int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, doubl
   fa.var_out = var;
   launch_dyn_finish(fa, s);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipFreeAsync(q, s));
   return GPMDM_OK;
 }
 

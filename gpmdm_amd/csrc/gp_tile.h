@@ -399,11 +399,15 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
   const int b = blockIdx.x;
   const int J = prm.n_j_max - 1 - b / prm.tiles_ub;
   // tile index within this launch's segments (a launch may cover classes c0..c0+7)
-  const int t = b - (b / prm.tiles_ub) * prm.tiles_ub + prm.seg_tile_start[0];
+  // segment tables: device arrays (filter: computed on the device), or one segment passed
+  // by value (predictive maps: no host-to-device copy of a table per call)
+  const bool inl = prm.seg_pos_begin == nullptr;
+  auto tile_start = [&](int s) { return inl ? prm.tab_inline[3 + s] : prm.seg_tile_start[s]; };
+  const int t = b - (b / prm.tiles_ub) * prm.tiles_ub + tile_start(0);
 
   int c = -1;
   for (int s = 0; s < prm.n_seg; ++s)
-    if (t >= prm.seg_tile_start[s] && t < prm.seg_tile_start[s + 1]) c = s;
+    if (t >= tile_start(s) && t < tile_start(s + 1)) c = s;
   c = __builtin_amdgcn_readfirstlane(c);
   if (c < 0) return;
   const int n_j = prm.seg[c].n_j;
@@ -426,10 +430,10 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
   }
   const double* tabl = tab + (TREP > 1 ? (tid & 63) % TREP : 0);   // this lane's copy
 
-  const int seg_begin = prm.seg_pos_begin[c];
-  const int pos0 = seg_begin + (t - prm.seg_tile_start[c]) * PT;
-  const int pos_end = prm.seg_pos_end[c];
-  const int out_base = prm.seg_out_base[c] - seg_begin;   // out = out_base + pos
+  const int seg_begin = inl ? prm.tab_inline[0] : prm.seg_pos_begin[c];
+  const int pos0 = seg_begin + (t - tile_start(c)) * PT;
+  const int pos_end = inl ? prm.tab_inline[1] : prm.seg_pos_end[c];
+  const int out_base = (inl ? prm.tab_inline[2] : prm.seg_out_base[c]) - seg_begin;   // out = out_base + pos
 
   // ---- this thread's particle (generation role: particle m, rows g + NG s) ----------
   const int m = tid % PT;
