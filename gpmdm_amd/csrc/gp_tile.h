@@ -318,6 +318,8 @@ __device__ __forceinline__ double exp2_64m(double t, const double* tab) {
 //   bit 23: final power of two by an integer add to the exponent field (clamped) instead
 //           of v_ldexp_f64
 //   bit 24: three workgroups per CU (register cap 168: small shapes, e.g. 16x512, 32x384)
+//   bit 25: GEN2 -- generate two K-steps' values (4 interleaved exp chains per thread) on
+//           even K-steps and none on odd ones (same VALU, half the exposed chain latency)
 //
 // Geometry: NW waves; each wave owns MT x NTW tiles of 16 x 16 (16 MT particles x 16 NTW
 // columns), so a workgroup covers PT = 16 MT particles x NB = 16 NTW NW columns.  K* costs
@@ -642,9 +644,22 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
     const int grb = ST ? ((SL + LOOK) & (RXS - 1)) : ((ks + LOOK) & (RXS - 1));
     double v[GV];
     double rr[RPT];
+    constexpr bool GEN2 = (VAR & 33554432) != 0;
+    double v2[GV];
+    const bool gen_now = !GEN2 || (ks & 1) == 0;
     if constexpr (!(VAR & 16)) {
       load_rows(ks + RA, rr);
-      if constexpr (!SPLIT) gen(ks + LOOK, grb, v);
+      if constexpr (GEN2) {
+        if (gen_now) {                                  // K-steps ks+2 and ks+3 together
+#pragma unroll
+          for (int s2 = 0; s2 < GV; ++s2) {
+            v[s2] = gen_one(ks + 2, (ks + 2) & (RXS - 1), s2);
+            v2[s2] = gen_one(ks + 3, (ks + 3) & (RXS - 1), s2);
+          }
+        }
+      } else if constexpr (!SPLIT) {
+        gen(ks + LOOK, grb, v);
+      }
     }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
@@ -678,7 +693,14 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
       loadB_part(ks + (kk + BR) / 4, (kk + BR) % 4, kk % BR, bb);   // sub-step kk + BR
     }
     if constexpr (!(VAR & 16)) {
-      store(gslot, v);
+      if constexpr (GEN2) {
+        if (gen_now) {
+          store((ks + 2) & (ASL - 1), v);
+          store((ks + 3) & (ASL - 1), v2);
+        }
+      } else {
+        store(gslot, v);
+      }
       store_rows(rslot, rr);
     }
     if constexpr (!(VAR & 8)) {
@@ -753,8 +775,21 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
     double v[GV];
     double rr[RPT];
     load_rows(ks + RA, rr);
-    gen(ks + LOOK, (ks + LOOK) & (RXS - 1), v);
-    store((ks + LOOK) & (ASL - 1), v);
+    if constexpr ((VAR & 33554432) != 0) {             // GEN2: both K-steps on even ks
+      if ((ks & 1) == 0) {
+        double v2[GV];
+#pragma unroll
+        for (int s2 = 0; s2 < GV; ++s2) {
+          v[s2] = gen_one(ks + 2, (ks + 2) & (RXS - 1), s2);
+          v2[s2] = gen_one(ks + 3, (ks + 3) & (RXS - 1), s2);
+        }
+        store((ks + 2) & (ASL - 1), v);
+        store((ks + 3) & (ASL - 1), v2);
+      }
+    } else {
+      gen(ks + LOOK, (ks + LOOK) & (RXS - 1), v);
+      store((ks + LOOK) & (ASL - 1), v);
+    }
     store_rows((ks + RA) & (RXS - 1), rr);
     if (ks % SB == SB - 1) __syncthreads();
   }

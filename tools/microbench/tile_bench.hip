@@ -97,10 +97,10 @@ int main(int argc, char** argv) {
               {launch_var<131072, 8>, 1, "64x512 LDS coords"}};
 #else
   V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512 production"},
-              {launch_var<0, 4, 1, 8>, 4, "16x512 (2 WG/CU)"},
-              {launch_var<16777216, 4, 1, 8>, 4, "16x512 (3 WG/CU)"},
-              {launch_var<0, 4, 2, 6>, 5, "32x384 (2 WG/CU)"},
-              {launch_var<16777216, 4, 2, 6>, 5, "32x384 (3 WG/CU)"},
+              {launch_var<33554432, 4, 2, 8>, 2, "32x512 GEN2"},
+              {launch_var<33554432 | 4194304, 4, 2, 8>, 2, "32x512 GEN2+T128"},
+              {launch_var<0, 4>, 0, "64x256"},
+              {launch_var<33554432, 4>, 0, "64x256 GEN2"},
               {launch_var<16, 4, 2, 8>, 2, "32x512 no gen"}};
 #endif
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
