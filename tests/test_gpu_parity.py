@@ -524,3 +524,42 @@ def test_stage_selective_timing(m2):
     st = pf.stage_times()
     pf.enable_timing(False)
     assert all(n == 1 for ms, n in st.values()), st
+
+
+@pytest.mark.parametrize("C,d,D,L", [(2, 24, 30, 40), (2, 32, 20, 35), (9, 2, 6, 20)])
+def test_wide_latents_and_many_classes_vs_oracle(C, d, D, L):
+    """The remaining supported shapes: latent dimensions 24 and 32 (launch bounds of one
+    workgroup per CU, 64x512 observation tiles), and C = 9 classes, which crosses the
+    8-segment limit of one dynamics launch (two launches per step).  Predictive maps and
+    one resynced filter step (replay draws) against the oracle."""
+    from gpmdm_amd import GPMDM, GPMDM_PF, synthetic
+    from oracle import gpmdm_oracle as O
+    data = synthetic.make_sequences(C=C, S=3, L=L, D=D, d=d, seed=41)
+    rng = np.random.RandomState(42)
+    N = C * 3 * L
+    X = rng.randn(N, d) * 0.3
+    lp = dict(y_log_lengthscales=np.log(rng.uniform(2.0, 4.0, d)), y_log_lambdas=np.log(rng.uniform(0.5, 2, D)),
+              y_log_sigma_n=np.log(0.15), x_log_lengthscales=np.log(rng.uniform(2.0, 4.0, d)),
+              x_log_lambdas=np.log(rng.uniform(0.5, 2, d)), x_log_sigma_n=np.log(0.12),
+              x_log_lin_coeff=np.log(rng.uniform(0.2, 0.8, d + 1)))
+    m = GPMDM.from_arrays(X, data.sequences, **lp)
+    om = O.OracleModel(X=X, Y=np.concatenate([y for c in data.sequences for y in c]).astype(np.float64),
+                       seq_lengths=[[L] * 3] * C, **lp).precompute()
+    xs = X[rng.randint(0, N, 257)] + 0.05 * rng.randn(257, d)
+    mu, var = m.map_x_to_y(torch.tensor(xs))
+    omu, ovar = om.map_x_to_y(xs)
+    assert nrel(mu.numpy(), omu) < 1e-8 and nrel(var.numpy(), ovar) < 1e-7
+    for c in range(C):
+        mu, var = m.map_x_dynamics_for_class(torch.tensor(xs), c)
+        omu, ovar = om.map_x_dynamics_for_class(xs, c)
+        assert nrel(mu.numpy(), omu) < 1e-8 and nrel(var.numpy(), ovar) < 1e-6, c
+    P = 999
+    T = synthetic.markov_matrix(C)
+    pf = GPMDM_PF(m, torch.tensor(T), P, rng="torch")
+    st0 = pf.export_state()
+    E, nrm, u = rng.exponential(size=(P, C)), rng.randn(P, d), rng.rand(P)
+    z = data.sequences[0][0][4].astype(np.float64)
+    pf.update_with_draws(z, E, nrm, u)
+    r = O.step(om, T, st0["states"], st0["classes"], z, E, nrm, u)
+    from conftest import assert_step_matches
+    assert_step_matches(pf.export_state(), r, pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), u)
