@@ -320,6 +320,9 @@ __device__ __forceinline__ double exp2_64m(double t, const double* tab) {
 //   bit 24: three workgroups per CU (register cap 168: small shapes, e.g. 16x512, 32x384)
 //   bit 25: GEN2 -- generate two K-steps' values (4 interleaved exp chains per thread) on
 //           even K-steps and none on odd ones (same VALU, half the exposed chain latency)
+//   bit 26: SPEC -- wave-specialised workgroup: NW/2 MFMA waves (the column geometry of an
+//           NW/2-wave shape) and NW/2 producer waves that stage rows and generate K* two
+//           K-steps ahead; no MFMA wave ever issues an exp chain (one workgroup per CU)
 //
 // Geometry: NW waves; each wave owns MT x NTW tiles of 16 x 16 (16 MT particles x 16 NTW
 // columns), so a workgroup covers PT = 16 MT particles x NB = 16 NTW NW columns.  K* costs
@@ -336,7 +339,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 template <int DI, bool DYN, int VAR = 0, int NW = 4, int MT = 4, int NTW = 4>
-__global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1)) void k_gp_tile(const TileParams prm) {
+__global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 16777216) ? 3 : 2) : 1)) void k_gp_tile(const TileParams prm) {
   static_assert(MT == 1 || MT == 2 || MT == 4, "MT");
   static_assert(NTW == 4 || NTW == 6 || NTW == 8 || NTW == 16, "NTW");
   // B fragments in flight: BR sub-steps (a full K-step, 4, for NTW <= 8; 2 for NTW = 16,
@@ -345,18 +348,22 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
   // tiles retire in groups of RG (NTW = 16: 8 phase groups instead of 16, so the K loop has
   // 36 phase variants rather than 136; a group runs until its last tile's diagonal)
   constexpr int RG = NTW >= 16 ? 2 : 1;
+  constexpr bool SPEC = (VAR & 67108864) != 0;
+  static_assert(!SPEC || NW == 8, "SPEC: 4 MFMA + 4 producer waves");
+  constexpr int NWM = SPEC ? NW / 2 : NW;                    // MFMA waves
   constexpr int NT = 64 * NW;                                // threads
+  constexpr int NTG = SPEC ? 64 * (NW - NWM) : NT;           // generation / row-staging threads
   constexpr int PT = 16 * MT;                                // particles per tile
-  constexpr int NB = 16 * NTW * NW;                          // columns per block
+  constexpr int NB = 16 * NTW * NWM;                         // columns per block
   constexpr int WS = 256 * NTW;                              // fragment doubles per wave per K-step
-  constexpr int FS = NW * WS;                                // fragment doubles per K-step
-  constexpr int NG = NT / PT;                                // generation row groups
+  constexpr int FS = NWM * WS;                               // fragment doubles per K-step
+  constexpr int NG = NTG / PT;                               // generation row groups
   constexpr int GV = kBK / NG;                               // K* values per thread per K-step
   static_assert(GV * NG == kBK, "generation split");
   constexpr int LDA = PT + 16;                               // rows k, k+1 land 32 banks apart
   constexpr int RW = DI + 1;                                 // row record: Xs[DI], |Xs|^2
   constexpr int NRV = kBK * RW;                              // row values per K-step
-  constexpr int RPT = (NRV + NT - 1) / NT;                   // row values per thread
+  constexpr int RPT = (NRV + NTG - 1) / NTG;                 // row values per thread
   // LDS rings.  Default: one barrier per two K-steps (after odd ones), K* generated
   // two K-steps ahead into 4 slots, rows staged four ahead into 4 slots -- a slot is
   // rewritten only after a barrier that follows its last read, and read only after a
@@ -372,7 +379,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
   constexpr int LOOK = SB;                                   // generation lookahead (K-steps)
   constexpr int RA = 2 * SB;                                 // row staging lookahead
   __shared__ double As[ASL][kBK][LDA];
-  __shared__ double RX[RXS][RPT * NT];                        // row records, then padding
+  __shared__ double RX[RXS][RPT * NTG];                       // row records, then padding
   constexpr bool E256 = (VAR & 256) != 0;
   constexpr bool FOLD = (VAR & 2097152) != 0;
   constexpr bool T128 = (VAR & 4194304) != 0;
@@ -398,6 +405,10 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // SPEC: waves [0, NWM) multiply, waves [NWM, NW) stage rows and generate K*
+  const bool producer = !SPEC || w >= NWM;
+  const bool consumer = !SPEC || w < NWM;
+  const int gtid = SPEC ? (tid >= 64 * NWM ? tid - 64 * NWM : tid) : tid;   // generation-role index
   const int b = blockIdx.x;
   const int J = prm.n_j_max - 1 - b / prm.tiles_ub;
   // tile index within this launch's segments (a launch may cover classes c0..c0+7)
@@ -438,8 +449,8 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
   const int out_base = (inl ? prm.tab_inline[2] : prm.seg_out_base[c]) - seg_begin;   // out = out_base + pos
 
   // ---- this thread's particle (generation role: particle m, rows g + NG s) ----------
-  const int m = tid % PT;
-  const int g = tid / PT;
+  const int m = gtid % PT;
+  const int g = gtid / PT;
   int pos = pos0 + m;
   if (pos >= pos_end) pos = pos0;                          // clamp (results unused)
   const int prow = prm.perm ? prm.perm[pos] : pos;
@@ -475,7 +486,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
   int kend[NTW];
 #pragma unroll
   for (int tt = 0; tt < NTW; ++tt) {
-    const int c0 = J * NB + 16 * (NW * tt + w) - coff;   // front-padding tiles: c0 < 0
+    const int c0 = J * NB + 16 * (NWM * tt + w) - coff;   // front-padding tiles: c0 < 0
     const bool real = c0 >= 0 && c0 < n_cols;
     if (real) T1 = tt + 1;
     const int hi = c0 + 16;
@@ -513,7 +524,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
   unsigned roff[RPT];
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
-    const int idx = tid + NT * k;
+    const int idx = gtid + NTG * k;
     roff[k] = (unsigned)(idx < NRV ? idx : NRV - 1) * 8u;
   }
   auto load_rows = [&](int ks, double (&rr)[RPT]) {
@@ -528,7 +539,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
     }
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-      int idx = tid + NT * k;
+      int idx = gtid + NTG * k;
       idx = idx < NRV ? idx : NRV - 1;
       const int r = idx / RW, f = idx - (idx / RW) * RW;
       int i = ks * kBK + r;
@@ -541,9 +552,9 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       if constexpr (VAR & 1024) {
-        if (tid + NT * k < NRV) RX[buf][tid + NT * k] = rr[k];
+        if (gtid + NTG * k < NRV) RX[buf][gtid + NTG * k] = rr[k];
       } else {
-        RX[buf][tid + NT * k] = rr[k];                      // unconditional (padding slots)
+        RX[buf][gtid + NTG * k] = rr[k];                    // unconditional (padding slots)
       }
     }
   };
@@ -647,7 +658,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
     constexpr bool GEN2 = (VAR & 33554432) != 0;
     double v2[GV];
     const bool gen_now = !GEN2 || (ks & 1) == 0;
-    if constexpr (!(VAR & 16)) {
+    if constexpr (!(VAR & 16) && !SPEC) {                // SPEC: producer waves generate
       load_rows(ks + RA, rr);
       if constexpr (GEN2) {
         if (gen_now) {                                  // K-steps ks+2 and ks+3 together
@@ -674,7 +685,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
 #pragma unroll
         for (int nt = T0; nt < T1c; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bb[(kk % BR) * NTW + nt], acc[mt][nt], 0, 0, 0);
-      if constexpr (SPLIT && !(VAR & 16)) {
+      if constexpr (SPLIT && !(VAR & 16) && !SPEC) {
         constexpr int PER = 4 / GV > 0 ? 4 / GV : 1;
         if (kk % PER == 0) {
 #pragma unroll
@@ -692,7 +703,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
       }
       loadB_part(ks + (kk + BR) / 4, (kk + BR) % 4, kk % BR, bb);   // sub-step kk + BR
     }
-    if constexpr (!(VAR & 16)) {
+    if constexpr (!(VAR & 16) && !SPEC) {
       if constexpr (GEN2) {
         if (gen_now) {
           store((ks + 2) & (ASL - 1), v);
@@ -731,7 +742,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
 #pragma unroll
     for (int q = 0; q < BR * NTW; ++q) bb[q] = 1e-3 * q + lane;
   }
-  {
+  if (producer) {
     double rr[RPT];
 #pragma unroll
     for (int j = 0; j < RA; ++j) {
@@ -742,19 +753,42 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
   __syncthreads();                                           // table + rows of steps 0 .. RA-1
   {
     double v[GV];
+    if (producer) {
 #pragma unroll
-    for (int j = 0; j < LOOK; ++j) {
-      gen(j, j & (RXS - 1), v);
-      store(j, v);
+      for (int j = 0; j < LOOK; ++j) {
+        gen(j, j & (RXS - 1), v);
+        store(j, v);
+      }
     }
+    if (consumer) {
 #pragma unroll
-    for (int kk = 0; kk < BR; ++kk) loadB_part(0, kk, kk, bb);
+      for (int kk = 0; kk < BR; ++kk) loadB_part(0, kk, kk, bb);
+    }
   }
   // Drain the prologue's loads (vmcnt(0)) so that the K loop's entry carries no pending
   // loads: otherwise the waitcnt pass merges the prologue's issue order into the loop
   // header and waits for every in-flight B fragment at sub-step 0 of each K-step.
   if constexpr (!(VAR & 2048)) __builtin_amdgcn_s_waitcnt(0x0F70);
   __syncthreads();
+
+  if constexpr (SPEC) {
+    if (producer) {                                          // stage rows, generate K*: all K-steps
+      for (int kp = 0; kp < nks; ++kp) {
+        double v[GV];
+        double rr[RPT];
+        load_rows(kp + RA, rr);
+        gen(kp + LOOK, (kp + LOOK) & (RXS - 1), v);
+        store((kp + LOOK) & (ASL - 1), v);
+        store_rows((kp + RA) & (RXS - 1), rr);
+        if (kp % SB == SB - 1) __syncthreads();
+      }
+      // the epilogue's barrier (the MFMA waves' cross-wave reduction)
+      const bool has_r0 = J * NB - coff < n_rows;
+      const bool has_m0 = (J + 1) * NB - coff > n_rows;
+      if (has_r0 || (has_m0 && prm.spart != nullptr)) __syncthreads();
+      return;
+    }
+  }
 
   int ks = 0;
   // K-steps [ks, kend[T0]) with tiles [T0, T1) active, for T0 = 0 .. T1-1
@@ -771,6 +805,8 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
     }
   });
   // the rest of the block's K range (other waves' tiles): generate only
+  for (; ks < nks && SPEC; ++ks)                             // SPEC: the producers generate
+    if (ks % SB == SB - 1) __syncthreads();
   for (; ks < nks; ++ks) {
     double v[GV];
     double rr[RPT];
@@ -815,7 +851,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
     // Linear-kernel share: acc += X~ H for this block.  A fragment: lane l holds
     // x~[particle mt*16 + (l&15)][4 kh + (l>>4)]; B fragment: Hf[J][kh][w][l][nt].
     constexpr int KH = (DI + 1 + 3) / 4;
-    const double* __restrict__ Hw = prm.seg[c].Hf + ((long long)J * KH * NW + w) * (64 * NTW) + lane * NTW;
+    const double* __restrict__ Hw = prm.seg[c].Hf + ((long long)J * KH * NWM + w) * (64 * NTW) + lane * NTW;
     int prw[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -829,7 +865,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
       double hb[NTW];
 #pragma unroll
       for (int h = 0; h < NTW / 2; ++h) {
-        const double2 hv = *reinterpret_cast<const double2*>(Hw + (long long)kh * NW * (64 * NTW) + 2 * h);
+        const double2 hv = *reinterpret_cast<const double2*>(Hw + (long long)kh * NWM * (64 * NTW) + 2 * h);
         hb[2 * h] = hv.x;
         hb[2 * h + 1] = hv.y;
       }
@@ -852,7 +888,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
     if (!fused) {
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
-        const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
+        const int jm = J * NB + 16 * (NWM * nt + w) + li - coff - n_rows;
         if (jm >= 0 && jm < n_m) {
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
@@ -877,7 +913,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
         for (int r = 0; r < 4; ++r) ss[mt][r] = 0.0;
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
-        const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
+        const int jm = J * NB + 16 * (NWM * nt + w) + li - coff - n_rows;
         if (jm >= 0 && jm < n_m) {
           const double lam = prm.lam2[jm];
           if (f0 == f1) {
@@ -918,7 +954,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
     // mean columns do not enter the quadratic form
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
-      const int col = J * NB + 16 * (NW * nt + w) + li - coff;
+      const int col = J * NB + 16 * (NWM * nt + w) + li - coff;
       if (col >= n_rows) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = (d4){0.0, 0.0, 0.0, 0.0};
@@ -958,13 +994,13 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? ((VAR & 16777216) ? 3 : 2) : 1
         if (has_r) {
           double q = 0.0;
 #pragma unroll
-          for (int ww = 0; ww < NW; ++ww) q += qred[ww][tid];
+          for (int ww = 0; ww < NWM; ++ww) q += qred[ww][tid];
           prm.qpart[(long long)J * prm.ld_q + out_base + p] = q;
         }
         if (has_m && fused) {
           double sm = 0.0;
 #pragma unroll
-          for (int ww = 0; ww < NW; ++ww) sm += sred[ww][tid];
+          for (int ww = 0; ww < NWM; ++ww) sm += sred[ww][tid];
           prm.spart[(long long)J * prm.ld_q + out_base + p] = sm;
         }
       }

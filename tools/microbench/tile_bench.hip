@@ -3,6 +3,7 @@
 // Variants run interleaved in one process (cdna_hip_programming.md §5.4 rule 24).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/microbench/tile_bench.hip -o tools/microbench/tile_bench
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -97,10 +98,8 @@ int main(int argc, char** argv) {
               {launch_var<131072, 8>, 1, "64x512 LDS coords"}};
 #else
   V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512 production"},
-              {launch_var<33554432, 4, 2, 8>, 2, "32x512 GEN2"},
-              {launch_var<33554432 | 4194304, 4, 2, 8>, 2, "32x512 GEN2+T128"},
-              {launch_var<0, 4>, 0, "64x256"},
-              {launch_var<33554432, 4>, 0, "64x256 GEN2"},
+              {launch_var<67108864, 8, 2, 8>, 2, "32x512 SPEC (4 MFMA + 4 producer waves)"},
+              {launch_var<67108864, 8, 4, 4>, 0, "64x256 SPEC"},
               {launch_var<16, 4, 2, 8>, 2, "32x512 no gen"}};
 #endif
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
@@ -116,6 +115,25 @@ int main(int argc, char** argv) {
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       t[v].push_back(ms / 3);
     }
+  // results check: every variant on the production geometry must write the same q partials
+  {
+    const size_t nq = (size_t)P * (pp[2].n_j_max);
+    std::vector<double> q0(nq), q1(nq);
+    CK(hipMemset(q, 0, nq * 8));
+    vars[0].fn(pp[vars[0].pi], s);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(q0.data(), q, nq * 8, hipMemcpyDeviceToHost));
+    for (int v = 1; v < NV; ++v) {
+      if (vars[v].pi != vars[0].pi) continue;
+      CK(hipMemset(q, 0, nq * 8));
+      vars[v].fn(pp[vars[v].pi], s);
+      CK(hipDeviceSynchronize());
+      CK(hipMemcpy(q1.data(), q, nq * 8, hipMemcpyDeviceToHost));
+      double md = 0, mx = 0;
+      for (size_t i = 0; i < nq; ++i) { md = std::max(md, std::abs(q1[i] - q0[i])); mx = std::max(mx, std::abs(q0[i])); }
+      printf("check %-30s max |q - q_production| = %.3g (max |q| %.3g)\n", vars[v].name, md, mx);
+    }
+  }
   double rows = 0;   // per 16-column tile: rows up to its diagonal (or all, for mean tiles)
   for (int tc = 0; tc * 16 < N + D; ++tc) {
     const int hi = tc * 16 + 16;
