@@ -154,6 +154,7 @@ struct gpmdm_pf {
   int *blockcounts = nullptr, *blockoff = nullptr, *small = nullptr;   // small: class tables
   int *obs_tab = nullptr;
   int* guide = nullptr;             // F x (GB + 3) inverse-CDF guide table
+  int *sys_mark = nullptr, *sys_block = nullptr;   // systematic resampling by scan (pf_kernels.hip)
   // ancestor de-duplication: owner/slot are C x P keyed by (class, ancestor)
   unsigned* owner = nullptr;
   int *slot = nullptr, *lflag = nullptr, *lblock = nullptr, *ltab = nullptr, *lperm = nullptr;
@@ -206,7 +207,7 @@ struct gpmdm_pf {
                     pred_q, pred_mu, pred_mu_p, pred_out};
     for (double* p : ds) dfree(p);
     int* is[] = {cls, cls_new, perm, ridx, blockcounts, blockoff, small, obs_tab,
-                 slot, lflag, lblock, ltab, lperm, guide, own};
+                 slot, lflag, lblock, ltab, lperm, guide, own, sys_mark, sys_block};
     for (int* p : is) dfree(p);
     dfree(own_tmp);
     dfree(gmax);
@@ -516,6 +517,10 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   ALLOC(partials, F * pf->nbf * (C + 1 + d));
   ALLOC(readout, F * (C + d + 1));
   ALLOC(health, kHealthN);
+  if (resample_mode == GPMDM_RESAMPLE_SYSTEMATIC) {
+    ALLOC(sys_mark, P);
+    ALLOC(sys_block, F * pf->nbf);
+  }
   if (n_ranks > 1 && rng_mode == GPMDM_RNG_PHILOX) {
     pf->own_tmp_bytes = std::max<size_t>(ancestor_order_temp_bytes(P), 1);
     ALLOC(own, P);
@@ -592,6 +597,8 @@ static ResampleArgs resample_args(gpmdm_pf* pf) {
   ra.readout = pf->readout;
   ra.guide = pf->guide;
   ra.GB = guide_buckets_used(pf->Pf);   // 0: plain search
+  ra.sys_mark = pf->sys_mark;           // systematic: by scan, no search
+  ra.sys_block = pf->sys_block;
   return ra;
 }
 

@@ -183,6 +183,11 @@ struct ResampleArgs {
   double* readout;                // per filter: C posterior, d mean, 1 likelihood sum
   int* guide;                     // F x (GB + 3): guide[b] = first i with cum[i] >= b / GB
   long long GB;                   // guide buckets per filter
+  // systematic resampling by scan (no per-slot search): run starts of each particle's
+  // offspring marked in sys_mark (F x P), block-local max-scan in place, block maxima
+  // (F x nb) scanned; slot s's ancestor = max(local[s], block prefix).  nullptr: search.
+  int* sys_mark;
+  int* sys_block;
 };
 
 // Guide buckets per filter for the inverse-CDF search (P / 4: a resample search then spans

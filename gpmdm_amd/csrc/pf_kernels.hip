@@ -507,6 +507,93 @@ __global__ __launch_bounds__(kB) void k_guide(ResampleArgs a) {
   a.guide[f * (a.GB + 3) + b] = (int)lo;
 }
 
+// ---------------------------------------------------------------------------------
+// Systematic resampling by scan (north_star's scan-based systematic resampler).  Slot s
+// draws u_s = (s + u0) / P; the search form gives slot s the first i with cum_i >= u_s, so
+// particle i owns slots [S_{i-1}, S_i) with S_i = #{s : u_s <= cum_i} (u_s is monotone in
+// s).  S_i comes from the closed form floor(cum_i P - u0) + 1, corrected against the same
+// fp64 expression for u_s the search compares, so the indices are exactly the search's.
+// Each particle with offspring marks the start of its run; an inclusive max-scan over the
+// slots then fills every run with its particle: O(P) work, no per-slot search, no load
+// imbalance when one ancestor takes most slots.
+__device__ __forceinline__ double sys_u(long long s, double u0, long long P) {
+  return ((double)s + u0) / (double)P;                      // exactly k_resample's expression
+}
+__device__ __forceinline__ long long sys_count(double c, double u0, long long P) {
+  long long k = (long long)floor(c * (double)P - u0) + 1;    // estimate of #{s : u_s <= c}
+  k = k < 0 ? 0 : (k > P ? P : k);
+  while (k > 0 && sys_u(k - 1, u0, P) > c) --k;
+  while (k < P && sys_u(k, u0, P) <= c) ++k;
+  return k;
+}
+__device__ __forceinline__ double sys_u0(const ResampleArgs& a, long long f) {
+  if (a.U) return a.U[0];
+  const uint4 r = philox4x32_10(make_uint4(0u, a.frame, kStreamSystematic, 0u), filter_key(a.seed_lo, a.seed_hi, f));
+  return u01_co(r.x, r.y);
+}
+
+// marks[s] = i where particle i's offspring start (-1 elsewhere: memset before)
+__global__ __launch_bounds__(kB) void k_sys_marks(ResampleArgs a) {
+  const long long f = blockIdx.y;
+  const long long i = (long long)blockIdx.x * kB + threadIdx.x;
+  if (i >= a.P) return;
+  const double u0 = sys_u0(a, f);
+  const double* cum = a.cum + f * a.P;
+  const long long lo = i > 0 ? sys_count(cum[i - 1], u0, a.P) : 0;
+  const long long hi = sys_count(cum[i], u0, a.P);
+  if (hi > lo) a.sys_mark[f * a.P + lo] = (int)i;
+}
+
+// block-local inclusive max-scan of the marks (in place) and the block maxima
+__global__ __launch_bounds__(kB) void k_sys_scan(ResampleArgs a) {
+  __shared__ int wmax[kB / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long f = blockIdx.y;
+  const long long s = (long long)blockIdx.x * kB + tid;
+  int x = s < a.P ? a.sys_mark[f * a.P + s] : -1;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x = max(x, y);
+  }
+  if (lane == 63) wmax[w] = x;
+  __syncthreads();
+  for (int v = 0; v < w; ++v) x = max(x, wmax[v]);
+  if (s < a.P) a.sys_mark[f * a.P + s] = x;
+  if (tid == kB - 1) a.sys_block[f * a.nb + blockIdx.x] = x;
+}
+
+// one workgroup per filter: exclusive max-scan of the block maxima (in place)
+__global__ __launch_bounds__(1024) void k_sys_blocks(ResampleArgs a) {
+  __shared__ int part[1024];
+  const int tid = threadIdx.x;
+  const long long f = blockIdx.x;
+  int* blk = a.sys_block + f * a.nb;
+  const int chunk = (a.nb + 1023) / 1024;
+  int mx = -1;
+  for (int i = 0; i < chunk; ++i) {
+    const int b = tid * chunk + i;
+    if (b < a.nb) mx = max(mx, blk[b]);
+  }
+  part[tid] = mx;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = tid >= off ? part[tid - off] : -1;
+    __syncthreads();
+    part[tid] = max(part[tid], v);
+    __syncthreads();
+  }
+  int run = tid ? part[tid - 1] : -1;
+  for (int i = 0; i < chunk; ++i) {
+    const int b = tid * chunk + i;
+    if (b < a.nb) {
+      const int v = blk[b];
+      blk[b] = run;
+      run = max(run, v);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
   __shared__ double red[kB / 64][kMaxReadout];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -523,17 +610,12 @@ __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
   if (act) {
     if (a.identity) {
       idx = s;
+    } else if (a.sys_mark) {                                // systematic by scan
+      idx = max(a.sys_mark[g0 + s], a.sys_block[f * a.nb + blockIdx.x]);
     } else {
       double u;
-      if (a.systematic) {
-        double u0;
-        if (a.U) {
-          u0 = a.U[0];
-        } else {
-          const uint4 r = philox4x32_10(make_uint4(0u, a.frame, kStreamSystematic, 0u), key);
-          u0 = u01_co(r.x, r.y);
-        }
-        u = ((double)s + u0) / (double)a.P;
+      if (a.systematic) {                    // (search form; the filter resamples by scan)
+        u = sys_u(s, sys_u0(a, f), a.P);
       } else if (a.U) {
         u = a.U[s];
       } else {
@@ -729,7 +811,12 @@ void launch_normalise(const NormArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_cdf, g, dim3(kB), 0, s, a);
 }
 void launch_resample(const ResampleArgs& a, hipStream_t s) {
-  if (!a.identity && a.GB > 0)
+  if (!a.identity && a.sys_mark) {
+    (void)hipMemsetAsync(a.sys_mark, 0xff, sizeof(int) * (size_t)a.P * a.F, s);   // -1: no run starts
+    hipLaunchKernelGGL(k_sys_marks, dim3(nblk(a.P, kB), (unsigned)a.F), dim3(kB), 0, s, a);
+    hipLaunchKernelGGL(k_sys_scan, dim3(nblk(a.P, kB), (unsigned)a.F), dim3(kB), 0, s, a);
+    hipLaunchKernelGGL(k_sys_blocks, dim3((unsigned)a.F), dim3(1024), 0, s, a);
+  } else if (!a.identity && a.GB > 0)
     hipLaunchKernelGGL(k_guide, dim3(nblk(a.GB + 3, kB), (unsigned)a.F), dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_resample, dim3(nblk(a.P, kB), (unsigned)a.F), dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_readout, dim3((unsigned)a.F), dim3(256), 0, s, a);

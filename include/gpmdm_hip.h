@@ -39,7 +39,9 @@ extern "C" {
 #define GPMDM_RNG_PHILOX 1     /* draws generated on the device (Philox4x32-10) */
 
 #define GPMDM_RESAMPLE_MULTINOMIAL 0  /* torch.multinomial(w, P, True): inverse CDF (reference) */
-#define GPMDM_RESAMPLE_SYSTEMATIC 1   /* systematic resampling: one uniform per step */
+#define GPMDM_RESAMPLE_SYSTEMATIC 1   /* systematic resampling: one uniform per step, slot s takes
+                                         the first i with cum_i >= (s + u0) / P; computed by a
+                                         scan over the slots (run starts + max-scan), no search */
 
 typedef struct gpmdm_model* gpmdm_model_t;
 typedef struct gpmdm_pf* gpmdm_pf_t;
