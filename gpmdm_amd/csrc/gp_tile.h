@@ -323,6 +323,8 @@ __device__ __forceinline__ double exp2_64m(double t, const double* tab) {
 //   bit 26: SPEC -- wave-specialised workgroup: NW/2 MFMA waves (the column geometry of an
 //           NW/2-wave shape) and NW/2 producer waves that stage rows and generate K* two
 //           K-steps ahead; no MFMA wave ever issues an exp chain (one workgroup per CU)
+//   bit 27: PRIO -- s_setprio 1 around a K-step's MFMAs, 0 around its generation (the
+//           SIMD arbiter then prefers the other wave's MFMAs while one wave generates)
 //
 // Geometry: NW waves; each wave owns MT x NTW tiles of 16 x 16 (16 MT particles x 16 NTW
 // columns), so a workgroup covers PT = 16 MT particles x NB = 16 NTW NW columns.  K* costs
@@ -658,9 +660,12 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
     constexpr bool GEN2 = (VAR & 33554432) != 0;
     double v2[GV];
     const bool gen_now = !GEN2 || (ks & 1) == 0;
+    constexpr bool PRIO = (VAR & 134217728) != 0;
     if constexpr (!(VAR & 16) && !SPEC) {                // SPEC: producer waves generate
       load_rows(ks + RA, rr);
-      if constexpr (GEN2) {
+      if constexpr (PRIO) {
+        // generation after the MFMAs, at low priority (below)
+      } else if constexpr (GEN2) {
         if (gen_now) {                                  // K-steps ks+2 and ks+3 together
 #pragma unroll
           for (int s2 = 0; s2 < GV; ++s2) {
@@ -672,6 +677,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
         gen(ks + LOOK, grb, v);
       }
     }
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       double af[MT];
@@ -702,6 +708,10 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
         }
       }
       loadB_part(ks + (kk + BR) / 4, (kk + BR) % 4, kk % BR, bb);   // sub-step kk + BR
+    }
+    if constexpr (PRIO && !(VAR & 16) && !SPEC) {
+      __builtin_amdgcn_s_setprio(0);
+      gen(ks + LOOK, grb, v);
     }
     if constexpr (!(VAR & 16) && !SPEC) {
       if constexpr (GEN2) {

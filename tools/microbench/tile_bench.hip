@@ -98,8 +98,9 @@ int main(int argc, char** argv) {
               {launch_var<131072, 8>, 1, "64x512 LDS coords"}};
 #else
   V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512 production"},
-              {launch_var<67108864, 8, 2, 8>, 2, "32x512 SPEC (4 MFMA + 4 producer waves)"},
-              {launch_var<67108864, 8, 4, 4>, 0, "64x256 SPEC"},
+              {launch_var<134217728, 4, 2, 8>, 2, "32x512 PRIO"},
+              {launch_var<0, 4>, 0, "64x256"},
+              {launch_var<134217728, 4>, 0, "64x256 PRIO"},
               {launch_var<16, 4, 2, 8>, 2, "32x512 no gen"}};
 #endif
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
