@@ -274,8 +274,9 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
   // tile shapes: the observation GP defaults to 32x512 (half the kernel-value generation per
   // MFMA of 64x256, tools/microbench/tile_bench.hip); the dynamics GPs use 64-particle tiles
   // (their class-grouped tile starts are computed on the device in 64s, pf_kernels.hip)
-  // (above d = 12 the 32x512 shape's registers spill; 64x512 (8 waves) is the best of the
-  // others there: config 5, d = 16, 0.79 of FP64 peak vs 0.70 for 64x256).  The dynamics
+  // (above d = 12 the 32x512 shape's registers spill -- launch_d then reads its particle
+  // coordinates from LDS -- and 64x512 (8 waves) is the best shape: config 5, d = 16,
+  // 760 ms per launch vs 850 ms for 32x512 with LDS coordinates, tile_ab.sh).  The dynamics
   // GPs run few rows (ancestor de-duplication) against short triangular blocks: their time
   // is the K loop of the heaviest blocks, which narrow particle tiles shorten (64 -> 32 ->
   // 16 particles: dyn GEMM 0.215 -> 0.163 -> 0.150 ms per step at config 2).  Evaluating
@@ -354,19 +355,19 @@ int gpmdm_predict_obs(gpmdm_model_t m, const double* Xs, int64_t n, double* mu, 
   // per-call scratch on the caller's stream (stream-ordered allocation: calls on different
   // streams never share it), freed in stream order after the finish kernel
   double* q = nullptr;
-  HIPCHK(hipMallocAsync((void**)&q, sizeof(double) * (size_t)nparts * n, s));
+  HIPCHK(hipMallocAsync((void**)&q, sizeof(double) * ((size_t)nparts * n + 4), s));
   TileParams tp{};
   tp.seg[0] = m->obs.seg();
   tp.n_seg = 1;
   tp.geo = m->obs.geo;
   tp.tiles_ub = m->obs.tiles(n);
   tp.n_j_max = m->obs.n_j;
-  tp.seg_pos_begin = tp.seg_pos_end = tp.seg_out_base = tp.seg_tile_start = nullptr;   // inline table
-  tp.tab_inline[0] = 0;
-  tp.tab_inline[1] = (int)n;
-  tp.tab_inline[2] = 0;
-  tp.tab_inline[3] = 0;
-  tp.tab_inline[4] = m->obs.tiles(n);
+  int* tab = reinterpret_cast<int*>(q + (size_t)nparts * n);   // segment table after q
+  launch_seg_table(tab, (int)n, m->obs.tiles(n), s);
+  tp.seg_pos_begin = tab + 0;
+  tp.seg_pos_end = tab + 1;
+  tp.seg_out_base = tab + 2;
+  tp.seg_tile_start = tab + 3;
   tp.perm = nullptr;
   tp.X = Xs;
   fill_tile_common(tp, m, false);
@@ -402,19 +403,19 @@ int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, doubl
   const GpImage& g = m->dyn_set(n >= kWideRows)[c];
   const int nparts = g.n_parts();
   double* q = nullptr;                 // per-call scratch, stream-ordered (see gpmdm_predict_obs)
-  HIPCHK(hipMallocAsync((void**)&q, sizeof(double) * (size_t)nparts * n, s));
+  HIPCHK(hipMallocAsync((void**)&q, sizeof(double) * ((size_t)nparts * n + 4), s));
   TileParams tp{};
   tp.seg[0] = g.seg();
   tp.n_seg = 1;
   tp.geo = g.geo;
   tp.tiles_ub = g.tiles(n);
   tp.n_j_max = g.n_j;
-  tp.seg_pos_begin = tp.seg_pos_end = tp.seg_out_base = tp.seg_tile_start = nullptr;   // inline table
-  tp.tab_inline[0] = 0;
-  tp.tab_inline[1] = (int)n;
-  tp.tab_inline[2] = 0;
-  tp.tab_inline[3] = 0;
-  tp.tab_inline[4] = g.tiles(n);
+  int* tab = reinterpret_cast<int*>(q + (size_t)nparts * n);   // segment table after q
+  launch_seg_table(tab, (int)n, g.tiles(n), s);
+  tp.seg_pos_begin = tab + 0;
+  tp.seg_pos_end = tab + 1;
+  tp.seg_out_base = tab + 2;
+  tp.seg_tile_start = tab + 3;
   tp.X = Xs;
   fill_tile_common(tp, m, true);
   tp.qpart = q;

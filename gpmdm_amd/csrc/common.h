@@ -32,7 +32,6 @@ struct TileParams {
   const int* seg_pos_end;         // [n_seg]
   const int* seg_out_base;        // [n_seg]   output row of the first position
   const int* seg_tile_start;      // [n_seg+1] prefix of tiles
-  int tab_inline[5];              // seg_* == nullptr: one segment {begin, end, out_base, tile_start[0..1]}
   const int* perm;                // position -> particle row (nullptr: identity)
   const double* X;                // particle rows, n x d
   double ls[kMaxD];               // RBF lengthscales

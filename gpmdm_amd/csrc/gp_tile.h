@@ -414,15 +414,15 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
   const int b = blockIdx.x;
   const int J = prm.n_j_max - 1 - b / prm.tiles_ub;
   // tile index within this launch's segments (a launch may cover classes c0..c0+7)
-  // segment tables: device arrays (filter: computed on the device), or one segment passed
-  // by value (predictive maps: no host-to-device copy of a table per call)
-  const bool inl = prm.seg_pos_begin == nullptr;
-  auto tile_start = [&](int s) { return inl ? prm.tab_inline[3 + s] : prm.seg_tile_start[s]; };
-  const int t = b - (b / prm.tiles_ub) * prm.tiles_ub + tile_start(0);
+  // segment tables live in device memory (the filter computes them on the device; the
+  // predictive maps write theirs with k_seg_table).  A by-value table with a per-thread
+  // select cost the d = 16 64x512 tile 6.7% through register allocation (tools/microbench/
+  // tile_ab.sh: 760 -> 811 ms per config-5 launch)
+  const int t = b - (b / prm.tiles_ub) * prm.tiles_ub + prm.seg_tile_start[0];
 
   int c = -1;
   for (int s = 0; s < prm.n_seg; ++s)
-    if (t >= tile_start(s) && t < tile_start(s + 1)) c = s;
+    if (t >= prm.seg_tile_start[s] && t < prm.seg_tile_start[s + 1]) c = s;
   c = __builtin_amdgcn_readfirstlane(c);
   if (c < 0) return;
   const int n_j = prm.seg[c].n_j;
@@ -445,10 +445,10 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
   }
   const double* tabl = tab + (TREP > 1 ? (tid & 63) % TREP : 0);   // this lane's copy
 
-  const int seg_begin = inl ? prm.tab_inline[0] : prm.seg_pos_begin[c];
-  const int pos0 = seg_begin + (t - tile_start(c)) * PT;
-  const int pos_end = inl ? prm.tab_inline[1] : prm.seg_pos_end[c];
-  const int out_base = (inl ? prm.tab_inline[2] : prm.seg_out_base[c]) - seg_begin;   // out = out_base + pos
+  const int seg_begin = prm.seg_pos_begin[c];
+  const int pos0 = seg_begin + (t - prm.seg_tile_start[c]) * PT;
+  const int pos_end = prm.seg_pos_end[c];
+  const int out_base = prm.seg_out_base[c] - seg_begin;   // out = out_base + pos
 
   // ---- this thread's particle (generation role: particle m, rows g + NG s) ----------
   const int m = gtid % PT;
@@ -1022,11 +1022,16 @@ template <int DI>
 void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
   const dim3 grid((unsigned)(p.n_j_max * p.tiles_ub));
   const TileGeo g = p.geo;
+  // 32 x 512 tiles above d = 12 (GPMDM_TILE_32x512, or wide dynamics images of such a
+  // model): particle coordinates from LDS (VAR bit 17) -- in VGPRs they push the
+  // 2-workgroup register budget into spills (config-5 shape, d = 16: 850 ms per launch vs
+  // 1037 ms; the default 64 x 512 shape: 760 ms; profiles/r02/ablations/tb9, tb10)
+  constexpr int kCoordVar = DI > 12 ? 131072 : 0;
   if (dyn) {
     if (g.nw == 8)
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 8>), grid, dim3(512), 0, stream, p);
     else if (g.mt == 2 && g.ntw == 8)
-      hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 2, 8>), grid, dim3(256), 0, stream, p);
+      hipLaunchKernelGGL((k_gp_tile<DI, true, kCoordVar, 4, 2, 8>), grid, dim3(256), 0, stream, p);
     else if (g.mt == 2)
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 2, 4>), grid, dim3(256), 0, stream, p);
     else if (g.mt == 1)
@@ -1034,7 +1039,7 @@ void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
     else
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4>), grid, dim3(256), 0, stream, p);
   } else if (g.mt == 2) {
-    hipLaunchKernelGGL((k_gp_tile<DI, false, 0, 4, 2, 8>), grid, dim3(256), 0, stream, p);
+    hipLaunchKernelGGL((k_gp_tile<DI, false, kCoordVar, 4, 2, 8>), grid, dim3(256), 0, stream, p);
   } else if (g.nw == 8) {
     hipLaunchKernelGGL((k_gp_tile<DI, false, 0, 8>), grid, dim3(512), 0, stream, p);
   } else {

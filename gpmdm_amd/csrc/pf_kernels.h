@@ -225,6 +225,8 @@ void launch_normalise(const NormArgs& a, hipStream_t s);
 void launch_resample(const ResampleArgs& a, hipStream_t s);
 void launch_pack(const PackArgs& a, hipStream_t s);
 // predict(): per-block class histogram of `cls` (blockcounts nb x C, nb = ceil(P / 256))
+// single-segment tile table {0, n, 0, 0, tiles} at t[0..4] (predictive maps)
+void launch_seg_table(int* t, int n, int tiles, hipStream_t s);
 void launch_class_hist(const int* cls, long long P, int C, int* blockcounts, hipStream_t s);
 // predict(): rows of mu (grouped order, perm: row -> particle) scattered to particle order,
 // then per filter the mean over its Pf particles (fixed-order reduction) into out (F x d)

@@ -760,8 +760,19 @@ __global__ __launch_bounds__(kB) void k_predict_mean(const double* mu_p, double*
   }
 }
 
+// One-segment table of a predictive map, written in stream order (no host-to-device copy
+// of a host array per call): {pos_begin, pos_end, out_base, tile_start[0], tile_start[1]}.
+__global__ void k_seg_table(int* t, int n, int tiles) {
+  const int i = threadIdx.x;
+  if (i < 5) t[i] = i == 1 ? n : (i == 4 ? tiles : 0);
+}
+
 // ---------------------------------------------------------------------------------
 static inline unsigned nblk(long long n, int b) { return (unsigned)((n + b - 1) / b); }
+
+void launch_seg_table(int* t, int n, int tiles, hipStream_t s) {
+  hipLaunchKernelGGL(k_seg_table, dim3(1), dim3(64), 0, s, t, n, tiles);
+}
 
 void launch_class_hist(const int* cls, long long P, int C, int* blockcounts, hipStream_t s) {
   hipLaunchKernelGGL(k_class_hist, dim3(nblk(P, kB)), dim3(kB), 0, s, cls, P, C, blockcounts);

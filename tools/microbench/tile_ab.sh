@@ -1,0 +1,24 @@
+#!/bin/bash
+# Build tile_ab.hip against gp_tile.h as of several commits (WT = the working tree), here:
+#   bash tools/microbench/tile_ab.sh build <commit>...
+# and run them alternately on the GPU box:  bash tools/microbench/tile_ab.sh run
+set -e
+cd "$(dirname "$0")/../.."
+out=tools/microbench/ab
+if [ "$1" = build ]; then
+  shift; rm -rf $out; mkdir -p $out
+  for c in "$@"; do
+    src=/tmp/tile_ab_src/$c; rm -rf $src; mkdir -p $src
+    if [ $c = WT ]; then cp -r gpmdm_amd include $src/; else git archive $c gpmdm_amd/csrc include | tar -x -C $src; fi
+    for d in 3 16; do
+      /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I $src/include -DTB_D=$d \
+        "-DGP_TILE_H=\"$src/gpmdm_amd/csrc/gp_tile.h\"" tools/microbench/tile_ab.hip -o $out/tile_ab_d${d}_$c &
+    done
+  done
+  wait; ls $out
+else
+  for r in 1 2; do
+    for b in $out/tile_ab_d16_*; do echo "== $b"; timeout -k 10 170 $b 125000 20000 256 | grep median; done
+    for b in $out/tile_ab_d3_*; do echo "== $b"; timeout -k 10 60 $b | grep median; done
+  done
+fi
