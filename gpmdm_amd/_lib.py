@@ -22,6 +22,7 @@ GPMDM_RNG_REPLAY = 0
 GPMDM_RNG_PHILOX = 1
 GPMDM_RESAMPLE_MULTINOMIAL = 0
 GPMDM_RESAMPLE_SYSTEMATIC = 1
+GPMDM_PACK_ALL, GPMDM_PACK_STATES, GPMDM_PACK_LL = 0, 1, 2
 DYN_TILES = {"auto": 0, "narrow": 1, "wide": 2}
 STAGES = ("switch", "dyn_gemm", "dyn_finish", "obs_gemm", "obs_finish", "resample")
 HEALTH = ("obs_var_nonpositive", "obs_ll_nonfinite", "dyn_var_nonpositive", "dyn_state_nonfinite")
@@ -53,9 +54,13 @@ _SIGS = {
     "gpmdm_pf_init": (c_int, [c_void_p, _dp, _i64p]),
     "gpmdm_pf_switch": (c_int, [c_void_p, _dp, _i64p, c_void_p]),
     "gpmdm_pf_propagate": (c_int, [c_void_p, _dp, _dp, c_void_p]),
+    "gpmdm_pf_propagate_dynamics": (c_int, [c_void_p, _dp, c_void_p]),
+    "gpmdm_pf_weigh": (c_int, [c_void_p, _dp, c_void_p]),
     "gpmdm_pf_exchange_width": (c_int, [c_void_p, _i64p, _i64p, _i64p]),
     "gpmdm_pf_pack": (c_int, [c_void_p, c_void_p, c_void_p]),
     "gpmdm_pf_unpack": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "gpmdm_pf_pack_part": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
+    "gpmdm_pf_unpack_part": (c_int, [c_void_p, c_void_p, c_int, c_void_p]),
     "gpmdm_pf_resample": (c_int, [c_void_p, _dp, c_void_p]),
     "gpmdm_pf_step": (c_int, [c_void_p, _dp, _dp, _dp, _dp, c_void_p]),
     "gpmdm_pf_read": (c_int, [c_void_p, _dp, _dp, _dp, c_void_p]),

@@ -145,6 +145,7 @@ struct gpmdm_pf {
   int n_ranks = 1, rank = 0, rng_mode = 0, resample_mode = 0, nb = 0, nbf = 0;
   unsigned seed_lo = 0, seed_hi = 0, frame = 0;
   bool initialised = false, switched = false, propagated = false;
+  bool dyn_done = false;             // gpmdm_pf_propagate_dynamics ran, gpmdm_pf_weigh not yet
   bool dedup = true;                  // ancestor de-duplication of the dynamics GP
   int dyn_tiles = GPMDM_DYN_TILES_AUTO;   // gpmdm_pf_set_dyn_tiles
   bool wide_dyn() const { return dyn_tiles == GPMDM_DYN_TILES_WIDE || (dyn_tiles == GPMDM_DYN_TILES_AUTO && !dedup); }
@@ -647,7 +648,7 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   HIPCHK(hipDeviceSynchronize());
   pf->initialised = true;
   pf->own_valid = false;               // no ancestors yet: identity ownership
-  pf->switched = pf->propagated = false;
+  pf->switched = pf->propagated = pf->dyn_done = false;
   return GPMDM_OK;
 }
 
@@ -763,21 +764,11 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   return GPMDM_OK;
 }
 
-int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, void* stream) {
-  CHECK(pf && zh, "null argument");
-  if (!pf->switched) return fail(GPMDM_E_STATE, "propagate called before switch");
+// _propogate_dynamics for this rank's particles (gpmdm_pf.py:153-168): the dynamics GP per
+// class (de-duplicated rows or every particle) and the new states X_prop.
+static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s) {
   gpmdm_model* m = pf->m;
-  hipStream_t s = (hipStream_t)stream;
-  HIPCHK(hipSetDevice(m->device));
-  const int C = m->C, d = m->d, D = m->D;
-  {
-    const int k = pf->zslot;
-    HIPCHK(hipEventSynchronize(pf->zev[k]));      // the slot's previous upload has run
-    std::memcpy(pf->zpin[k], zh, sizeof(double) * D * pf->F);
-    HIPCHK(hipMemcpyAsync(pf->z, pf->zpin[k], sizeof(double) * D * pf->F, hipMemcpyHostToDevice, s));
-    HIPCHK(hipEventRecord(pf->zev[k], s));
-    pf->zslot ^= 1;
-  }
+  const int C = m->C, d = m->d;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
     CHECK(normals, "replay mode needs the dynamics normals");
     HIPCHK(hipMemcpyAsync(pf->normals, normals, sizeof(double) * pf->P * d, hipMemcpyHostToDevice, s));
@@ -854,6 +845,29 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     launch_dyn_finish(fa, s);
     pf->mark_end(s, GPMDM_STAGE_DYN_FINISH, t0);
 
+  }
+  HIPCHK(hipGetLastError());
+  pf->dyn_done = true;
+  pf->switched = false;
+  return GPMDM_OK;
+}
+
+// _update_weights' likelihoods for this rank's particles (gpmdm_pf.py:170-192): uploads z,
+// runs the observation GP tile and the likelihood finish.
+static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
+  gpmdm_model* m = pf->m;
+  const int d = m->d, D = m->D;
+  hipEvent_t t0;
+  {
+    const int k = pf->zslot;
+    HIPCHK(hipEventSynchronize(pf->zev[k]));      // the slot's previous upload has run
+    std::memcpy(pf->zpin[k], zh, sizeof(double) * D * pf->F);
+    HIPCHK(hipMemcpyAsync(pf->z, pf->zpin[k], sizeof(double) * D * pf->F, hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(pf->zev[k], s));
+    pf->zslot ^= 1;
+  }
+  const long long nl = pf->nloc;
+  if (nl > 0) {
     // ---- observation GP + likelihood over particles [lo, hi) ----
     pf->mark_begin(s, GPMDM_STAGE_OBS_GEMM, t0);
     TileParams tp{};
@@ -901,8 +915,32 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
   }
   HIPCHK(hipGetLastError());
   pf->propagated = true;
-  pf->switched = false;
+  pf->dyn_done = false;
   return GPMDM_OK;
+}
+
+int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, void* stream) {
+  CHECK(pf && zh, "null argument");
+  if (!pf->switched) return fail(GPMDM_E_STATE, "propagate called before switch");
+  if (pf->rng_mode == GPMDM_RNG_REPLAY) CHECK(normals, "replay mode needs the dynamics normals");
+  HIPCHK(hipSetDevice(pf->m->device));
+  const int rc = propagate_dynamics(pf, normals, (hipStream_t)stream);
+  return rc ? rc : weigh(pf, zh, (hipStream_t)stream);
+}
+
+int gpmdm_pf_propagate_dynamics(gpmdm_pf_t pf, const double* normals, void* stream) {
+  CHECK(pf, "null handle");
+  if (!pf->switched) return fail(GPMDM_E_STATE, "propagate_dynamics called before switch");
+  if (pf->rng_mode == GPMDM_RNG_REPLAY) CHECK(normals, "replay mode needs the dynamics normals");
+  HIPCHK(hipSetDevice(pf->m->device));
+  return propagate_dynamics(pf, normals, (hipStream_t)stream);
+}
+
+int gpmdm_pf_weigh(gpmdm_pf_t pf, const double* zh, void* stream) {
+  CHECK(pf && zh, "null argument");
+  if (!pf->dyn_done) return fail(GPMDM_E_STATE, "weigh called before propagate_dynamics");
+  HIPCHK(hipSetDevice(pf->m->device));
+  return weigh(pf, zh, (hipStream_t)stream);
 }
 
 int gpmdm_pf_exchange_width(gpmdm_pf_t pf, int64_t* width, int64_t* lo, int64_t* hi) {
@@ -914,7 +952,16 @@ int gpmdm_pf_exchange_width(gpmdm_pf_t pf, int64_t* width, int64_t* lo, int64_t*
 }
 
 int gpmdm_pf_pack(gpmdm_pf_t pf, double* send, void* stream) {
+  return gpmdm_pf_pack_part(pf, send, GPMDM_PACK_ALL, stream);
+}
+
+int gpmdm_pf_unpack(gpmdm_pf_t pf, const double* recv, void* stream) {
+  return gpmdm_pf_unpack_part(pf, recv, GPMDM_PACK_ALL, stream);
+}
+
+int gpmdm_pf_pack_part(gpmdm_pf_t pf, double* send, int part, void* stream) {
   CHECK(pf && send, "null argument");
+  CHECK(part >= GPMDM_PACK_ALL && part <= GPMDM_PACK_LL, "part must be GPMDM_PACK_*");
   HIPCHK(hipSetDevice(pf->m->device));
   PackArgs a{};
   a.n = pf->nloc;
@@ -922,6 +969,7 @@ int gpmdm_pf_pack(gpmdm_pf_t pf, double* send, void* stream) {
   a.d = pf->m->d;
   a.own = pf->own_order();
   a.buf = send;
+  a.part = part;
   a.ll = pf->ll;
   a.cls = pf->cls_new;
   a.X = pf->X_prop;
@@ -930,8 +978,9 @@ int gpmdm_pf_pack(gpmdm_pf_t pf, double* send, void* stream) {
   return GPMDM_OK;
 }
 
-int gpmdm_pf_unpack(gpmdm_pf_t pf, const double* recv, void* stream) {
+int gpmdm_pf_unpack_part(gpmdm_pf_t pf, const double* recv, int part, void* stream) {
   CHECK(pf && recv, "null argument");
+  CHECK(part >= GPMDM_PACK_ALL && part <= GPMDM_PACK_LL, "part must be GPMDM_PACK_*");
   HIPCHK(hipSetDevice(pf->m->device));
   PackArgs a{};
   a.n = pf->P;
@@ -939,6 +988,7 @@ int gpmdm_pf_unpack(gpmdm_pf_t pf, const double* recv, void* stream) {
   a.d = pf->m->d;
   a.own = pf->own_order();
   a.buf = const_cast<double*>(recv);
+  a.part = part;
   a.ll = pf->ll;
   a.cls = pf->cls_new;
   a.X = pf->X_prop;
@@ -1046,7 +1096,7 @@ int gpmdm_pf_export(gpmdm_pf_t pf, double* states, int64_t* classes, double* ll,
 
 int gpmdm_pf_set_dedup(gpmdm_pf_t pf, int enable) {
   CHECK(pf, "null handle");
-  if (pf->switched) return fail(GPMDM_E_STATE, "set_dedup between switch and propagate");
+  if (pf->switched || pf->dyn_done) return fail(GPMDM_E_STATE, "set_dedup between switch and propagate");
   pf->dedup = enable != 0;
   return GPMDM_OK;
 }
@@ -1055,14 +1105,14 @@ int gpmdm_pf_set_dyn_tiles(gpmdm_pf_t pf, int mode) {
   CHECK(pf, "null handle");
   CHECK(mode == GPMDM_DYN_TILES_AUTO || mode == GPMDM_DYN_TILES_NARROW || mode == GPMDM_DYN_TILES_WIDE,
         "mode must be GPMDM_DYN_TILES_*");
-  if (pf->switched) return fail(GPMDM_E_STATE, "set_dyn_tiles between switch and propagate");
+  if (pf->switched || pf->dyn_done) return fail(GPMDM_E_STATE, "set_dyn_tiles between switch and propagate");
   pf->dyn_tiles = mode;
   return GPMDM_OK;
 }
 
 int gpmdm_pf_set_shard_order(gpmdm_pf_t pf, int enable) {
   CHECK(pf, "null handle");
-  if (pf->switched || pf->propagated) return fail(GPMDM_E_STATE, "set_shard_order inside a step");
+  if (pf->switched || pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "set_shard_order inside a step");
   pf->shard_order = enable != 0;
   if (!pf->shard_order) pf->own_valid = false;
   return GPMDM_OK;
@@ -1123,7 +1173,7 @@ int gpmdm_pf_frame(gpmdm_pf_t pf, int64_t* frame) {
 
 int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
   CHECK(pf && m, "null argument");
-  if (pf->switched || pf->propagated) return fail(GPMDM_E_STATE, "set_model inside a step");
+  if (pf->switched || pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "set_model inside a step");
   gpmdm_model* old = pf->m;
   if (m == old) return GPMDM_OK;
   CHECK(m->C == old->C && m->d == old->d && m->D == old->D,
@@ -1178,7 +1228,7 @@ int gpmdm_pf_health(gpmdm_pf_t pf, int64_t* counts, int reset, void* stream) {
 int gpmdm_pf_predict(gpmdm_pf_t pf, double* mean, void* stream) {
   CHECK(pf && mean, "null argument");
   if (!pf->initialised) return fail(GPMDM_E_STATE, "particle filter not initialised");
-  if (pf->switched || pf->propagated) return fail(GPMDM_E_STATE, "predict inside a step");
+  if (pf->switched || pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "predict inside a step");
   gpmdm_model* m = pf->m;
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;

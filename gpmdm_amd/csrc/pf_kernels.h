@@ -1,6 +1,7 @@
 // Argument blocks and launchers of the particle-filter kernels (pf_kernels.hip).
 #pragma once
 
+#include "../../include/gpmdm_hip.h"
 #include "common.h"
 
 namespace gpmdm {
@@ -203,6 +204,7 @@ struct PackArgs {
   int d;
   const int* own;                 // row r holds particle own[lo + r] (nullptr: identity)
   double* buf;
+  int part;                       // GPMDM_PACK_*: {ll, class, X} | {class, X} | {ll}
   double* ll;
   int* cls;
   double* X;

@@ -702,20 +702,28 @@ __global__ __launch_bounds__(kB) void k_pack(PackArgs a) {
   const long long r = (long long)blockIdx.x * kB + threadIdx.x;
   if (r >= a.n) return;
   const long long p = a.own ? a.own[a.lo + r] : a.lo + r;
-  double* o = a.buf + r * (a.d + 2);
-  o[0] = a.ll[p];
-  o[1] = (double)a.cls[p];
-  for (int j = 0; j < a.d; ++j) o[2 + j] = a.X[p * a.d + j];
+  const int lo = a.part == GPMDM_PACK_STATES ? 1 : 0;            // first column present
+  const int hi = a.part == GPMDM_PACK_LL ? 1 : a.d + 2;           // one past the last
+  double* o = a.buf + r * (hi - lo);                              // o[k - lo]: column k
+  if (lo == 0) o[0] = a.ll[p];
+  if (hi > 1) {
+    o[1 - lo] = (double)a.cls[p];
+    for (int j = 0; j < a.d; ++j) o[2 - lo + j] = a.X[p * a.d + j];
+  }
 }
 
 __global__ __launch_bounds__(kB) void k_unpack(PackArgs a) {
   const long long r = (long long)blockIdx.x * kB + threadIdx.x;   // row = ownership position
   if (r >= a.n) return;
   const long long p = a.own ? a.own[r] : r;
-  const double* i = a.buf + r * (a.d + 2);
-  a.ll[p] = i[0];
-  a.cls[p] = (int)i[1];
-  for (int j = 0; j < a.d; ++j) a.X[p * a.d + j] = i[2 + j];
+  const int lo = a.part == GPMDM_PACK_STATES ? 1 : 0;
+  const int hi = a.part == GPMDM_PACK_LL ? 1 : a.d + 2;
+  const double* i = a.buf + r * (hi - lo);
+  if (lo == 0) a.ll[p] = i[0];
+  if (hi > 1) {
+    a.cls[p] = (int)i[1 - lo];
+    for (int j = 0; j < a.d; ++j) a.X[p * a.d + j] = i[2 - lo + j];
+  }
 }
 
 // ---------------------------------------------------------------------------------

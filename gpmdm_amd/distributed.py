@@ -1,11 +1,13 @@
 """Particle sharding over ranks (one process per GPU).
 
 Rank r owns particles [r*P/R, (r+1)*P/R) of the dynamics and observation GPs; the
-filter state is replicated.  Once per frame every rank packs its rows {ll, class,
-state[d]} (gpmdm_pf_pack) and one all-gather builds the full P x (d+2) array that every
-rank unpacks (gpmdm_pf_unpack) before the identical, replicated normalise/resample.  With
-the nccl backend (RCCL over xGMI) the tensors live on the GPU and the collective runs on
-torch's current stream, the same stream the library launches on.
+filter state is replicated.  Once per frame every rank's rows {ll, class, state[d]} are
+all-gathered into the full P-row array that every rank unpacks before the identical,
+replicated normalise/resample.  GPMDM_PF splits the rows in two: {class, state[d]} is known
+after the dynamics GP and is all-gathered while the observation GP runs (allgather_rows_start:
+with the nccl backend -- RCCL over xGMI -- the collective runs on RCCL's own stream, ordered
+after the packing kernel and joined back to torch's current stream, the stream the library
+launches on); only {ll} (8 bytes per particle) is exchanged after it.
 """
 from __future__ import annotations
 
@@ -67,3 +69,33 @@ def allgather_rows(recv: torch.Tensor, send: torch.Tensor, group=None) -> None:
     for r, s in enumerate(sizes):
         recv[off: off + s] = parts[r][:s]
         off += s
+
+
+def allgather_rows_start(recv: torch.Tensor, send: torch.Tensor, group=None):
+    """Start allgather_rows(recv, send); returns ``wait()``, after which recv is valid on the
+    current stream.  nccl: asynchronous (the collective overlaps the kernels the caller
+    launches before wait(); wait() orders the current stream after it, without blocking the
+    host).  gloo: done before returning (wait() is a no-op)."""
+    import torch.distributed as dist
+    if dist.get_backend(group) == "gloo":
+        allgather_rows(recv, send, group)
+        return lambda: None
+    world = dist.get_world_size(group)
+    P, W = recv.shape
+    sizes = [shard_range(P, world, r)[1] - shard_range(P, world, r)[0] for r in range(world)]
+    mx = max(sizes)
+    if all(s == mx for s in sizes):
+        work = dist.all_gather_into_tensor(recv, send, group=group, async_op=True)
+        return work.wait
+    padded = torch.zeros((mx, W), dtype=send.dtype, device=send.device)
+    padded[: send.shape[0]] = send
+    parts = [torch.empty_like(padded) for _ in range(world)]
+    work = dist.all_gather(parts, padded, group=group, async_op=True)
+
+    def wait():
+        work.wait()
+        off = 0
+        for r, s in enumerate(sizes):
+            recv[off: off + s] = parts[r][:s]
+            off += s
+    return wait

@@ -10,7 +10,8 @@ every per-frame computation runs in the HIP library.  Extra keyword options:
 * ``seed``: Philox key (default: drawn from torch's generator);
 * ``resample='multinomial'`` (reference, gpmdm_pf.py:211) or ``'systematic'``;
 * ``process_group``: a ``torch.distributed`` group to shard particles over (one process
-  per GPU; one all-gather of the packed particle rows per frame).  The Philox seed and
+  per GPU; per frame, the new {class, state} rows are all-gathered while the observation GP
+  runs and the likelihoods after it).  The Philox seed and
   the initial particles are broadcast from the group's rank 0, so every rank holds the
   same replicated filter whatever its local torch RNG state; replay mode (``rng='torch'``)
   consumes the host generator on every rank and therefore requires identical torch RNG
@@ -113,8 +114,14 @@ class GPMDM_PF:
             w, lo, hi = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
             lib.gpmdm_pf_exchange_width(h, ctypes.byref(w), ctypes.byref(lo), ctypes.byref(hi))
             dev = self.device
-            self._send = torch.empty((hi.value - lo.value, w.value), dtype=torch.float64, device=dev)
-            self._recv = torch.empty((self._num_particles, w.value), dtype=torch.float64, device=dev)
+            n_loc, P = hi.value - lo.value, self._num_particles
+            self._send = torch.empty((n_loc, w.value), dtype=torch.float64, device=dev)
+            self._recv = torch.empty((P, w.value), dtype=torch.float64, device=dev)
+            # the split exchange: {class, state} during the observation GP, then {ll}
+            self._send_s = torch.empty((n_loc, w.value - 1), dtype=torch.float64, device=dev)
+            self._recv_s = torch.empty((P, w.value - 1), dtype=torch.float64, device=dev)
+            self._send_l = torch.empty((n_loc, 1), dtype=torch.float64, device=dev)
+            self._recv_l = torch.empty((P, 1), dtype=torch.float64, device=dev)
         self._init_particles()
 
     def __del__(self):
@@ -175,14 +182,12 @@ class GPMDM_PF:
             counts = np.zeros(C, dtype=np.int64)
             _lib.check(lib.gpmdm_pf_switch(h, _lib.dptr(E), _lib.i64ptr(counts), s), "switch")
             normals = np.ascontiguousarray(replay.dynamics_draws(counts, d))
-            _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), _lib.dptr(normals), s), "propagate")
-            self._exchange(s)
+            self._propagate(z, normals, s)
             U = replay.resample_draws(P if self._resample_mode == "multinomial" else 1)
             _lib.check(lib.gpmdm_pf_resample(h, _lib.dptr(np.ascontiguousarray(U)), s), "resample")
         else:
             _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
-            _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), None, s), "propagate")
-            self._exchange(s)
+            self._propagate(z, None, s)
             _lib.check(lib.gpmdm_pf_resample(h, None, s), "resample")
         self._readout = None
 
@@ -201,23 +206,37 @@ class GPMDM_PF:
         E = np.ascontiguousarray(exp_draws, dtype=np.float64).reshape(P, C)
         _lib.check(lib.gpmdm_pf_switch(h, _lib.dptr(E), None, s), "switch")
         nrm = np.ascontiguousarray(normals, dtype=np.float64).reshape(P, d)
-        _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), _lib.dptr(nrm), s), "propagate")
-        self._exchange(s)
+        self._propagate(z, nrm, s)
         U = np.ascontiguousarray(uniforms, dtype=np.float64).reshape(-1)
         _lib.check(lib.gpmdm_pf_resample(h, _lib.dptr(U), s), "resample")
         self._readout = None
 
-    def _exchange(self, s):
+    def _propagate(self, z, normals, s):
+        """gpmdm_pf.py:153-192 for this rank's particles, and on several ranks the exchange:
+        the new {class, state} rows are all-gathered while the observation GP runs (they are
+        final once the dynamics GP is done), the likelihoods after it."""
+        lib, h = _lib.load(), self._h
+        nrm = None if normals is None else _lib.dptr(normals)
         if self._world == 1:
+            _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), nrm, s), "propagate")
             return
-        lib = _lib.load()
-        _lib.check(lib.gpmdm_pf_pack(self._h, self._send.data_ptr(), s), "pack")
+        _lib.check(lib.gpmdm_pf_propagate_dynamics(h, nrm, s), "propagate_dynamics")
+        _lib.check(lib.gpmdm_pf_pack_part(h, self._send_s.data_ptr(), _lib.GPMDM_PACK_STATES, s), "pack")
+        states_done = self._gather(self._recv_s, self._send_s)
+        _lib.check(lib.gpmdm_pf_weigh(h, _lib.dptr(z), s), "weigh")
+        _lib.check(lib.gpmdm_pf_pack_part(h, self._send_l.data_ptr(), _lib.GPMDM_PACK_LL, s), "pack")
+        self._gather(self._recv_l, self._send_l)()
+        states_done()
+        _lib.check(lib.gpmdm_pf_unpack_part(h, self._recv_s.data_ptr(), _lib.GPMDM_PACK_STATES, s), "unpack")
+        _lib.check(lib.gpmdm_pf_unpack_part(h, self._recv_l.data_ptr(), _lib.GPMDM_PACK_LL, s), "unpack")
+
+    def _gather(self, recv, send):
+        """Start the all-gather of recv <- send; returns the function that completes it."""
         if self._exchange_fn is not None:
-            self._exchange_fn(self._recv, self._send)
-        else:
-            from .distributed import allgather_rows
-            allgather_rows(self._recv, self._send, self._group)
-        _lib.check(lib.gpmdm_pf_unpack(self._h, self._recv.data_ptr(), s), "unpack")
+            self._exchange_fn(recv, send)
+            return lambda: None
+        from .distributed import allgather_rows_start
+        return allgather_rows_start(recv, send, self._group)
 
     # staged update for callers that drive the exchange themselves (tests, schedulers)
     def _stage_propagate(self, z):

@@ -138,11 +138,23 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* exp_draws, int64_t* class_count
  * per-class order (replay) or NULL (philox). */
 int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* z, const double* normals, void* stream);
 
+/* gpmdm_pf_propagate in two halves, so a multi-rank caller can exchange the new states
+ * while the observation GP runs: propagate_dynamics = _propogate_dynamics
+ * (gpmdm_pf.py:153-168; normals as for gpmdm_pf_propagate), weigh = _update_weights'
+ * likelihoods (gpmdm_pf.py:170-192).  switch -> propagate_dynamics -> weigh -> resample. */
+int gpmdm_pf_propagate_dynamics(gpmdm_pf_t pf, const double* normals, void* stream);
+int gpmdm_pf_weigh(gpmdm_pf_t pf, const double* z, void* stream);
+
 /* Multi-rank exchange: pack this rank's rows [lo, hi) as (hi-lo) x (d+2) doubles
- * {ll, class, state[d]}; unpack all P rows after an all-gather. */
+ * {ll, class, state[d]}; unpack all P rows after an all-gather.  The _part forms move
+ * column subsets: GPMDM_PACK_STATES = {class, state[d]} (d+1 wide; valid after
+ * propagate_dynamics), GPMDM_PACK_LL = {ll} (1 wide; valid after weigh). */
+enum { GPMDM_PACK_ALL = 0, GPMDM_PACK_STATES = 1, GPMDM_PACK_LL = 2 };
 int gpmdm_pf_exchange_width(gpmdm_pf_t pf, int64_t* width, int64_t* lo, int64_t* hi);
 int gpmdm_pf_pack(gpmdm_pf_t pf, double* send_dev, void* stream);
 int gpmdm_pf_unpack(gpmdm_pf_t pf, const double* recv_dev, void* stream);
+int gpmdm_pf_pack_part(gpmdm_pf_t pf, double* send_dev, int part, void* stream);
+int gpmdm_pf_unpack_part(gpmdm_pf_t pf, const double* recv_dev, int part, void* stream);
 
 /* _update_weights' normalisation + _resample + the read-outs  (gpmdm_pf.py:194-262,
  * 302-312).  uniforms: P host (replay, multinomial), 1 host (replay, systematic) or NULL. */

@@ -29,6 +29,14 @@ def _worker(rank, world, port, P, W, out_q):
         recv = torch.full((P, W), -1.0, dtype=torch.float64)
         allgather_rows(recv, send)
         ok_rows = bool(torch.equal(recv, torch.arange(P * W, dtype=torch.float64).reshape(P, W)))
+        # the split exchange's start/wait form (GPMDM_PF._propagate): {class, state} columns
+        # started first, {ll} gathered and waited, then the first completed
+        from gpmdm_amd.distributed import allgather_rows_start
+        rs, rl = torch.full((P, W - 1), -1.0, dtype=torch.float64), torch.full((P, 1), -1.0, dtype=torch.float64)
+        wait_s = allgather_rows_start(rs, send[:, 1:].contiguous())
+        allgather_rows_start(rl, send[:, :1].contiguous())()
+        wait_s()
+        ok_rows = ok_rows and bool(torch.equal(torch.cat([rl, rs], 1), recv))
         # replicated draws: every rank seeds torch identically and draws the same streams
         torch.manual_seed(123)
         E = replay.switch_draws(P, 3)

@@ -414,16 +414,39 @@ def test_tiny_model_and_particle_counts(P):
         assert nrel(pf.current_state_mean().numpy(), r.mean) < 1e-6, k
 
 
-@pytest.mark.parametrize("world,rng_mode,order,P", [(4, "philox", True, 10_007), (8, "philox", True, 10_007),
-                                                    (8, "philox", False, 10_007), (3, "torch", True, 10_007),
-                                                    (8, "philox", True, 400_003)])
-def test_logical_shards_match_one_rank(m2, world, rng_mode, order, P):
+def _split_exchange(lib, ranks, z):
+    """In-process stand-in for GPMDM_PF._propagate's two all-gathers over logical shards."""
+    from gpmdm_amd import _lib
+    for pf in ranks:
+        _lib.check(lib.gpmdm_pf_pack_part(pf._h, pf._send_s.data_ptr(), _lib.GPMDM_PACK_STATES, pf._stream()), "pack")
+    states = torch.cat([pf._send_s for pf in ranks], 0)    # complete before any rank weighs
+    for pf in ranks:
+        h, s = pf._h, pf._stream()
+        _lib.check(lib.gpmdm_pf_weigh(h, _lib.dptr(z), s), "weigh")
+        _lib.check(lib.gpmdm_pf_pack_part(h, pf._send_l.data_ptr(), _lib.GPMDM_PACK_LL, s), "pack")
+    ll = torch.cat([pf._send_l for pf in ranks], 0)
+    for pf in ranks:
+        h, s = pf._h, pf._stream()
+        pf._recv_s.copy_(states)
+        pf._recv_l.copy_(ll)
+        _lib.check(lib.gpmdm_pf_unpack_part(h, pf._recv_s.data_ptr(), _lib.GPMDM_PACK_STATES, s), "unpack")
+        _lib.check(lib.gpmdm_pf_unpack_part(h, pf._recv_l.data_ptr(), _lib.GPMDM_PACK_LL, s), "unpack")
+
+
+@pytest.mark.parametrize("world,rng_mode,order,P,split", [
+    (4, "philox", True, 10_007, False), (8, "philox", True, 10_007, False), (8, "philox", False, 10_007, False),
+    (3, "torch", True, 10_007, False), (8, "philox", True, 400_003, False),
+    (4, "philox", True, 10_007, True), (3, "torch", True, 10_007, True)])
+def test_logical_shards_match_one_rank(m2, world, rng_mode, order, P, split):
     """results at R ranks equal the single-rank filter, with R logical shards
     on one GPU and the all-gather done in-process.  Philox draws at 4 and 8 ranks; the
     replay stream (torch generator) at 3 ranks, every rank drawing the same full streams
     in the reference's order (gpmdm_amd.replay).  P = 10007 (uneven shards).  Philox ranks
     run with and without ancestor-ordered shards (``shard_order``); P = 400003 at 8 ranks
-    exercises the bucket pass at bench scale and the guide-table resample search."""
+    exercises the bucket pass at bench scale and the guide-table resample search.
+    ``split``: the exchange GPMDM_PF uses on a process group -- {class, state} rows packed
+    after gpmdm_pf_propagate_dynamics and gathered before any rank's gpmdm_pf_weigh, {ll}
+    after it (gpmdm_pf_pack_part / unpack_part)."""
     from gpmdm_amd import GPMDM_PF, _lib, replay
     T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
     Y = m2.get_Y()
@@ -448,16 +471,33 @@ def test_logical_shards_match_one_rank(m2, world, rng_mode, order, P):
                 counts = np.zeros(2, dtype=np.int64)
                 _lib.check(lib.gpmdm_pf_switch(h, _lib.dptr(E), _lib.i64ptr(counts), s), "switch")
                 nrm = np.ascontiguousarray(replay.dynamics_draws(counts, m2.d))
-                _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), _lib.dptr(nrm), s), "propagate")
-                _lib.check(lib.gpmdm_pf_pack(h, pf._send.data_ptr(), s), "pack")
+                if split:
+                    _lib.check(lib.gpmdm_pf_propagate_dynamics(h, _lib.dptr(nrm), s), "propagate_dynamics")
+                else:
+                    _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), _lib.dptr(nrm), s), "propagate")
+                    _lib.check(lib.gpmdm_pf_pack(h, pf._send.data_ptr(), s), "pack")
                 draws_u.append(np.ascontiguousarray(replay.resample_draws(P)))
             assert torch.equal(torch.get_rng_state(), after)
-            full = torch.cat([pf._send for pf in ranks], 0)
+            if split:
+                _split_exchange(lib, ranks, z)
+            else:
+                full = torch.cat([pf._send for pf in ranks], 0)
             for pf, U in zip(ranks, draws_u):                 # unpack + resample
-                pf._recv.copy_(full)
                 h, s = pf._h, pf._stream()
-                _lib.check(lib.gpmdm_pf_unpack(h, pf._recv.data_ptr(), s), "unpack")
+                if not split:
+                    pf._recv.copy_(full)
+                    _lib.check(lib.gpmdm_pf_unpack(h, pf._recv.data_ptr(), s), "unpack")
                 _lib.check(lib.gpmdm_pf_resample(h, _lib.dptr(U), s), "resample")
+                pf._readout = None
+        elif split:
+            ref.update(z)
+            for pf in ranks:
+                h, s = pf._h, pf._stream()
+                _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
+                _lib.check(lib.gpmdm_pf_propagate_dynamics(h, None, s), "propagate_dynamics")
+            _split_exchange(lib, ranks, z)
+            for pf in ranks:
+                _lib.check(lib.gpmdm_pf_resample(pf._h, None, pf._stream()), "resample")
                 pf._readout = None
         else:
             ref.update(z)

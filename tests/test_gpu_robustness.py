@@ -107,3 +107,31 @@ def test_predictive_maps_on_concurrent_streams(fx_config2):
         torch.cuda.synchronize()
         for got, want in zip((ga, gb, da, db), ref):
             assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
+
+
+def test_step_call_order_is_enforced(fx_config1):
+    """switch -> propagate_dynamics -> weigh -> resample (or switch -> propagate -> resample):
+    a call out of order returns GPMDM_E_STATE and leaves the filter usable, and a step done
+    in halves is bitwise the one-call step."""
+    from gpmdm_amd import GPMDM_PF, _lib
+    m = product_model(fx_config1)
+    T = torch.tensor(fx_config1["T"])
+    z = np.ascontiguousarray(fx_config1["z"][0], dtype=np.float64)
+    lib = _lib.load()
+    pfs = []
+    for _ in range(2):
+        torch.manual_seed(0)                 # same initial particles
+        pfs.append(GPMDM_PF(m, T, 3000, rng="philox", seed=3))
+    h, s = pfs[0]._h, pfs[0]._stream()
+    assert lib.gpmdm_pf_weigh(h, _lib.dptr(z), s) == _lib.GPMDM_E_STATE
+    assert lib.gpmdm_pf_propagate_dynamics(h, None, s) == _lib.GPMDM_E_STATE
+    _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
+    _lib.check(lib.gpmdm_pf_propagate_dynamics(h, None, s), "propagate_dynamics")
+    assert lib.gpmdm_pf_resample(h, None, s) == _lib.GPMDM_E_STATE
+    assert lib.gpmdm_pf_set_dedup(h, 0) == _lib.GPMDM_E_STATE
+    _lib.check(lib.gpmdm_pf_weigh(h, _lib.dptr(z), s), "weigh")
+    _lib.check(lib.gpmdm_pf_resample(h, None, s), "resample")
+    pfs[1].update(z)
+    a, b = pfs[0].export_state(), pfs[1].export_state()
+    for key in ("states", "classes", "ll", "resample_idx"):
+        assert np.array_equal(a[key], b[key]), key

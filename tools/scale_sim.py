@@ -14,12 +14,14 @@ in-process (the data every rank sees is exactly what an N-GPU run sees), and rep
 rank's GPU time per step from its stage events (kernels only, no host gaps) and its
 dynamics-GP rows; the slowest rank bounds the N-GPU step.
 
-The RCCL all-gather is modelled, not measured (one GPU here): every rank receives the
-(N-1)/N share of P_total x (d+2) doubles.  Two bounds per N: a ring on one xGMI link per
-GPU (153 GB/s) and the ring's chunks spread over min(N-1, 7) links (RCCL's channels use
-distinct links on the fully connected 8-GPU node).  The modelled step adds the all-gather
-to the slowest rank's compute (no overlap) -- the weak-scaling figure the N-GPU bench would
-show with the collective on the critical path.
+The RCCL all-gathers are modelled, not measured (one GPU here): every rank receives the
+(N-1)/N share of P_total rows.  Two bounds per N: a ring on one xGMI link per GPU
+(153 GB/s) and the ring's chunks spread over min(N-1, 7) links (RCCL's channels use
+distinct links on the fully connected 8-GPU node).  GPMDM_PF exchanges {class, state}
+(d+1 doubles per row) while the observation GP runs and {ll} (1 double) after it, so the
+modelled step is the slowest rank's compute + the ll gather + whatever of the state
+gather the observation GP does not cover; the fully serial figure (one (d+2)-wide gather
+after the step's compute) is printed beside it.
 """
 
 XGMI_LINK_GBPS = 153.0
@@ -130,12 +132,18 @@ def ranks_mode():
             per.append({k: v[0] / max(v[1], 1) for k, v in st.items()})
         tot = [sum(p.values()) for p in per]
         worst = max(range(n), key=lambda r: tot[r])
-        ag1, agm = allgather_ms(P, model.d + 2, n)
+        ser1, serm = allgather_ms(P, model.d + 2, n)
+        st1, stm = allgather_ms(P, model.d + 1, n)
+        ll1, llm = allgather_ms(P, 1, n)
+        obs = per[worst]["obs_gemm"] + per[worst]["obs_finish"]
+        ag1, agm = ll1 + max(0.0, st1 - obs), llm + max(0.0, stm - obs)
+        print(f"[shard_order={order}] N={n}: serial exchange (one gather after compute) "
+              f"{ser1:.3f} / {serm:.3f} ms -> step {max(tot) + ser1:.3f} / {max(tot) + serm:.3f} ms", flush=True)
         print(f"[shard_order={order}] N={n}: P_total={P}, GPU ms per step per rank: max {max(tot):.3f} min {min(tot):.3f} "
               f"(rank {worst}: dyn_gemm {per[worst]['dyn_gemm']:.3f} obs_gemm {per[worst]['obs_gemm']:.3f} "
               f"switch {per[worst]['switch']:.3f} resample {per[worst]['resample']:.3f}); "
               f"dyn rows per rank (mean over steps): {[r // steps for r in rows]}; "
-              f"modelled all-gather {ag1:.3f} ms (1 link) / {agm:.3f} ms ({min(max(n - 1, 1), 7)} links) -> "
+              f"modelled exposed exchange (states overlapped with the observation GP, then ll) {ag1:.3f} ms (1 link) / {agm:.3f} ms ({min(max(n - 1, 1), 7)} links) -> "
               f"step {max(tot) + ag1:.3f} / {max(tot) + agm:.3f} ms, "
               f"{P * 1e3 / (max(tot) + ag1):.3e} / {P * 1e3 / (max(tot) + agm):.3e} particle-steps/s", flush=True)
         del pfs
