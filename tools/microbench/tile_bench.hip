@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "../../gpmdm_amd/csrc/gp_tile.h"
@@ -98,10 +99,13 @@ int main(int argc, char** argv) {
               {launch_var<131072, 8>, 1, "64x512 LDS coords"}};
 #else
   V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512 production"},
-              {launch_var<134217728, 4, 2, 8>, 2, "32x512 PRIO"},
-              {launch_var<0, 4>, 0, "64x256"},
-              {launch_var<134217728, 4>, 0, "64x256 PRIO"},
-              {launch_var<16, 4, 2, 8>, 2, "32x512 no gen"}};
+              {launch_var<16, 4, 2, 8>, 2, "no gen"},
+              {launch_var<16 | 32, 4, 2, 8>, 2, "no gen, no B loads"},
+              {launch_var<16 | 32 | 64, 4, 2, 8>, 2, "no gen/B/A reads"},
+              {launch_var<16 | 32 | 64 | 8, 4, 2, 8>, 2, "no gen/B/A/barrier"},
+              {launch_var<128, 4, 2, 8>, 2, "production fullK"},
+              {launch_var<16 | 128, 4, 2, 8>, 2, "no gen fullK"},
+              {launch_var<16 | 32 | 64 | 8 | 128, 4, 2, 8>, 2, "no gen/B/A/barrier fullK"}};
 #endif
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
   std::vector<std::vector<float>> t(NV);
@@ -141,10 +145,13 @@ int main(int argc, char** argv) {
     rows += (double)ksteps(hi <= N ? hi : N) * kBK;
   }
   const double fl = 2.0 * 16 * rows * P;
+  // fullK variants (VAR bit 7): every 16-column tile runs all K-steps
+  const double fl_full = 2.0 * 16 * ((N + D + 15) / 16) * (double)ksteps(N) * kBK * P;
   for (int v = 0; v < NV; ++v) {
     std::sort(t[v].begin(), t[v].end());
+    const bool full = std::string(vars[v].name).find("fullK") != std::string::npos;
     printf("%-30s median %.3f ms  min %.3f ms   (%.1f TF/s executed MFMA)\n", vars[v].name, t[v][ROUNDS / 2],
-           t[v][0], fl / t[v][ROUNDS / 2] / 1e9);
+           t[v][0], (full ? fl_full : fl) / t[v][ROUNDS / 2] / 1e9);
   }
   return 0;
 }
