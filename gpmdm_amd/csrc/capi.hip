@@ -162,6 +162,7 @@ struct gpmdm_pf {
   // ancestor-ordered shards (multi-rank philox filters, shard_order.hip): own = particles
   // in order of their resampling ancestor's bucket; this rank evaluates positions [lo, hi)
   int* own = nullptr;
+  int* own_inv = nullptr;            // own_inv[own[r]] = r
   unsigned char* own_tmp = nullptr;
   size_t own_tmp_bytes = 0;
   bool own_valid = false;
@@ -208,7 +209,7 @@ struct gpmdm_pf {
                     pred_q, pred_mu, pred_mu_p, pred_out};
     for (double* p : ds) dfree(p);
     int* is[] = {cls, cls_new, perm, ridx, blockcounts, blockoff, small, obs_tab,
-                 slot, lflag, lblock, ltab, lperm, guide, own, sys_mark, sys_block};
+                 slot, lflag, lblock, ltab, lperm, guide, own, own_inv, sys_mark, sys_block};
     for (int* p : is) dfree(p);
     dfree(own_tmp);
     dfree(gmax);
@@ -526,6 +527,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   if (n_ranks > 1 && rng_mode == GPMDM_RNG_PHILOX) {
     pf->own_tmp_bytes = std::max<size_t>(ancestor_order_temp_bytes(P), 1);
     ALLOC(own, P);
+    ALLOC(own_inv, P);
     ALLOC(own_tmp, pf->own_tmp_bytes);
   }
 #undef ALLOC
@@ -987,6 +989,7 @@ int gpmdm_pf_unpack_part(gpmdm_pf_t pf, const double* recv, int part, void* stre
   a.lo = 0;
   a.d = pf->m->d;
   a.own = pf->own_order();
+  a.inv = pf->own_valid ? pf->own_inv : nullptr;
   a.buf = const_cast<double*>(recv);
   a.part = part;
   a.ll = pf->ll;
@@ -1017,7 +1020,7 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   // next frame's ownership order (identical on every rank: same replicated ancestors)
   pf->own_valid = false;
   if (pf->own && pf->dedup && pf->shard_order) {
-    if (launch_ancestor_order(pf->ridx, pf->own, pf->P, pf->own_tmp, pf->own_tmp_bytes, s) != 0)
+    if (launch_ancestor_order(pf->ridx, pf->own, pf->own_inv, pf->P, pf->own_tmp, pf->own_tmp_bytes, s) != 0)
       return fail(GPMDM_E_HIP, "ancestor-order pass failed");
     pf->own_valid = true;
   }

@@ -203,6 +203,7 @@ struct PackArgs {
   long long n, lo;
   int d;
   const int* own;                 // row r holds particle own[lo + r] (nullptr: identity)
+  const int* inv;                 // unpack: particle p's row is inv[p] (nullptr: identity)
   double* buf;
   int part;                       // GPMDM_PACK_*: {ll, class, X} | {class, X} | {ll}
   double* ll;
@@ -215,7 +216,9 @@ struct PackArgs {
 // slice of that order covers a contiguous range of ancestors.  Deterministic (identical on
 // every rank).  temp: ancestor_order_temp_bytes(P) of device memory.
 size_t ancestor_order_temp_bytes(long long P);
-int launch_ancestor_order(const int* anc, int* own, long long P, void* temp, size_t temp_bytes, hipStream_t s);
+// inv: the inverse permutation, inv[own[r]] = r (unpack reads particle p's row inv[p])
+int launch_ancestor_order(const int* anc, int* own, int* inv, long long P, void* temp, size_t temp_bytes,
+                          hipStream_t s);
 
 void launch_switch(const SwitchArgs& a, hipStream_t s);
 void launch_scan_counts(const ScanArgs& a, hipStream_t s);

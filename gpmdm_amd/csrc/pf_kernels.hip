@@ -671,21 +671,35 @@ __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void k_readout(ResampleArgs a) {
-  __shared__ double red[4];
+__global__ __launch_bounds__(1024) void k_readout(ResampleArgs a) {
+  __shared__ double red[8][16];
   __shared__ double tot[kMaxReadout];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nq = a.C + 1 + a.d;
   const long long f = blockIdx.x;
   const double* partials = a.partials + f * a.nb * nq;
   double* readout = a.readout + f * (a.C + a.d + 1);
-  for (int k = 0; k < nq; ++k) {
-    double s = 0.0;
-    for (long long b = tid; b < a.nb; b += 256) s += partials[b * nq + k];
-    s = wave_sum(s);
-    if (lane == 0) red[w] = s;
+  // eight read-out quantities per pass over the partials (every thread's loads in flight
+  // together; per quantity the same thread-strided order as one quantity at a time)
+  for (int k0 = 0; k0 < nq; k0 += 8) {
+    double s[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) s[kk] = 0.0;
+    for (long long b = tid; b < a.nb; b += 1024)
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+        if (k0 + kk < nq) s[kk] += partials[b * nq + k0 + kk];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const double v = wave_sum(s[kk]);
+      if (lane == 0) red[kk][w] = v;
+    }
     __syncthreads();
-    if (tid == 0) tot[k] = red[0] + red[1] + red[2] + red[3];
+    if (tid < 8 && k0 + tid < nq) {
+      double t = 0.0;
+      for (int v = 0; v < 16; ++v) t += red[tid][v];
+      tot[k0 + tid] = t;
+    }
     __syncthreads();
   }
   if (tid == 0) {
@@ -712,10 +726,12 @@ __global__ __launch_bounds__(kB) void k_pack(PackArgs a) {
   }
 }
 
+// one thread per particle p, reading its row inv[p] (a gather: the writes stay coalesced;
+// scattering the rows to own[r] made every write a partial-line write, 57 us at P = 800k)
 __global__ __launch_bounds__(kB) void k_unpack(PackArgs a) {
-  const long long r = (long long)blockIdx.x * kB + threadIdx.x;   // row = ownership position
-  if (r >= a.n) return;
-  const long long p = a.own ? a.own[r] : r;
+  const long long p = (long long)blockIdx.x * kB + threadIdx.x;
+  if (p >= a.n) return;
+  const long long r = a.inv ? a.inv[p] : p;
   const int lo = a.part == GPMDM_PACK_STATES ? 1 : 0;
   const int hi = a.part == GPMDM_PACK_LL ? 1 : a.d + 2;
   const double* i = a.buf + r * (hi - lo);
@@ -838,7 +854,7 @@ void launch_resample(const ResampleArgs& a, hipStream_t s) {
   } else if (!a.identity && a.GB > 0)
     hipLaunchKernelGGL(k_guide, dim3(nblk(a.GB + 3, kB), (unsigned)a.F), dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_resample, dim3(nblk(a.P, kB), (unsigned)a.F), dim3(kB), 0, s, a);
-  hipLaunchKernelGGL(k_readout, dim3((unsigned)a.F), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_readout, dim3((unsigned)a.F), dim3(1024), 0, s, a);
 }
 void launch_pack(const PackArgs& a, hipStream_t s) {
   if (a.n > 0) hipLaunchKernelGGL(k_pack, dim3(nblk(a.n, kB)), dim3(kB), 0, s, a);

@@ -16,7 +16,7 @@
 //   k_bucket_hist     per-block bucket histograms, bucket-major H[b][block]
 //   k_chunk_scan      exclusive scan of H inside 1024-entry chunks, chunk totals
 //   k_chunk_offsets   one workgroup: exclusive scan of the chunk totals
-//   k_bucket_scatter  own[start(b, block) + rank in block] = particle
+//   k_bucket_scatter  own[start(b, block) + rank in block] = particle, and its inverse
 // (rocPRIM's radix sort of the same keys measured 145 us at P = 800k on MI355X,
 // tools/microbench/sort_probe.hip; this pass is a few us per launch.)
 #include "pf_kernels.h"
@@ -95,18 +95,36 @@ __global__ __launch_bounds__(1024) void k_chunk_offsets(int* chunk_tot, int nchu
 }
 
 __global__ __launch_bounds__(kOB) void k_bucket_scatter(const int* anc, long long P, int nblk, const int* H,
-                                                         const int* chunk_off, int* own) {
-  __shared__ int bk[kOB];
-  const int tid = threadIdx.x;
+                                                         const int* chunk_off, int* own, int* inv) {
+  constexpr int kW = kOB / 64;
+  __shared__ int cnt[kW][kOB];                        // bucket counts per wave
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const long long s = (long long)blockIdx.x * kOB + tid;
   const int b = s < P ? bucket_of(anc[s], P) : -1;
-  bk[tid] = b;
+  for (int i = tid; i < kW * kOB; i += kOB) (&cnt[0][0])[i] = 0;
+  // rank among this block's bucket-b particles, in particle order: lanes of this wave with
+  // the same bucket (ballots over the bucket's 8 bits and its validity), then the earlier
+  // waves' counts of that bucket -- deterministic, so every rank builds the same order
+  unsigned long long same = ~0ull;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool bit = (b >> k) & 1;
+    const unsigned long long m = __ballot(bit);
+    same &= bit ? m : ~m;
+  }
+  const unsigned long long valid = __ballot(b >= 0);
+  same &= b >= 0 ? valid : ~valid;
+  const int r_wave = __popcll(same & ((1ull << lane) - 1));
+  __syncthreads();
+  if (b >= 0 && r_wave == 0) cnt[w][b] = __popcll(same);   // one writer per (wave, bucket)
   __syncthreads();
   if (b < 0) return;
-  int r = 0;                                          // rank among this block's bucket-b particles
-  for (int j = 0; j < tid; ++j) r += bk[j] == b;      // same j on every lane: LDS broadcast
+  int r = r_wave;
+  for (int v = 0; v < w; ++v) r += cnt[v][b];
   const long long h = (long long)b * nblk + blockIdx.x;
-  own[chunk_off[h / kChunk] + H[h] + r] = (int)s;
+  const int pos = chunk_off[h / kChunk] + H[h] + r;
+  own[pos] = (int)s;
+  inv[s] = pos;
 }
 
 inline unsigned nblocks(long long n, int b) { return (unsigned)((n + b - 1) / b); }
@@ -120,7 +138,8 @@ size_t ancestor_order_temp_bytes(long long P) {
   return sizeof(int) * (size_t)(n + nchunk);
 }
 
-int launch_ancestor_order(const int* anc, int* own, long long P, void* temp, size_t temp_bytes, hipStream_t s) {
+int launch_ancestor_order(const int* anc, int* own, int* inv, long long P, void* temp, size_t temp_bytes,
+                          hipStream_t s) {
   const int nblk = (int)nblocks(P, kOB);
   const long long n = (long long)nblk * kOB;
   const int nchunk = (int)nblocks(n, kChunk);
@@ -130,7 +149,7 @@ int launch_ancestor_order(const int* anc, int* own, long long P, void* temp, siz
   hipLaunchKernelGGL(k_bucket_hist, dim3(nblk), dim3(kOB), 0, s, anc, P, nblk, H);
   hipLaunchKernelGGL(k_chunk_scan, dim3(nchunk), dim3(256), 0, s, H, n, chunk);
   hipLaunchKernelGGL(k_chunk_offsets, dim3(1), dim3(1024), 0, s, chunk, nchunk);
-  hipLaunchKernelGGL(k_bucket_scatter, dim3(nblk), dim3(kOB), 0, s, anc, P, nblk, H, chunk, own);
+  hipLaunchKernelGGL(k_bucket_scatter, dim3(nblk), dim3(kOB), 0, s, anc, P, nblk, H, chunk, own, inv);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
