@@ -433,11 +433,12 @@ def _split_exchange(lib, ranks, z):
         _lib.check(lib.gpmdm_pf_unpack_part(h, pf._recv_l.data_ptr(), _lib.GPMDM_PACK_LL, s), "unpack")
 
 
-@pytest.mark.parametrize("world,rng_mode,order,P,split", [
-    (4, "philox", True, 10_007, False), (8, "philox", True, 10_007, False), (8, "philox", False, 10_007, False),
-    (3, "torch", True, 10_007, False), (8, "philox", True, 400_003, False),
-    (4, "philox", True, 10_007, True), (3, "torch", True, 10_007, True)])
-def test_logical_shards_match_one_rank(m2, world, rng_mode, order, P, split):
+@pytest.mark.parametrize("world,rng_mode,order,P,split,resample", [
+    (4, "philox", True, 10_007, False, "multinomial"), (8, "philox", True, 10_007, False, "multinomial"),
+    (8, "philox", False, 10_007, False, "multinomial"), (3, "torch", True, 10_007, False, "multinomial"),
+    (8, "philox", True, 400_003, False, "multinomial"), (4, "philox", True, 10_007, True, "multinomial"),
+    (3, "torch", True, 10_007, True, "multinomial"), (4, "philox", True, 10_007, True, "systematic")])
+def test_logical_shards_match_one_rank(m2, world, rng_mode, order, P, split, resample):
     """results at R ranks equal the single-rank filter, with R logical shards
     on one GPU and the all-gather done in-process.  Philox draws at 4 and 8 ranks; the
     replay stream (torch generator) at 3 ranks, every rank drawing the same full streams
@@ -451,11 +452,12 @@ def test_logical_shards_match_one_rank(m2, world, rng_mode, order, P, split):
     T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
     Y = m2.get_Y()
     torch.manual_seed(4)
-    ref = GPMDM_PF(m2, T, P, rng=rng_mode, seed=91)
+    ref = GPMDM_PF(m2, T, P, rng=rng_mode, seed=91, resample=resample)
     ranks = []
     for r in range(world):
         torch.manual_seed(4)
-        ranks.append(GPMDM_PF(m2, T, P, rng=rng_mode, seed=91, shard=(world, r), shard_order=order))
+        ranks.append(GPMDM_PF(m2, T, P, rng=rng_mode, seed=91, shard=(world, r), shard_order=order,
+                              resample=resample))
     lib = _lib.load()
     for k in range(3):
         z = np.ascontiguousarray(np.asarray(Y[60 + 3 * k], dtype=np.float64))
