@@ -10,7 +10,7 @@ if [ "$1" = build ]; then
   for c in "$@"; do
     src=/tmp/tile_ab_src/$c; rm -rf $src; mkdir -p $src
     if [ $c = WT ]; then cp -r gpmdm_amd include $src/; else git archive $c gpmdm_amd/csrc include | tar -x -C $src; fi
-    for d in 3 16; do
+    for d in 3 8 16; do
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I $src/include -DTB_D=$d \
         "-DGP_TILE_H=\"$src/gpmdm_amd/csrc/gp_tile.h\"" tools/microbench/tile_ab.hip -o $out/tile_ab_d${d}_$c &
     done
@@ -19,6 +19,7 @@ if [ "$1" = build ]; then
 else
   for r in 1 2; do
     for b in $out/tile_ab_d16_*; do echo "== $b"; timeout -k 10 170 $b 125000 20000 256 | grep median; done
+    for b in $out/tile_ab_d8_*; do echo "== $b"; timeout -k 10 120 $b 100000 10000 128 | grep median; done
     for b in $out/tile_ab_d3_*; do echo "== $b"; timeout -k 10 60 $b | grep median; done
   done
 fi
