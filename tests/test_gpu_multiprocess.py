@@ -123,3 +123,50 @@ def test_process_group_replay_refuses_different_torch_states():
     for r in range(2):
         kind, msg = res[r]
         assert kind == "ValueError" and "identical torch RNG" in msg
+
+
+def _nccl_worker(port, out_q):
+    """World-size-1 RCCL group: the asynchronous all-gather GPMDM_PF overlaps with the
+    observation GP (distributed.allgather_rows_start, nccl branch), with kernels queued on
+    the current stream between start and wait, and the uneven-shard (padded) branch."""
+    import torch.distributed as dist
+    from gpmdm_amd.distributed import allgather_rows_start
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        ok = True
+        for P, W in ((100_000, 4), (7, 1)):
+            send = torch.arange(P * W, dtype=torch.float64, device=dev).reshape(P, W)
+            recv = torch.full((P, W), -1.0, dtype=torch.float64, device=dev)
+            wait = allgather_rows_start(recv, send)
+            busy = torch.randn(2048, 2048, dtype=torch.float64, device=dev)
+            for _ in range(4):                     # work on the current stream meanwhile
+                busy = busy @ busy * 1e-3
+            wait()
+            ok = ok and bool(torch.equal(recv, send))
+        torch.cuda.synchronize()
+        out_q.put(("ok", ok))
+    except Exception as e:                         # noqa: BLE001 -- reported to the parent
+        out_q.put(("error", repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_rccl_async_allgather_world1():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        kind, payload = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert kind == "ok", payload
+    assert payload
+    assert p.exitcode == 0
