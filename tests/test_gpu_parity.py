@@ -299,7 +299,7 @@ def test_tile_shapes_vs_oracle(shape, d, D, monkeypatch):
     GPMDM_TILE_SHAPE) on a ragged model: N = 2 x 3 x 157 rows (not a multiple of any block
     width), query counts not multiples of the 32- or 64-particle tiles.  Predictive maps and
     one resynced filter step against the oracle; the 32x512 shape at d=16 (beyond the
-    default's d <= 12 cut, registers spill) must still be exact."""
+    default's d <= 12 cut: particle coordinates from LDS) must still be exact."""
     from gpmdm_amd import GPMDM, GPMDM_PF, synthetic
     from oracle import gpmdm_oracle as O
     monkeypatch.setenv("GPMDM_TILE_SHAPE", str(shape))
@@ -568,12 +568,14 @@ def test_stage_selective_timing(m2):
     assert all(n == 1 for ms, n in st.values()), st
 
 
-@pytest.mark.parametrize("C,d,D,L", [(2, 24, 30, 40), (2, 32, 20, 35), (9, 2, 6, 20)])
+@pytest.mark.parametrize("C,d,D,L", [(2, 24, 30, 40), (2, 32, 20, 35), (9, 2, 6, 20), (32, 3, 6, 9),
+                                     (2, 12, 20, 40), (2, 13, 20, 40)])
 def test_wide_latents_and_many_classes_vs_oracle(C, d, D, L):
     """The remaining supported shapes: latent dimensions 24 and 32 (launch bounds of one
-    workgroup per CU, 64x512 observation tiles), and C = 9 classes, which crosses the
-    8-segment limit of one dynamics launch (two launches per step).  Predictive maps and
-    one resynced filter step (replay draws) against the oracle."""
+    workgroup per CU, 64x512 observation tiles); C = 9 classes, which crosses the 8-segment
+    limit of one dynamics launch (two launches per step), and the maximum C = 32 (four);
+    d = 12 / 13 on either side of the 32x512 -> 64x512 observation-tile cut.  Predictive
+    maps and one resynced filter step (replay draws) against the oracle."""
     from gpmdm_amd import GPMDM, GPMDM_PF, synthetic
     from oracle import gpmdm_oracle as O
     data = synthetic.make_sequences(C=C, S=3, L=L, D=D, d=d, seed=41)
