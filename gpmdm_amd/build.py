@@ -39,7 +39,35 @@ def _flags():
             "-Wno-unused-function", "-munsafe-fp-atomics", f"-I{ROOT / 'include'}"]
 
 
+C_HOST_SRC = ROOT / "examples" / "c_host" / "pf_main.c"
+C_HOST = ROOT / "examples" / "c_host" / "pf_main"
+
+
+def build_c_host(force: bool = False, verbose: bool = False) -> Path:
+    """The native C host of the C ABI (examples/c_host/pf_main.c): plain gcc against
+    include/gpmdm_hip.h, linked to the in-tree library by a relative rpath."""
+    if not C_HOST_SRC.exists():
+        return C_HOST
+    deps = max(C_HOST_SRC.stat().st_mtime, (ROOT / "include" / "gpmdm_hip.h").stat().st_mtime)
+    if not force and C_HOST.exists() and C_HOST.stat().st_mtime >= deps:
+        return C_HOST
+    cmd = ["gcc", "-std=c99", "-O2", "-Wall", "-Wextra", f"-I{ROOT / 'include'}", str(C_HOST_SRC),
+           "-o", str(C_HOST), f"-L{PKG}", "-lgpmdm_hip", "-Wl,-rpath,$ORIGIN/../../gpmdm_amd"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return C_HOST
+
+
 def build(force: bool = False, verbose: bool = False) -> Path:
+    lib = _build_lib(force, verbose)
+    build_c_host(force, verbose)
+    return lib
+
+
+def _build_lib(force: bool = False, verbose: bool = False) -> Path:
     newest_hdr = max(h.stat().st_mtime for h in HEADERS)
     newest_src = max((CSRC / src).stat().st_mtime for src in SOURCES)
     if not force and LIB.exists() and LIB.stat().st_mtime >= max(newest_hdr, newest_src):

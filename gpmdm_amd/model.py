@@ -325,7 +325,7 @@ class GPMDM:
             X = np.ascontiguousarray(X, dtype=np.float64)
             B = np.ascontiguousarray(B, dtype=np.float64)
             n, d = X.shape
-            ls = np.ascontiguousarray(np.exp(_to_np(log_ls)))
+            ls = np.ascontiguousarray(_to_np(torch.exp(log_ls)))   # the descriptor's lengthscales, bit for bit
             c2 = None if lin_c2 is None else np.ascontiguousarray(lin_c2, dtype=np.float64)
             R = np.empty((n, n))
             M = np.empty((n, B.shape[1]))

@@ -99,3 +99,14 @@ def test_synthetic_shapes():
     assert data.sequences[0][0].dtype == np.float32
     T = synthetic.markov_matrix(3)
     assert np.allclose(T.sum(1), 1.0) and T[0, 0] == 0.9
+
+
+def test_c_host_builds_and_links():
+    """examples/c_host/pf_main (the native C host of the C ABI) compiles with gcc against
+    include/gpmdm_hip.h alone and resolves every symbol it uses from the in-tree library
+    (run without arguments: usage, exit status 2, no GPU touched)."""
+    import subprocess
+    from gpmdm_amd import build
+    exe = build.build_c_host()
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "usage" in r.stderr
