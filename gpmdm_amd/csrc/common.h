@@ -47,6 +47,11 @@ struct TileParams {
   const double* z;                // F x n_m
   const double* lam2;             // n_m: exp(y_log_lambdas)^2 = 1 / il2
   long long Pf;                   // particles per filter
+  // K* cache (observation GP, gp_tile.h VAR bits 28/29): the full-K block's workgroups
+  // store each K-step's A fragments here (tile-major, fragment order); the other blocks'
+  // workgroups, launched after them, load them instead of generating K* again.
+  double* kcache;
+  int j_skip;                     // blocks skipped from the top: J = n_j_max - 1 - j_skip - b / tiles_ub
 };
 
 void launch_gp_tile(const TileParams& p, int d, bool dyn, hipStream_t stream);

@@ -325,6 +325,13 @@ __device__ __forceinline__ double exp2_64m(double t, const double* tab) {
 //           K-steps ahead; no MFMA wave ever issues an exp chain (one workgroup per CU)
 //   bit 27: PRIO -- s_setprio 1 around a K-step's MFMAs, 0 around its generation (the
 //           SIMD arbiter then prefers the other wave's MFMAs while one wave generates)
+//   bit 28: KPROD -- K* cache producer (launched on the full-K block only): as production,
+//           and every A fragment the workgroup multiplies is also stored to prm.kcache
+//           (wave w stores sub-step w of each K-step: one 1 KiB buffer store per K-step)
+//   bit 29: KCONS -- K* cache consumer (the other blocks, launched after the producer): no
+//           generation, no row staging, no LDS ring and no barrier in the K loop; the A
+//           fragments stream from prm.kcache into VGPRs one K-step ahead, like B.  The
+//           values are the producer's, so the results are bitwise production's.
 //
 // Geometry: NW waves; each wave owns MT x NTW tiles of 16 x 16 (16 MT particles x 16 NTW
 // columns), so a workgroup covers PT = 16 MT particles x NB = 16 NTW NW columns.  K* costs
@@ -352,6 +359,9 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
   constexpr int RG = NTW >= 16 ? 2 : 1;
   constexpr bool SPEC = (VAR & 67108864) != 0;
   static_assert(!SPEC || NW == 8, "SPEC: 4 MFMA + 4 producer waves");
+  constexpr bool KPROD = (VAR & 268435456) != 0;
+  constexpr bool KCONS = (VAR & 536870912) != 0;
+  static_assert(!(KPROD && KCONS) && !((KPROD || KCONS) && (SPEC || DYN)), "K* cache: observation GP only");
   constexpr int NWM = SPEC ? NW / 2 : NW;                    // MFMA waves
   constexpr int NT = 64 * NW;                                // threads
   constexpr int NTG = SPEC ? 64 * (NW - NWM) : NT;           // generation / row-staging threads
@@ -408,11 +418,11 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
   const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   // SPEC: waves [0, NWM) multiply, waves [NWM, NW) stage rows and generate K*
-  const bool producer = !SPEC || w >= NWM;
+  const bool producer = (!SPEC || w >= NWM) && !KCONS;     // KCONS: nothing to generate
   const bool consumer = !SPEC || w < NWM;
   const int gtid = SPEC ? (tid >= 64 * NWM ? tid - 64 * NWM : tid) : tid;   // generation-role index
   const int b = blockIdx.x;
-  const int J = prm.n_j_max - 1 - b / prm.tiles_ub;
+  const int J = prm.n_j_max - 1 - ((KPROD || KCONS) ? prm.j_skip : 0) - b / prm.tiles_ub;
   // tile index within this launch's segments (a launch may cover classes c0..c0+7)
   // segment tables live in device memory (the filter computes them on the device; the
   // predictive maps write theirs with k_seg_table).  A by-value table with a per-thread
@@ -510,6 +520,59 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
 #pragma unroll
   for (int tt = 0; tt < NTW; ++tt) kmaxw = max(kmaxw, kend[tt]);
   const int ks_last = (kmaxw > 0 ? kmaxw : 1) - 1;
+
+  // K* cache (KPROD / KCONS): tile t's A fragments, K-step ks, sub-step kk, at doubles
+  // ((ks 4 + kk) 64 + lane) MT of the tile's slab of ksteps(n_rows) K-steps.  Buffer
+  // addressing as for B: SGPR resource and K-step offset, constant lane offset.
+  typedef unsigned v2u __attribute__((ext_vector_type(2)));
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t krsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((KPROD || KCONS) ? prm.kcache + (long long)t * ksteps(n_rows) * (256 * MT) : Bw), (short)0,
+      0x7fffffff, 0x00020000);
+  const unsigned klane_off = (unsigned)lane * (unsigned)(MT * 8);
+  double an[4 * MT];                                         // KCONS: the next K-step's A fragments
+  auto loadA_part = [&](int ks, int kk) {
+    const int kc = ks < ks_last ? ks : ks_last;
+    const int soff = (kc * 4 + kk) * (64 * MT) * 8;
+    if constexpr ((VAR & 1073741824) != 0) {              // A/B: flat global loads
+      const double* src = prm.kcache + (long long)t * ksteps(n_rows) * (256 * MT) + (kc * 4 + kk) * (64 * MT) + lane * MT;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) an[kk * MT + mt] = src[mt];
+    } else if constexpr (MT == 1) {
+      const v2u x = __builtin_amdgcn_raw_buffer_load_b64(krsrc, klane_off, soff, 0);
+      an[kk] = __builtin_bit_cast(double, (unsigned long long)x.x | ((unsigned long long)x.y << 32));
+    } else {
+#pragma unroll
+      for (int h = 0; h < MT / 2; ++h) {
+        const v4u x = __builtin_amdgcn_raw_buffer_load_b128(krsrc, klane_off + 16u * h, soff, 0);
+        an[kk * MT + 2 * h + 0] = __builtin_bit_cast(double, (unsigned long long)x.x | ((unsigned long long)x.y << 32));
+        an[kk * MT + 2 * h + 1] = __builtin_bit_cast(double, (unsigned long long)x.z | ((unsigned long long)x.w << 32));
+      }
+    }
+  };
+  auto storeA_part = [&](int ks, int kk, const double (&af)[MT]) {
+    const int soff = (ks * 4 + kk) * (64 * MT) * 8;
+    if constexpr (MT == 1) {
+      const unsigned long long u = __builtin_bit_cast(unsigned long long, af[0]);
+      __builtin_amdgcn_raw_buffer_store_b64((v2u){(unsigned)u, (unsigned)(u >> 32)}, krsrc, klane_off, soff, 0);
+    } else {
+      if constexpr ((VAR & 1073741824) != 0) {              // A/B: 8-byte stores
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const unsigned long long u = __builtin_bit_cast(unsigned long long, af[mt]);
+          __builtin_amdgcn_raw_buffer_store_b64((v2u){(unsigned)u, (unsigned)(u >> 32)}, krsrc, klane_off + 8u * mt, soff, 0);
+        }
+      } else {
+#pragma unroll
+        for (int h = 0; h < MT / 2; ++h) {
+          const unsigned long long u0 = __builtin_bit_cast(unsigned long long, af[2 * h]);
+          const unsigned long long u1 = __builtin_bit_cast(unsigned long long, af[2 * h + 1]);
+          __builtin_amdgcn_raw_buffer_store_b128((v4u){(unsigned)u0, (unsigned)(u0 >> 32), (unsigned)u1, (unsigned)(u1 >> 32)},
+                                                 krsrc, klane_off + 16u * h, soff, 0);
+        }
+      }
+    }
+  };
 
   // Training rows of a K-step are staged through an LDS ring (RX) one step ahead with
   // vector loads, so generation reads them as LDS broadcasts: no scalar loads whose
@@ -661,7 +724,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
     double v2[GV];
     const bool gen_now = !GEN2 || (ks & 1) == 0;
     constexpr bool PRIO = (VAR & 134217728) != 0;
-    if constexpr (!(VAR & 16) && !SPEC) {                // SPEC: producer waves generate
+    if constexpr (!(VAR & 16) && !SPEC && !KCONS) {                // SPEC: producer waves generate
       load_rows(ks + RA, rr);
       if constexpr (PRIO) {
         // generation after the MFMAs, at low priority (below)
@@ -684,6 +747,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         if constexpr (VAR & 64) af[mt] = asq + mt + kk + buf;
+        else if constexpr (KCONS) af[mt] = an[kk * MT + mt];
         else af[mt] = As[buf][kk * 4 + lk][mt * 16 + li];
       }
 #pragma unroll
@@ -691,7 +755,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
 #pragma unroll
         for (int nt = T0; nt < T1c; ++nt)
           acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bb[(kk % BR) * NTW + nt], acc[mt][nt], 0, 0, 0);
-      if constexpr (SPLIT && !(VAR & 16) && !SPEC) {
+      if constexpr (SPLIT && !(VAR & 16) && !SPEC && !KCONS) {
         constexpr int PER = 4 / GV > 0 ? 4 / GV : 1;
         if (kk % PER == 0) {
 #pragma unroll
@@ -708,12 +772,24 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
         }
       }
       loadB_part(ks + (kk + BR) / 4, (kk + BR) % 4, kk % BR, bb);   // sub-step kk + BR
+      // KCONS: an[j] is reloaded one sub-step after its last MFMA read, not right behind it
+      // (a reload issued directly after the MFMA that reads the registers gave
+      // nondeterministic results: L1-hit loads of fragments the WG's other waves had just
+      // fetched overtook the MFMA's operand read).  an[3] for step ks is loaded after step
+      // ks's sub-step 0.
+      if constexpr (KCONS) {
+        if (kk == 0) loadA_part(ks, 3);
+        else loadA_part(ks + 1, kk - 1);
+      }
+      if constexpr (KPROD) {
+        if (w == kk) storeA_part(ks, kk, af);
+      }
     }
-    if constexpr (PRIO && !(VAR & 16) && !SPEC) {
+    if constexpr (PRIO && !(VAR & 16) && !SPEC && !KCONS) {
       __builtin_amdgcn_s_setprio(0);
       gen(ks + LOOK, grb, v);
     }
-    if constexpr (!(VAR & 16) && !SPEC) {
+    if constexpr (!(VAR & 16) && !SPEC && !KCONS) {
       if constexpr (GEN2) {
         if (gen_now) {
           store((ks + 2) & (ASL - 1), v);
@@ -724,7 +800,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
       }
       store_rows(rslot, rr);
     }
-    if constexpr (!(VAR & 8)) {
+    if constexpr (!(VAR & 8) && !KCONS) {
       if constexpr (ST) {
         if constexpr (SL % SB == SB - 1) __syncthreads();
       } else {
@@ -773,6 +849,10 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
     if (consumer) {
 #pragma unroll
       for (int kk = 0; kk < BR; ++kk) loadB_part(0, kk, kk, bb);
+      if constexpr (KCONS) {
+#pragma unroll
+        for (int kk = 0; kk < 3; ++kk) loadA_part(0, kk);   // sub-step 3: inside step 0
+      }
     }
   }
   // Drain the prologue's loads (vmcnt(0)) so that the K loop's entry carries no pending
@@ -817,7 +897,15 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
   // the rest of the block's K range (other waves' tiles): generate only
   for (; ks < nks && SPEC; ++ks)                             // SPEC: the producers generate
     if (ks % SB == SB - 1) __syncthreads();
-  for (; ks < nks; ++ks) {
+  for (; ks < nks && !KCONS; ++ks) {
+    if constexpr (KPROD) {                                   // this wave's sub-step of ks
+      if (w < 4) {
+        double af[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) af[mt] = As[ks & (ASL - 1)][w * 4 + lk][mt * 16 + li];
+        storeA_part(ks, w, af);
+      }
+    }
     double v[GV];
     double rr[RPT];
     load_rows(ks + RA, rr);

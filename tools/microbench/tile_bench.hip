@@ -24,6 +24,63 @@ void launch_var(const TileParams& p, hipStream_t s) {
   hipLaunchKernelGGL((k_gp_tile<TB_D, false, VAR, NW, MT, NTW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, p);
 }
 
+// K* cache pair (gp_tile.h VAR bits 28/29): the full-K block generates and stores K*, the
+// other blocks load it.  Chunked: particle tiles in CH chunks; producer of chunk k on the
+// main stream, consumer of chunk k on a second stream after an event, so the producers'
+// grid tail overlaps the consumers' work.
+static hipStream_t g_s2 = nullptr;
+static hipEvent_t g_ev[17];
+static std::vector<TileParams> g_chunk[9];    // per chunk count: one TileParams per chunk
+template <int NW, int MT, int NTW, int CH>
+void launch_kc(const TileParams& p, hipStream_t s) {
+  TileParams a = p, c = p;
+  a.j_skip = 0;
+  c.j_skip = 1;
+  if (CH == 1) {
+    hipLaunchKernelGGL((k_gp_tile<TB_D, false, 268435456, NW, MT, NTW>), dim3(p.tiles_ub), dim3(64 * NW), 0, s, a);
+    hipLaunchKernelGGL((k_gp_tile<TB_D, false, 536870912, NW, MT, NTW>), dim3((p.n_j_max - 1) * p.tiles_ub), dim3(64 * NW), 0, s, c);
+    return;
+  }
+  for (int k = 0; k < CH; ++k) {
+    TileParams pa = g_chunk[CH][k], pc = g_chunk[CH][k];
+    pa.j_skip = 0;
+    pc.j_skip = 1;
+    hipLaunchKernelGGL((k_gp_tile<TB_D, false, 268435456, NW, MT, NTW>), dim3(pa.tiles_ub), dim3(64 * NW), 0, s, pa);
+    hipEventRecord(g_ev[k], s);
+    hipStreamWaitEvent(g_s2, g_ev[k], 0);
+    hipLaunchKernelGGL((k_gp_tile<TB_D, false, 536870912, NW, MT, NTW>), dim3((pc.n_j_max - 1) * pc.tiles_ub), dim3(64 * NW), 0, g_s2, pc);
+  }
+  hipEventRecord(g_ev[16], g_s2);
+  hipStreamWaitEvent(s, g_ev[16], 0);
+}
+
+template <int NW, int MT, int NTW, int XV = 0>
+void launch_kc_allcons(const TileParams& p, hipStream_t s) {   // producer, then consumers on every block
+  TileParams a = p, c = p;
+  a.j_skip = 0;
+  c.j_skip = 0;
+  hipLaunchKernelGGL((k_gp_tile<TB_D, false, 268435456 | XV, NW, MT, NTW>), dim3(p.tiles_ub), dim3(64 * NW), 0, s, a);
+  hipLaunchKernelGGL((k_gp_tile<TB_D, false, 536870912 | XV, NW, MT, NTW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, c);
+}
+template <int NW, int MT, int NTW>
+void launch_kc_allprod(const TileParams& p, hipStream_t s) {   // every block a producer (same values stored)
+  TileParams a = p;
+  a.j_skip = 0;
+  hipLaunchKernelGGL((k_gp_tile<TB_D, false, 268435456, NW, MT, NTW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, a);
+}
+template <int NW, int MT, int NTW>
+void launch_kc_prod(const TileParams& p, hipStream_t s) {
+  TileParams a = p;
+  a.j_skip = 0;
+  hipLaunchKernelGGL((k_gp_tile<TB_D, false, 268435456, NW, MT, NTW>), dim3(p.tiles_ub), dim3(64 * NW), 0, s, a);
+}
+template <int NW, int MT, int NTW>
+void launch_kc_cons(const TileParams& p, hipStream_t s) {
+  TileParams c = p;
+  c.j_skip = 1;
+  hipLaunchKernelGGL((k_gp_tile<TB_D, false, 536870912, NW, MT, NTW>), dim3((p.n_j_max - 1) * p.tiles_ub), dim3(64 * NW), 0, s, c);
+}
+
 int main(int argc, char** argv) {
   // argv: P N D (defaults: the config-2 observation GP); d = TB_D at compile time
   const int P = argc > 1 ? atoi(argv[1]) : 100000;
@@ -86,9 +143,29 @@ int main(int argc, char** argv) {
     p.X = X;
     for (int j = 0; j < d; ++j) p.ls[j] = 1.0;
     p.qpart = q; p.ld_q = P; p.mu = mu; p.ld_mu = D;
+    if (v == 2) {                       // K* cache for the production geometry
+      CK(hipMalloc(&p.kcache, (size_t)ntiles * ksteps(N) * 256 * geos[v].mt * 8));
+      for (int CH = 2; CH <= 8; CH *= 2) {
+        int* ct;
+        CK(hipMalloc(&ct, CH * 8 * sizeof(int)));
+        for (int k = 0; k < CH; ++k) {
+          const int t0 = (int)((long long)ntiles * k / CH), t1 = (int)((long long)ntiles * (k + 1) / CH);
+          int h[5] = {t0 * pt, std::min(P, t1 * pt), t0 * pt, 0, t1 - t0};
+          CK(hipMemcpy(ct + 8 * k, h, sizeof(h), hipMemcpyHostToDevice));
+          TileParams c = p;
+          c.tiles_ub = t1 - t0;
+          c.seg_pos_begin = ct + 8 * k; c.seg_pos_end = ct + 8 * k + 1; c.seg_out_base = ct + 8 * k + 2;
+          c.seg_tile_start = ct + 8 * k + 3;
+          c.kcache = p.kcache + (size_t)t0 * ksteps(N) * 256 * geos[v].mt;
+          g_chunk[CH].push_back(c);
+        }
+      }
+    }
   }
 
   hipStream_t s = nullptr;
+  CK(hipStreamCreateWithFlags(&g_s2, hipStreamNonBlocking));
+  for (int i = 0; i < 17; ++i) CK(hipEventCreateWithFlags(&g_ev[i], hipEventDisableTiming));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   typedef void (*L)(const TileParams&, hipStream_t);
@@ -99,13 +176,17 @@ int main(int argc, char** argv) {
               {launch_var<131072, 8>, 1, "64x512 LDS coords"}};
 #else
   V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512 production"},
-              {launch_var<16, 4, 2, 8>, 2, "no gen"},
-              {launch_var<16 | 32, 4, 2, 8>, 2, "no gen, no B loads"},
-              {launch_var<16 | 32 | 64, 4, 2, 8>, 2, "no gen/B/A reads"},
-              {launch_var<16 | 32 | 64 | 8, 4, 2, 8>, 2, "no gen/B/A/barrier"},
-              {launch_var<128, 4, 2, 8>, 2, "production fullK"},
-              {launch_var<16 | 128, 4, 2, 8>, 2, "no gen fullK"},
-              {launch_var<16 | 32 | 64 | 8 | 128, 4, 2, 8>, 2, "no gen/B/A/barrier fullK"}};
+              {launch_var<0, 4, 2, 8>, 2, "production again"},
+              {launch_kc_allprod<4, 2, 8>, 2, "K* cache: every block produces"},
+              {launch_kc_allcons<4, 2, 8>, 2, "K* cache: consumers on all J"},
+              {launch_kc_allcons<4, 2, 8, 1073741824>, 2, "K* cache: 8-B stores, global loads, all J"},
+              {launch_kc<4, 2, 8, 1>, 2, "K* cache: producer + consumer"},
+              {launch_kc<4, 2, 8, 2>, 2, "K* cache: 2 chunks, 2 streams"},
+              {launch_kc<4, 2, 8, 4>, 2, "K* cache: 4 chunks, 2 streams"},
+              {launch_kc<4, 2, 8, 8>, 2, "K* cache: 8 chunks, 2 streams"},
+              {launch_kc_prod<4, 2, 8>, 2, "K* cache: producer alone"},
+              {launch_kc_cons<4, 2, 8>, 2, "K* cache: consumer alone"},
+              {launch_var<16, 4, 2, 8>, 2, "no gen"}};
 #endif
   const int NV = sizeof(vars) / sizeof(vars[0]), ROUNDS = 7;
   std::vector<std::vector<float>> t(NV);
@@ -135,8 +216,67 @@ int main(int argc, char** argv) {
       CK(hipDeviceSynchronize());
       CK(hipMemcpy(q1.data(), q, nq * 8, hipMemcpyDeviceToHost));
       double md = 0, mx = 0;
-      for (size_t i = 0; i < nq; ++i) { md = std::max(md, std::abs(q1[i] - q0[i])); mx = std::max(mx, std::abs(q0[i])); }
-      printf("check %-30s max |q - q_production| = %.3g (max |q| %.3g)\n", vars[v].name, md, mx);
+      size_t ndiff = 0, imax = 0;
+      for (size_t i = 0; i < nq; ++i) {
+        const double dd = std::abs(q1[i] - q0[i]);
+        if (q1[i] != q0[i]) ++ndiff;
+        if (dd > md) { md = dd; imax = i; }
+        mx = std::max(mx, std::abs(q0[i]));
+      }
+      if (getenv("TB_KDUMP") && std::string(vars[v].name).find("all J") != std::string::npos) {
+        std::vector<size_t> byJ(pp[2].n_j_max, 0), byX(8, 0), tiles;
+        size_t tiles_bad = 0;
+        for (size_t i = 0; i < nq; ++i)
+          if (q1[i] != q0[i]) { ++byJ[i / P]; ++byX[((i % P) / 32) % 8]; }
+        for (int tt = 0; tt < P / 32; ++tt) {
+          bool b = false;
+          for (int J = 0; J < pp[2].n_j_max; ++J) for (int k = 0; k < 32; ++k) { size_t i = (size_t)J * P + tt * 32 + k; b |= q1[i] != q0[i]; }
+          tiles_bad += b;
+        }
+        printf("  by J:"); for (auto x : byJ) printf(" %zu", x);
+        printf("  by tile%%8:"); for (auto x : byX) printf(" %zu", x);
+        printf("  tiles with a difference: %zu of %d\n", tiles_bad, P / 32);
+        std::vector<double> q2(nq);
+        CK(hipMemset(q, 0, nq * 8));
+        vars[v].fn(pp[vars[v].pi], s);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(q2.data(), q, nq * 8, hipMemcpyDeviceToHost));
+        size_t nd2 = 0;
+        for (size_t i = 0; i < nq; ++i) nd2 += q2[i] != q1[i];
+        printf("  rerun of the same variant: %zu entries differ from the first run\n", nd2);
+      }
+      printf("check %-30s max |q - q_production| = %.3g (max |q| %.3g), %zu of %zu differ; worst [J=%zu, p=%zu] %.17g vs %.17g\n",
+             vars[v].name, md, mx, ndiff, nq, imax / P, imax % P, q1[imax], q0[imax]);
+    }
+  }
+  // K* cache contents after the producer alone vs the host value 2^(t/64) (TB_KDUMP)
+  if (getenv("TB_KDUMP")) {
+    const int nks = ksteps(N), MT = 2, NT = P / 32;
+    for (int rep = 0; rep < 3; ++rep) {
+    if (rep == 0) launch_kc_prod<4, 2, 8>(pp[2], s);
+    else if (rep == 1) launch_kc_allcons<4, 2, 8>(pp[2], s);
+    else launch_kc_allcons<4, 2, 8, 1073741824>(pp[2], s);
+    CK(hipDeviceSynchronize());
+    std::vector<double> kc((size_t)NT * nks * 256 * MT);
+    CK(hipMemcpy(kc.data(), pp[2].kcache, kc.size() * 8, hipMemcpyDeviceToHost));
+    size_t bad = 0, shown = 0;
+    for (int t = 0; t < NT; ++t)
+      for (int ks = 0; ks < nks; ++ks)
+        for (int kk = 0; kk < 4; ++kk)
+          for (int l = 0; l < 64; ++l)
+            for (int mt = 0; mt < MT; ++mt) {
+              const int pi = t * 32 + mt * 16 + (l & 15), r = ks * 16 + kk * 4 + (l >> 4);
+              double asq = 0, dot = 0;
+              for (int j = 0; j < d; ++j) { asq += hX[(size_t)pi * d + j] * hX[(size_t)pi * d + j]; dot += hX[(size_t)pi * d + j] * hXs[(size_t)r * d + j]; }
+              const double tt = -(asq * kLog2eX64 + hXsq[r]) + 2.0 * kLog2eX64 * dot;
+              const double ex = std::exp2(tt / 64.0);
+              const double got = kc[(((size_t)t * nks + ks) * 4 + kk) * 128 + l * 2 + mt];
+              if (!(std::abs(got - ex) <= 1e-12 * std::abs(ex) + 1e-300)) {
+                ++bad;
+                if (shown++ < 3) printf("kdump bad t=%d ks=%d kk=%d lane=%d mt=%d got %.17g want %.17g\n", t, ks, kk, l, mt, got, ex);
+              }
+            }
+    printf("kdump (%s): %zu bad of %zu\n", rep == 0 ? "producer alone" : rep == 1 ? "producer + consumers" : "8-B stores", bad, (size_t)NT * nks * 512);
     }
   }
   double rows = 0;   // per 16-column tile: rows up to its diagonal (or all, for mean tiles)
