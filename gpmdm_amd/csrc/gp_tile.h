@@ -534,11 +534,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
   auto loadA_part = [&](int ks, int kk) {
     const int kc = ks < ks_last ? ks : ks_last;
     const int soff = (kc * 4 + kk) * (64 * MT) * 8;
-    if constexpr ((VAR & 1073741824) != 0) {              // A/B: flat global loads
-      const double* src = prm.kcache + (long long)t * ksteps(n_rows) * (256 * MT) + (kc * 4 + kk) * (64 * MT) + lane * MT;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) an[kk * MT + mt] = src[mt];
-    } else if constexpr (MT == 1) {
+    if constexpr (MT == 1) {
       const v2u x = __builtin_amdgcn_raw_buffer_load_b64(krsrc, klane_off, soff, 0);
       an[kk] = __builtin_bit_cast(double, (unsigned long long)x.x | ((unsigned long long)x.y << 32));
     } else {
@@ -550,27 +546,14 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 && !(VAR & 67108864) ? ((VAR & 1
       }
     }
   };
+  // 8-byte stores: 16-byte stores of these registers (refilled by the next sub-step's LDS
+  // reads right behind the store) wrote a wrong low dword for 0.33% of the values
   auto storeA_part = [&](int ks, int kk, const double (&af)[MT]) {
     const int soff = (ks * 4 + kk) * (64 * MT) * 8;
-    if constexpr (MT == 1) {
-      const unsigned long long u = __builtin_bit_cast(unsigned long long, af[0]);
-      __builtin_amdgcn_raw_buffer_store_b64((v2u){(unsigned)u, (unsigned)(u >> 32)}, krsrc, klane_off, soff, 0);
-    } else {
-      if constexpr ((VAR & 1073741824) != 0) {              // A/B: 8-byte stores
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const unsigned long long u = __builtin_bit_cast(unsigned long long, af[mt]);
-          __builtin_amdgcn_raw_buffer_store_b64((v2u){(unsigned)u, (unsigned)(u >> 32)}, krsrc, klane_off + 8u * mt, soff, 0);
-        }
-      } else {
-#pragma unroll
-        for (int h = 0; h < MT / 2; ++h) {
-          const unsigned long long u0 = __builtin_bit_cast(unsigned long long, af[2 * h]);
-          const unsigned long long u1 = __builtin_bit_cast(unsigned long long, af[2 * h + 1]);
-          __builtin_amdgcn_raw_buffer_store_b128((v4u){(unsigned)u0, (unsigned)(u0 >> 32), (unsigned)u1, (unsigned)(u1 >> 32)},
-                                                 krsrc, klane_off + 16u * h, soff, 0);
-        }
-      }
+    for (int mt = 0; mt < MT; ++mt) {
+      const unsigned long long u = __builtin_bit_cast(unsigned long long, af[mt]);
+      __builtin_amdgcn_raw_buffer_store_b64((v2u){(unsigned)u, (unsigned)(u >> 32)}, krsrc, klane_off + 8u * mt, soff, 0);
     }
   };
 

@@ -178,12 +178,8 @@ int main(int argc, char** argv) {
   V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512 production"},
               {launch_var<0, 4, 2, 8>, 2, "production again"},
               {launch_kc_allprod<4, 2, 8>, 2, "K* cache: every block produces"},
-              {launch_kc_allcons<4, 2, 8>, 2, "K* cache: consumers on all J"},
-              {launch_kc_allcons<4, 2, 8, 1073741824>, 2, "K* cache: 8-B stores, global loads, all J"},
               {launch_kc<4, 2, 8, 1>, 2, "K* cache: producer + consumer"},
-              {launch_kc<4, 2, 8, 2>, 2, "K* cache: 2 chunks, 2 streams"},
-              {launch_kc<4, 2, 8, 4>, 2, "K* cache: 4 chunks, 2 streams"},
-              {launch_kc<4, 2, 8, 8>, 2, "K* cache: 8 chunks, 2 streams"},
+              {launch_kc_allcons<4, 2, 8>, 2, "K* cache: consumers on all J"},
               {launch_kc_prod<4, 2, 8>, 2, "K* cache: producer alone"},
               {launch_kc_cons<4, 2, 8>, 2, "K* cache: consumer alone"},
               {launch_var<16, 4, 2, 8>, 2, "no gen"}};
@@ -252,10 +248,10 @@ int main(int argc, char** argv) {
   // K* cache contents after the producer alone vs the host value 2^(t/64) (TB_KDUMP)
   if (getenv("TB_KDUMP")) {
     const int nks = ksteps(N), MT = 2, NT = P / 32;
-    for (int rep = 0; rep < 3; ++rep) {
+    for (int rep = 0; rep < 2; ++rep) {
     if (rep == 0) launch_kc_prod<4, 2, 8>(pp[2], s);
-    else if (rep == 1) launch_kc_allcons<4, 2, 8>(pp[2], s);
-    else launch_kc_allcons<4, 2, 8, 1073741824>(pp[2], s);
+    else launch_kc_allcons<4, 2, 8>(pp[2], s);
+
     CK(hipDeviceSynchronize());
     std::vector<double> kc((size_t)NT * nks * 256 * MT);
     CK(hipMemcpy(kc.data(), pp[2].kcache, kc.size() * 8, hipMemcpyDeviceToHost));
@@ -276,7 +272,7 @@ int main(int argc, char** argv) {
                 if (shown++ < 3) printf("kdump bad t=%d ks=%d kk=%d lane=%d mt=%d got %.17g want %.17g\n", t, ks, kk, l, mt, got, ex);
               }
             }
-    printf("kdump (%s): %zu bad of %zu\n", rep == 0 ? "producer alone" : rep == 1 ? "producer + consumers" : "8-B stores", bad, (size_t)NT * nks * 512);
+    printf("kdump (%s): %zu bad of %zu\n", rep == 0 ? "producer alone" : "producer + consumers", bad, (size_t)NT * nks * 512);
     }
   }
   double rows = 0;   // per 16-column tile: rows up to its diagonal (or all, for mean tiles)
