@@ -445,6 +445,47 @@ class GPMDM:
             var = var + extra * (torch.exp(self.x_log_lambdas) ** -2).to(var.device)[None, :]
         return mu, var
 
+    # ---- map read-outs used by train_gpmdm.ipynb (gpmdm.py:1103-1273) -------------
+    def get_next_x(self, gp_mean_out, gp_out_var, Xold, flg_sample: bool = False):
+        """gpmdm.py:1103-1145: the next latent state from a dynamics-GP output (the mean, or
+        a draw from N(mean, var) with torch's generator; 'delta' targets add Xold)."""
+        step = torch.distributions.Normal(gp_mean_out, torch.sqrt(gp_out_var)).rsample() if flg_sample else gp_mean_out
+        if self.dyn_target == "full":
+            return step
+        if self.dyn_target == "delta":
+            return Xold + step
+
+    @staticmethod
+    def _nmse(target, mu, var) -> float:
+        # the reference's expression, floor division included (gpmdm.py:1192, 1235, 1269)
+        return float(np.mean((target - mu) ** 2 // var))
+
+    def get_dynamics_map_performance_for_class(self, class_index: int, flg_noise: bool = False):
+        """gpmdm.py:1147-1196: class c's dynamics GP on every Xin row (all classes' rows,
+        as the reference does) -> (mean, var, Xout, Xin, NMSE) as numpy arrays."""
+        with torch.no_grad():
+            Xin, Xout, _ = self.get_Xin_Xout_matrices()
+            mu, var = self.map_x_dynamics_for_class(Xin, class_index, flg_noise=flg_noise)
+            mu, var, Xout, Xin = _to_np(mu), _to_np(var), _to_np(Xout), _to_np(Xin)
+        return mu, var, Xout, Xin, self._nmse(Xout, mu, var)
+
+    def get_latent_map_performance(self, flg_noise: bool = False):
+        """gpmdm.py:1199-1239: the observation GP at the training latents ->
+        (mean, var, Y, NMSE) as numpy arrays."""
+        with torch.no_grad():
+            mu, var = self.map_x_to_y(self.X, flg_noise=flg_noise)
+            mu, var = _to_np(mu), _to_np(var)
+            Y = self.get_Y() + self.meanY
+        return mu, var, Y, self._nmse(Y, mu, var)
+
+    def get_latent_map_performance_for_class(self, class_index: int, flg_noise: bool = False):
+        """gpmdm.py:1241-1273: as get_latent_map_performance on class c's latents."""
+        with torch.no_grad():
+            mu, var = self.map_x_to_y(self.get_X_for_class(class_index), flg_noise=flg_noise)
+            mu, var = _to_np(mu), _to_np(var)
+            Y = self.get_Y_for_class(class_index) + self.meanY
+        return mu, var, Y, self._nmse(Y, mu, var)
+
     # ---- persistence (gpmdm.py:1307-1414) ---------------------------------------
     def config_dict(self):
         return {

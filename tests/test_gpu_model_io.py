@@ -35,3 +35,36 @@ def test_reference_checkpoint_predictive_maps_and_step():
     pf.update_with_draws(z, E, nrm, u)
     r = O.step(om, T, st0["states"], st0["classes"], z, E, nrm, u)
     assert_step_matches(pf.export_state(), r, pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), u)
+
+
+def test_map_performance_readouts_match_reference():
+    """train_gpmdm.ipynb's evaluation calls (gpmdm.py:1147-1273) on the reference-written
+    checkpoint against the reference's own outputs for it (tests/golden/
+    make_map_performance.py).  NMSE is a mean of floors, (target - mu)^2 // var, so a
+    value within rounding of an integer may floor the other way: at most 0.2% of the
+    entries may differ by one."""
+    from gpmdm_amd import GPMDM
+    g = dict(np.load(GOLDEN / "ref_map_performance_config1.npz", allow_pickle=False))
+    m = GPMDM.load(GOLDEN / "ref_checkpoint_config1.pth")
+
+    def nmse_close(got, want, n):
+        assert abs(got - want) * n <= max(1.0, 0.002 * n), (got, want)
+
+    for c in range(m.n_classes):
+        mu, var, Xout, Xin, nmse = m.get_dynamics_map_performance_for_class(c)
+        assert np.array_equal(Xin, g["dyn_Xin"]) and np.array_equal(Xout, g["dyn_Xout"])
+        assert nrel(mu, g[f"dyn{c}_mu"]) < 1e-8, c
+        assert nrel(var, g[f"dyn{c}_var"]) < 1e-5, c
+        nmse_close(nmse, float(g[f"dyn{c}_nmse"]), mu.size)
+        lo, hi = g[f"obs{c}_rows"]
+        mu, var, Y, nmse = m.get_latent_map_performance_for_class(c)
+        assert nrel(mu, g["obs_mu"][lo:hi]) < 1e-8, c
+        assert nrel(var, g["obs_var"][lo:hi]) < 1e-6, c
+        nmse_close(nmse, float(g[f"obs{c}_nmse"]), mu.size)
+    mu, var, Y, nmse = m.get_latent_map_performance()
+    assert nrel(mu, g["obs_mu"]) < 1e-8
+    assert nrel(var, g["obs_var"]) < 1e-6
+    nmse_close(nmse, float(g["obs_nmse"]), mu.size)
+    # get_next_x: the mean for 'full' targets, a N(mean, var) draw with flg_sample
+    x = m.get_next_x(torch.ones(1, 3), torch.full((1, 3), 1e-12), torch.zeros(1, 3), flg_sample=True)
+    assert torch.allclose(x, torch.ones(1, 3), atol=1e-4)

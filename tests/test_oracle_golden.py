@@ -183,3 +183,24 @@ def test_systematic_resample_oracle():
         assert np.all(n >= np.floor(P * w - 1e-9)) and np.all(n <= np.ceil(P * w + 1e-9))
         u = (np.arange(P) + u0) / P
         assert np.array_equal(idx, O.multinomial_resample_indices(w, u))
+
+
+def test_oracle_map_performance_matches_reference():
+    """The oracle's maps on the reference-trained checkpoint reproduce the reference's
+    train_gpmdm.ipynb read-outs (gpmdm.py:1147-1273; tests/golden/make_map_performance.py),
+    NMSE with the reference's floor division (up to 0.2% of entries flooring the other way)."""
+    from conftest import GOLDEN
+    f = dict(np.load(GOLDEN / "ref_checkpoint_config1.npz", allow_pickle=False))
+    g = dict(np.load(GOLDEN / "ref_map_performance_config1.npz", allow_pickle=False))
+    om = oracle_model(f)
+    Xin, Xout, _ = om.xin_xout()
+    assert np.array_equal(Xin, g["dyn_Xin"]) and np.array_equal(Xout, g["dyn_Xout"])
+    for c in range(om.n_classes):
+        mu, var = om.map_x_dynamics_for_class(Xin, c)
+        assert nrel(mu, g[f"dyn{c}_mu"]) < 1e-8 and nrel(var, g[f"dyn{c}_var"]) < 1e-5
+        nmse = float(np.mean((Xout - mu) ** 2 // var))
+        assert abs(nmse - g[f"dyn{c}_nmse"]) * mu.size <= max(1.0, 0.002 * mu.size)
+    mu, var = om.map_x_to_y(om.X)
+    assert nrel(mu, g["obs_mu"]) < 1e-8 and nrel(var, g["obs_var"]) < 1e-6
+    nmse = float(np.mean((om.Y - mu) ** 2 // var))
+    assert abs(nmse - g["obs_nmse"]) * mu.size <= max(1.0, 0.002 * mu.size)
