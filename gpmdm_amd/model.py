@@ -445,6 +445,100 @@ class GPMDM:
             var = var + extra * (torch.exp(self.x_log_lambdas) ** -2).to(var.device)[None, :]
         return mu, var
 
+    # ---- kernel helpers (gpmdm.py:311-378, 381-548, 965-991, 1070-1101) ------------
+    # torch fp64 on the inputs' device; the per-frame path never calls them (the tile kernel
+    # generates its kernel rows itself), they serve analyses and the all-class map below.
+    def _par(self, t, like):
+        return t.to(device=like.device, dtype=torch.float64)
+
+    def get_weighted_distances(self, X1, X2, log_lengthscales_par):
+        """gpmdm.py:483-517 (expansion form)."""
+        return _sq_dist(X1, X2, self._par(log_lengthscales_par, X1))
+
+    def get_rbf_kernel(self, X1, X2, log_lengthscales_par, log_sigma_n_par, sigma_n_num=0, flg_noise=True):
+        """gpmdm.py:436-481 (noise on the diagonal of X1's rows when flg_noise)."""
+        K = torch.exp(-self.get_weighted_distances(X1, X2, log_lengthscales_par))
+        if flg_noise:
+            N = X1.shape[0]
+            eye = torch.eye(N, dtype=torch.float64, device=X1.device)
+            K = K + torch.exp(self._par(log_sigma_n_par, X1)) ** 2 * eye + sigma_n_num ** 2 * eye
+        return K
+
+    def get_lin_kernel(self, X1, X2, log_lin_coeff_par):
+        """gpmdm.py:520-548."""
+        return _lin(X1, X2, self._par(log_lin_coeff_par, X1))
+
+    def get_y_kernel(self, X1, X2, flg_noise=True):
+        """gpmdm.py:381-406."""
+        return self.get_rbf_kernel(X1, X2, self.y_log_lengthscales, self.y_log_sigma_n, self.sigma_n_num_Y, flg_noise)
+
+    def get_x_kernel(self, X1, X2, flg_noise=True):
+        """gpmdm.py:408-434 (RBF + linear)."""
+        return (self.get_rbf_kernel(X1, X2, self.x_log_lengthscales, self.x_log_sigma_n, self.sigma_n_num_X, flg_noise)
+                + self.get_lin_kernel(X1, X2, self.x_log_lin_coeff))
+
+    def get_y_diag_kernel(self, X, flg_noise=False):
+        """gpmdm.py:965-991."""
+        n = X.shape[0]
+        k = torch.ones(n, dtype=torch.float64, device=X.device)
+        if flg_noise:
+            k = k + torch.exp(self._par(self.y_log_sigma_n, X)) ** 2 + self.sigma_n_num_Y ** 2
+        return k
+
+    def get_x_diag_kernel(self, X, flg_noise=False):
+        """gpmdm.py:1070-1101: 1 + x~^T C^2 x~ (+ noise)."""
+        c2 = torch.exp(self._par(self.x_log_lin_coeff, X)) ** 2
+        k = 1.0 + (X * X) @ c2[:-1] + c2[-1]
+        if flg_noise:
+            k = k + torch.exp(self._par(self.x_log_sigma_n, X)) ** 2 + self.sigma_n_num_X ** 2
+        return k
+
+    def _class_rows(self):
+        return [sum(len(s) - 1 for s in seqs) for seqs in self.class_aware_observations_list]
+
+    def get_M(self):
+        """gpmdm.py:311-340: block-diagonal ones, one Nx x Nx block per class (dense, as the
+        reference builds it; the library itself only ever stores the class blocks)."""
+        rows = self._class_rows()
+        return torch.block_diag(*[torch.ones(n, n, dtype=torch.float64) for n in rows])
+
+    def get_M_for_class(self, class_index: int):
+        """gpmdm.py:342-378: the class's block of get_M, zeros elsewhere."""
+        rows = self._class_rows()
+        o = sum(rows[:class_index])
+        M = torch.zeros(sum(rows), sum(rows), dtype=torch.float64)
+        M[o:o + rows[class_index], o:o + rows[class_index]] = 1.0
+        return M
+
+    def map_x_dynamics(self, Xstar, flg_noise: bool = False):
+        """gpmdm.py:993-1030: the all-class dynamics map with Kx_inv = inverse of the
+        M-masked kernel (block diagonal: per class block, no 1e-6 jitter, gpmdm.py:1291-1295)
+        against the unmasked K(Xin, X*), i.e. sum over classes of the class-block terms.
+        Torch fp64 on the model's device, class blocks only (not on the per-frame path)."""
+        if self.dyn_back_step != 1:
+            raise NotImplementedError("dyn_back_step=2 models are not supported (as in the reference filter)")
+        dev = self.device
+        xs = torch.as_tensor(Xstar, dtype=torch.float64)
+        out_dev = xs.device
+        xs = xs.to(dev)
+        Xin, Xout, _ = self.get_Xin_Xout_matrices()
+        Xin, Xout = Xin.to(dev), Xout.to(dev)
+        mean = torch.zeros(xs.shape[0], self.d, dtype=torch.float64, device=dev)
+        quad = torch.zeros(xs.shape[0], dtype=torch.float64, device=dev)
+        o = 0
+        for n in self._class_rows():
+            xi, xo = Xin[o:o + n], Xout[o:o + n]
+            U, _ = torch.linalg.cholesky_ex(self.get_x_kernel(xi, xi), upper=True)   # info ignored, as the reference
+            Ui = torch.inverse(U)
+            A = Ui @ Ui.T
+            ks = self.get_x_kernel(xi, xs, False)
+            mean = mean + (xo.T @ A @ ks).T
+            quad = quad + torch.sum((ks.T @ A) * ks.T, dim=1)
+            o += n
+        vc = self.get_x_diag_kernel(xs, flg_noise) - quad
+        lam = torch.exp(self.x_log_lambdas.to(dev)) ** -2
+        return mean.to(out_dev), (vc[:, None] * lam[None, :]).to(out_dev)
+
     # ---- map read-outs used by train_gpmdm.ipynb (gpmdm.py:1103-1273) -------------
     def get_next_x(self, gp_mean_out, gp_out_var, Xold, flg_sample: bool = False):
         """gpmdm.py:1103-1145: the next latent state from a dynamics-GP output (the mean, or

@@ -12,7 +12,9 @@ below belong to ``ref_checkpoint_config1.pth``.  Written (numbers only):
 ``get_latent_map_performance_for_class(c)`` (NMSE and its row range: its means and variances
 are those rows of the all-rows read-out to 1e-10, asserted here) and once ``get_latent_map_performance()``
 (means, variances, NMSE).  The reference computes NMSE with floor division,
-``(Y - mu) ** 2 // var``.
+``(Y - mu) ** 2 // var``.  Also: the all-class ``map_x_dynamics`` at 32 fixed points and a few
+kernel-helper values (get_x/y_kernel with and without noise, the diagonal kernels, row sums of
+get_M / get_M_for_class).
 Run here only: the reference never travels to the GPU box.
 """
 from __future__ import annotations
@@ -58,6 +60,20 @@ def main():
         arr[f"obs{c}_nmse"] = np.float64(nmse_c)
         arr[f"obs{c}_rows"] = np.array([off, off + n])
         off += n
+    # the all-class dynamics map and the kernel helpers at fixed query points
+    rng = np.random.RandomState(21)
+    Xin_t, _, _ = m.get_Xin_Xout_matrices()
+    xq = torch.tensor(rng.randn(32, cfg["d"]), dtype=torch.float64)
+    with torch.no_grad():
+        mu, var = m.map_x_dynamics(xq)
+        arr.update({"alldyn_xs": xq.numpy(), "alldyn_mu": mu.numpy(), "alldyn_var": var.numpy(),
+                    "k_x_noise": m.get_x_kernel(Xin_t[:7], Xin_t[3:10]).numpy(),
+                    "k_x": m.get_x_kernel(Xin_t[:7], xq[:4], False).numpy(),
+                    "k_y_noise": m.get_y_kernel(m.X[:6], m.X[2:8]).numpy(),
+                    "kd_x": m.get_x_diag_kernel(xq, True).numpy(),
+                    "kd_y": m.get_y_diag_kernel(xq, True).numpy(),
+                    "M_rowsums": m.get_M().sum(1).numpy(),
+                    "M1_rowsums": m.get_M_for_class(1).sum(1).numpy()})
     np.savez_compressed(OUT / "ref_map_performance_config1.npz", **arr)
     print("wrote ref_map_performance_config1.npz:",
           {k: float(v) for k, v in arr.items() if k.endswith("nmse")})

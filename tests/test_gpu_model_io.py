@@ -68,3 +68,14 @@ def test_map_performance_readouts_match_reference():
     # get_next_x: the mean for 'full' targets, a N(mean, var) draw with flg_sample
     x = m.get_next_x(torch.ones(1, 3), torch.full((1, 3), 1e-12), torch.zeros(1, 3), flg_sample=True)
     assert torch.allclose(x, torch.ones(1, 3), atol=1e-4)
+
+
+def test_all_class_dynamics_map_matches_reference():
+    """map_x_dynamics (gpmdm.py:993-1030: the M-masked, un-jittered Kx_inv against the
+    unmasked kernel) on the reference-trained checkpoint."""
+    from gpmdm_amd import GPMDM
+    g = dict(np.load(GOLDEN / "ref_map_performance_config1.npz", allow_pickle=False))
+    m = GPMDM.load(GOLDEN / "ref_checkpoint_config1.pth")
+    mu, var = m.map_x_dynamics(torch.tensor(g["alldyn_xs"]))
+    assert nrel(mu.numpy(), g["alldyn_mu"]) < 1e-8
+    assert nrel(var.numpy(), g["alldyn_var"]) < 1e-6

@@ -75,3 +75,23 @@ def test_reference_written_checkpoint_loads(tmp_path):
     m.save(q)
     m2 = GPMDM.load(q, upload=False)
     assert np.array_equal(m2.X.numpy(), f["X"]) and np.array_equal(m2.get_Y(), f["Y"])
+
+
+def test_kernel_helpers_match_reference():
+    """GPMDM's kernel helpers (gpmdm.py:311-548, 965-991, 1070-1101) on the reference-trained
+    checkpoint against the reference's own values (tests/golden/make_map_performance.py);
+    host tensors, no device model."""
+    from pathlib import Path
+    golden = Path(__file__).resolve().parent / "golden"
+    g = dict(np.load(golden / "ref_map_performance_config1.npz", allow_pickle=False))
+    m = GPMDM.load(golden / "ref_checkpoint_config1.pth", upload=False)
+    Xin, _, _ = m.get_Xin_Xout_matrices()
+    xq = torch.tensor(g["alldyn_xs"])
+    close = lambda a, b: np.testing.assert_allclose(a.numpy(), b, rtol=1e-12, atol=1e-13)
+    close(m.get_x_kernel(Xin[:7], Xin[3:10]), g["k_x_noise"])
+    close(m.get_x_kernel(Xin[:7], xq[:4], False), g["k_x"])
+    close(m.get_y_kernel(m.X[:6], m.X[2:8]), g["k_y_noise"])
+    close(m.get_x_diag_kernel(xq, True), g["kd_x"])
+    close(m.get_y_diag_kernel(xq, True), g["kd_y"])
+    close(m.get_M().sum(1), g["M_rowsums"])
+    close(m.get_M_for_class(1).sum(1), g["M1_rowsums"])
