@@ -113,7 +113,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(X, hX.data(), (size_t)P * d * 8, hipMemcpyHostToDevice));
   // geometries: {waves, particle tiles MT, column tiles per wave NTW}
   struct Geo { int nw, mt, ntw; };
-  const Geo geos[] = {{4, 4, 4}, {8, 4, 4}, {4, 2, 8}, {4, 1, 16}, {4, 1, 8}, {4, 2, 6}};
+  const Geo geos[] = {{4, 4, 4}, {8, 4, 4}, {4, 2, 8}, {4, 1, 16}, {4, 1, 8}, {4, 2, 6}, {8, 2, 8}};
   const int NGEO = sizeof(geos) / sizeof(geos[0]);
   TileParams pp[NGEO];
   int* tabs;
@@ -176,6 +176,12 @@ int main(int argc, char** argv) {
               {launch_var<131072, 8>, 1, "64x512 LDS coords"}};
 #else
   V vars[] = {{launch_var<0, 4, 2, 8>, 2, "32x512 production"},
+              {launch_var<0, 8, 2, 8>, 6, "32x1024 NW8, sync every 2"},
+              {launch_var<65536, 8, 2, 8>, 6, "32x1024 NW8, sync every 4"},
+              {launch_var<65536 | 16, 8, 2, 8>, 6, "32x1024 NW8 sync 4, no gen"},
+              {launch_var<65536 | 4096, 8, 2, 8>, 6, "32x1024 NW8 sync 4, gen interleaved"},
+              {launch_var<65536 | 8192, 8, 2, 8>, 6, "32x1024 NW8 sync 4, gen split"},
+              {launch_var<65536 | 2, 8, 2, 8>, 6, "32x1024 NW8 sync 4, cheap exp"},
               {launch_var<0, 4, 2, 8>, 2, "production again"},
               {launch_kc_allprod<4, 2, 8>, 2, "K* cache: every block produces"},
               {launch_kc<4, 2, 8, 1>, 2, "K* cache: producer + consumer"},
