@@ -120,8 +120,10 @@ def pmc_traffic(cfg):
             continue
         key = "obs_gemm_hbm_bytes_per_launch" if cfg == 2 else f"config{cfg}_obs_gemm_hbm_bytes_per_launch"
         if j.get(key) is not None:
+            sub = j if cfg == 2 else j.get(f"config{cfg}", {})   # each configuration's passes name their build
+            commit = sub.get("commit") or j.get("commit") or "unrecorded"
             return j[key], (f"profiles/{name}: rocprofv3 --pmc passes (FETCH_SIZE x2 + WRITE_SIZE, gfx950 "
-                            f"correction) of bench.py --config {cfg} at commit {j.get('commit', 'unrecorded')}")
+                            f"correction) of bench.py --config {cfg} at commit {commit}")
     return None, None
 
 
