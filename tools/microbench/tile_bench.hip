@@ -113,7 +113,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(X, hX.data(), (size_t)P * d * 8, hipMemcpyHostToDevice));
   // geometries: {waves, particle tiles MT, column tiles per wave NTW}
   struct Geo { int nw, mt, ntw; };
-  const Geo geos[] = {{4, 4, 4}, {8, 4, 4}, {4, 2, 8}, {4, 1, 16}, {4, 1, 8}, {4, 2, 6}, {8, 2, 8}};
+  const Geo geos[] = {{4, 4, 4}, {8, 4, 4}, {4, 2, 8}, {4, 1, 16}, {4, 1, 8}, {4, 2, 6}, {8, 2, 8}, {4, 1, 4}, {4, 2, 4}};
   const int NGEO = sizeof(geos) / sizeof(geos[0]);
   TileParams pp[NGEO];
   int* tabs;
@@ -170,7 +170,13 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   typedef void (*L)(const TileParams&, hipStream_t);
   struct V { L fn; int pi; const char* name; };
-#if TB_D > 12
+#if defined(TB_SHAPES)
+  // tile shapes on a small-row problem (the de-duplicated dynamics GP: a few thousand rows
+  // against N_c ~ 1000 training rows): run as  tile_bench_shapes 7200 995 3
+  V vars[] = {{launch_var<0, 4, 1, 4>, 7, "16x256"}, {launch_var<0, 4, 1, 8>, 4, "16x512"},
+              {launch_var<0, 4, 2, 4>, 8, "32x256"}, {launch_var<0, 4, 2, 8>, 2, "32x512"},
+              {launch_var<0, 4, 4, 4>, 0, "64x256"}};
+#elif TB_D > 12
   V vars[] = {{launch_var<0, 4>, 0, "64x256"}, {launch_var<0, 8>, 1, "64x512 (NW8)"},
               {launch_var<0, 4, 2, 8>, 2, "32x512 (VGPR coords)"}, {launch_var<131072, 4, 2, 8>, 2, "32x512 LDS coords"},
               {launch_var<131072, 8>, 1, "64x512 LDS coords"}};
