@@ -595,6 +595,41 @@ class GPMDM:
             "x_lin_coeff_init": torch.exp(self.x_log_lin_coeff).tolist(),
         }
 
+    # ---- torch.nn.Module-style parameter access (the reference class is an nn.Module whose
+    # parameters are registered in this order, gpmdm.py:201-230, 773) ----------------------
+    _PARAMS = ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n", "x_log_lengthscales",
+               "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff", "X")
+
+    def named_parameters(self):
+        for k in self._PARAMS:
+            if getattr(self, k, None) is not None:
+                yield k, getattr(self, k)
+
+    def parameters(self):
+        for _, v in self.named_parameters():
+            yield v
+
+    def state_dict(self):
+        """The reference's state_dict keys (as ``GPMDM.save`` stores them), float64 copies."""
+        import collections
+        return collections.OrderedDict((k, v.detach().clone()) for k, v in self.named_parameters())
+
+    def load_state_dict(self, state_dict, strict: bool = True):
+        """Install parameters by the reference's names; the device model is rebuilt (and
+        filters built on this model rebind on their next call)."""
+        missing = [k for k in self._PARAMS if k not in state_dict]
+        unexpected = [k for k in state_dict if k not in self._PARAMS]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"load_state_dict: missing keys {missing}, unexpected keys {unexpected}")
+        for k in self._PARAMS[:-1]:
+            if k in state_dict:
+                setattr(self, k, torch.as_tensor(_to_np(state_dict[k]), dtype=torch.float64).reshape(
+                    getattr(self, k).shape).clone())
+        if "X" in state_dict:
+            self.set_latents(state_dict["X"])
+        elif self.X is not None:
+            self._precompute_kernel_inverses()
+
     def save(self, file_path) -> None:
         """Save to a pickle-free ``.npz`` (the reference's torch.save dict holds numpy
         arrays that torch>=2.6 refuses to load with weights_only=True)."""

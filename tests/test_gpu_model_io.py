@@ -79,3 +79,21 @@ def test_all_class_dynamics_map_matches_reference():
     mu, var = m.map_x_dynamics(torch.tensor(g["alldyn_xs"]))
     assert nrel(mu.numpy(), g["alldyn_mu"]) < 1e-8
     assert nrel(var.numpy(), g["alldyn_var"]) < 1e-6
+
+
+def test_load_state_dict_rebuilds_the_device_model():
+    """load_state_dict installs parameters by the reference's names and rebuilds the device
+    model; a filter built before rebinds (the reference filter reads its model live)."""
+    from gpmdm_amd import GPMDM, GPMDM_PF, synthetic
+    m = GPMDM.load(GOLDEN / "ref_checkpoint_config1.pth")
+    xs = torch.tensor(np.random.RandomState(4).randn(64, 3))
+    mu0, var0 = m.map_x_to_y(xs)
+    pf = GPMDM_PF(m, torch.tensor(synthetic.markov_matrix(2)), 1000, rng="philox", seed=3)
+    sd = m.state_dict()
+    sd["y_log_lambdas"] = sd["y_log_lambdas"] + 0.1
+    m.load_state_dict(sd)
+    mu1, var1 = m.map_x_to_y(xs)
+    assert nrel(mu1.numpy(), mu0.numpy()) < 1e-12            # the mean does not use the lambdas
+    assert nrel(var1.numpy(), var0.numpy() * np.exp(-0.2)) < 1e-12
+    pf.update(np.zeros(m.D))                                 # rebinds to the rebuilt model
+    assert np.isfinite(pf.class_probabilities().numpy()).all()

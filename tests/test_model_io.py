@@ -95,3 +95,24 @@ def test_kernel_helpers_match_reference():
     close(m.get_y_diag_kernel(xq, True), g["kd_y"])
     close(m.get_M().sum(1), g["M_rowsums"])
     close(m.get_M_for_class(1).sum(1), g["M1_rowsums"])
+
+
+def test_state_dict_matches_reference_checkpoint():
+    """state_dict()/named_parameters() carry the reference nn.Module's parameter names in its
+    registration order (gpmdm.py:201-230, 773) and the values GPMDM.save stored."""
+    from pathlib import Path
+    pth = Path(__file__).resolve().parent / "golden" / "ref_checkpoint_config1.pth"
+    _, ref_sd = read_reference_checkpoint(pth)
+    m = GPMDM.load(pth, upload=False)
+    sd = m.state_dict()
+    assert list(sd.keys()) == list(ref_sd.keys())
+    for k, v in ref_sd.items():
+        assert torch.equal(sd[k], v.to(torch.float64)), k
+    assert [k for k, _ in m.named_parameters()] == list(sd.keys())
+    assert len(list(m.parameters())) == len(sd)
+    try:
+        m.load_state_dict({"X": sd["X"]})
+    except RuntimeError as e:
+        assert "missing keys" in str(e)
+    else:
+        raise AssertionError("strict load_state_dict accepted a partial state")
