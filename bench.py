@@ -1,6 +1,7 @@
 """Benchmark: GPMDM particle-filter step on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config {2,3,4,5}]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config {1,2,3,4,5}]
+                    [--rng {auto,philox,torch}] [--stream {mocap,predictive}] [--y-lambda L]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Workload (BASELINE.json configs[1]): N=2000 training latents, D=62, d=3, C=2 classes, 500 frames,
@@ -10,6 +11,22 @@ observation stream.  One step = ``update(z)`` + ``class_proba
 with device-side Philox draws and the reference's multinomial resampling.
 ``--config 3|4|5`` runs the other BASELINE.json configurations (per-GPU share of P for
 the 8-GPU ones); they are not the headline line.
+
+``--config 1`` is the notebook's own filter (N=500, P=100) in the drop-in's default mode:
+``rng='torch'`` (host draws from torch's generator in the reference's order, uploaded per
+frame) and multinomial resampling; the line adds ``ms_per_frame`` beside the reference's
+published 78.2 ms/frame (test_gpmdm_pf.ipynb:259-260) and its 16.3 ms measured in the
+build container, and ``bank``: the 39-trial loop of test_gpmdm_pf.ipynb
+cell 4 as one GPMDM_PF_Bank of 39 filters x 100 particles stepped per frame.
+
+``--stream predictive`` replaces the mocap-surrogate observation stream by one drawn from
+the filter's own predictive distribution: a first, untimed pass of the same filter (same
+seed) takes at each frame a random particle x_r of the current cloud and observes
+z = mu(x_r) + sqrt(var(x_r)) eps (map_x_to_y); the timed pass replays those z on a fresh
+filter, which follows the same trajectory bit for bit (checked).  ``--y-lambda`` sets the
+observation GP's output scales (exp(y_log_lambdas)); below 1 the likelihood is less peaked.
+Together they keep the cloud spread out (ESS well above the mocap stream's ~0.3%), so the
+resample path and the dynamics tiles are timed on many distinct ancestors.
 
 Prints ONE JSON line (rank 0) with the contract fields plus:
   roofline      dominant kernel (observation-GP tile kernel) vs the FP64 MFMA peak;
@@ -66,6 +83,7 @@ def build_model(device):
     w = WORKLOAD
     data = synthetic.make_sequences(w["C"], w["S"], w["L"], w["D"], w["d"], seed=0)
     hp = synthetic.default_hyperparameters(w["D"], w["d"], 0.1)
+    hp["y_lambdas_init"] = hp["y_lambdas_init"] * w["y_lambda"]
     m = GPMDM(D=w["D"], d=w["d"], n_classes=w["C"], dyn_target="full", dyn_back_step=1, device=device, **hp)
     for c in range(w["C"]):
         for y in data.sequences[c]:
@@ -127,23 +145,48 @@ def pmc_traffic(cfg):
     return None, None
 
 
-def cpu_baseline(data, budget_s=20.0):
+def host_cores():
+    """(threads the environment caps BLAS at, cores this process may run on, nproc)."""
+    nproc = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = nproc
+    capped = None
+    for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+        v = os.environ.get(k)
+        if v and v.isdigit():
+            capped = int(v)
+            break
+    return capped, usable, nproc
+
+
+def cgroup_cpu_quota():
+    """CPUs the cgroup's CFS quota allows (cgroup v2 cpu.max), or None."""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except Exception:
+        return None
+
+
+def cpu_baseline(data, budget_s=12.0):
     """The numpy oracle on the same workload: this configuration's own particle count when
-    N <= 2000 (configs 1, 2, 4: a few frames of P = 100k / 125k), 1000 particles above."""
+    N <= 2000 (configs 1, 2, 4: a few frames of P = 100k / 125k), a 1000-particle sample
+    above.  Runs once on every core this process may use (threadpoolctl sets the BLAS pool;
+    ``cores``) and, when the environment caps the BLAS threads (OMP_NUM_THREADS on the GPU
+    box), once more at that cap (``capped``)."""
     from oracle import gpmdm_oracle as O
     from gpmdm_amd import synthetic
     import torch
-    try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
-    except Exception:
-        cores = os.cpu_count() or 1
-    torch_threads = torch.get_num_threads()
+    from threadpoolctl import threadpool_limits
+    capped, usable, nproc = host_cores()
     w = WORKLOAD
     from sklearn.decomposition import PCA
     Y = np.concatenate([y for c in data.sequences for y in c]).astype(np.float64)
     X = PCA(n_components=w["d"]).fit_transform(Y)
     hp = synthetic.default_hyperparameters(w["D"], w["d"], 0.1)
+    hp["y_lambdas_init"] = hp["y_lambdas_init"] * w["y_lambda"]
     N = Y.shape[0]
     m = O.OracleModel(X=X, Y=Y, seq_lengths=[[w["L"]] * w["S"]] * w["C"],
                       y_log_lengthscales=np.log(hp["y_lengthscales_init"]), y_log_lambdas=np.log(hp["y_lambdas_init"]),
@@ -154,24 +197,138 @@ def cpu_baseline(data, budget_s=20.0):
     T = synthetic.markov_matrix(w["C"])
     Ps = w["P_per_gpu"] if N <= 2000 else 1000
     Ps -= Ps % w["C"]
-    rng = np.random.RandomState(0)
-    parts = [rng.randint(0, m.X_for_class(c).shape[0], Ps // w["C"]) for c in range(w["C"])]
-    s, c = O.init_particles(m, Ps, parts)
     z = data.observation_stream(64, seed=1)
-    steps, t0 = 0, time.perf_counter()
-    while True:
-        r = O.step(m, T, s, c, z[steps % 64], rng.exponential(size=(Ps, w["C"])), rng.randn(Ps, w["d"]), rng.rand(Ps))
-        s, c = r.states, r.classes
-        steps += 1
-        el = time.perf_counter() - t0
-        if el > budget_s or steps >= (3 if Ps >= 100_000 else 50):
-            break
-    return {"value": Ps * steps / el, "unit": "particle-steps/s", "cores": int(cores), "kind": "port",
-            "nproc": os.cpu_count(), "torch_threads": int(torch_threads),
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
-            "sample": f"oracle (numpy fp64 restatement of gpmdm_pf.py's step, BLAS on {cores} threads) N={N} "
-                      f"D={w['D']} d={w['d']} C={w['C']}, P={Ps} particles x {steps} frames in {el:.1f} s "
-                      f"(model precompute excluded)"}
+
+    def run(threads):
+        rng = np.random.RandomState(0)
+        parts = [rng.randint(0, m.X_for_class(c).shape[0], Ps // w["C"]) for c in range(w["C"])]
+        s, c = O.init_particles(m, Ps, parts)
+        with threadpool_limits(threads):
+            steps, t0 = 0, time.perf_counter()
+            while True:
+                r = O.step(m, T, s, c, z[steps % 64], rng.exponential(size=(Ps, w["C"])), rng.randn(Ps, w["d"]),
+                           rng.rand(Ps))
+                s, c = r.states, r.classes
+                steps += 1
+                el = time.perf_counter() - t0
+                if el > budget_s or steps >= (3 if Ps >= 100_000 else 50):
+                    break
+        return Ps * steps / el, steps, el
+
+    v, steps, el = run(usable)
+    rec = {"value": v, "unit": "particle-steps/s", "cores": int(usable), "kind": "port",
+           "nproc": nproc, "sched_affinity_cores": usable, "cgroup_cpu_quota": cgroup_cpu_quota(), "torch_threads": int(torch.get_num_threads()),
+           "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+           "sample": f"oracle (numpy fp64 restatement of gpmdm_pf.py's step, BLAS pool set to all {usable} usable "
+                     f"cores) N={N} D={w['D']} d={w['d']} C={w['C']}, P={Ps} particles x {steps} frames in "
+                     f"{el:.1f} s (model precompute excluded)",
+           "calibration": "port vs the unmodified reference on 8 threads of the build container: "
+                          "profiles/r03/cpu_calibration.txt, BASELINE.md §2"}
+    if capped and capped != usable:
+        vc, sc, ec = run(capped)
+        rec["capped"] = {"value": vc, "cores": capped, "frames": sc, "seconds": ec,
+                         "note": "BLAS pool at the environment's OMP_NUM_THREADS cap"}
+    return rec
+
+
+def predictive_stream(pf, model, frames, seed=5):
+    """Observations drawn from the filter's own predictive distribution (see the module
+    docstring): frame f observes z = mu(x_r) + sqrt(var(x_r)) eps for a uniformly chosen
+    particle r of the cloud after frame f - 1.  Returns the stream and the last frame's
+    posterior (the timed replay must reproduce it bit for bit)."""
+    import torch
+    rng = np.random.RandomState(seed)
+    zs = np.zeros((frames + 64, model.D))
+    ess = []
+    for f in range(frames):
+        st = pf.export_state()
+        x = torch.tensor(st["states"][rng.randint(len(st["states"]))][None, :])
+        mu, var = model.map_x_to_y(x)
+        zs[f] = mu.numpy()[0] + np.sqrt(np.maximum(var.numpy()[0], 0.0)) * rng.randn(model.D)
+        pf.update(zs[f])
+        if f >= frames - 10:
+            w = pf.export_state()["w"]
+            ess.append(float(1.0 / np.sum(w * w)))
+    zs[frames:] = zs[:64]
+    return zs, {"posterior": pf.class_probabilities().numpy(), "generator_ess_last10_mean": float(np.mean(ess)),
+                "note": "z_f = mu(x_r) + sqrt(var(x_r)) eps, r a uniform particle of the cloud after frame "
+                        "f-1, from an untimed pass of the same filter (same seed); the timed pass replays "
+                        "the stream"}
+
+
+def nodedup_line(model, T, P_total, group, dist, device, zs, steps, rng):
+    """The same step with ancestor de-duplication off (every particle's dynamics GP)."""
+    import torch
+    from gpmdm_amd import GPMDM_PF
+    n_nd = min(steps, 20)
+    torch.manual_seed(11)
+    pf_nd = GPMDM_PF(model, T, P_total, rng=rng, seed=11 if rng == "philox" else None, process_group=group,
+                     dedup=False)
+    for k in range(3):
+        pf_nd.update(zs[k])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t_nd = time.perf_counter()
+    for k in range(n_nd):
+        pf_nd.update(zs[3 + k])
+        pf_nd.get_most_likely_class()
+        pf_nd.class_probabilities()
+        pf_nd.current_state_mean()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el_nd = time.perf_counter() - t_nd
+    if dist is not None:
+        t = torch.tensor([el_nd], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el_nd = float(t.item())
+    pf_nd.enable_timing(True)
+    for k in range(min(n_nd, 10)):
+        pf_nd.update(zs[3 + n_nd + k])
+    torch.cuda.synchronize()
+    pf_nd.enable_timing(False)
+    nd_stages = pf_nd.stage_times()
+    P_local = P_total // (dist.get_world_size() if dist is not None else 1)
+    return {"ms_per_step": el_nd / n_nd * 1e3, "value": P_total * n_nd / el_nd, "steps": n_nd,
+            "stages_ms_per_step": {k: v[0] / max(v[1], 1) for k, v in nd_stages.items()},
+            "dyn_gemm_tflops": dyn_row_flops(model) * P_local / max(nd_stages["dyn_gemm"][0] / max(nd_stages["dyn_gemm"][1], 1), 1e-9) / 1e9,
+            "note": "dedup=False: the dynamics GP runs on every particle (the reference's work) on "
+                    "the wide dynamics tiles; the same filter as the headline's up to summation order; "
+                    "dyn_gemm_tflops = algorithmic N_c(N_c+1) + 2 N_c d FLOP per row (class mean) / "
+                    "launch time"}
+
+
+def bank_line(model, T, F, P, zs, warmup, steps):
+    """test_gpmdm_pf.ipynb cell 4's trial loop as one bank: F filters of P particles, each
+    frame one bank update plus the read-outs (every filter sees its own observation; here
+    the stream shifted by the filter index)."""
+    import torch
+    from gpmdm_amd import GPMDM_PF_Bank
+    bank = GPMDM_PF_Bank(model, T, F, P, seed=11)
+    n = len(zs) - F
+
+    def frame(k):
+        Z = np.stack([zs[(k + f) % n] for f in range(F)])
+        bank.update(Z)
+        bank.get_most_likely_class()
+        bank.class_probabilities()
+        bank.current_state_mean()
+
+    for k in range(warmup):
+        frame(k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        frame(warmup + k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"filters": F, "particles_per_filter": P, "frames": steps, "ms_per_frame": el / steps * 1e3,
+            "ms_per_filter_frame": el / steps / F * 1e3, "value": F * P * steps / el,
+            "unit": "particle-steps/s", "rng": "philox (a bank draws on the device)",
+            "note": "one GPMDM_PF_Bank update + get_most_likely_class + class_probabilities + "
+                    "current_state_mean per frame for all filters; the notebook runs its 39 trials one "
+                    "after another with one filter"}
 
 
 def main():
@@ -182,11 +339,22 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--config", type=int, default=2, choices=(1, 2, 3, 4, 5))
+    ap.add_argument("--rng", default="auto", choices=("auto", "philox", "torch"),
+                    help="auto: 'torch' (the drop-in default, host draws) for config 1, else 'philox'")
+    ap.add_argument("--stream", default="mocap", choices=("mocap", "predictive"))
+    ap.add_argument("--y-lambda", type=float, default=1.0)
+    ap.add_argument("--bank", type=int, default=None,
+                    help="filters of the bank line (config 1: 39, the notebook's test trials)")
+    ap.add_argument("--no-nodedup", action="store_true")
     args = ap.parse_args()
     global WORKLOAD
     WORKLOAD = workload(args.config)
+    WORKLOAD["y_lambda"] = args.y_lambda
     if args.steps is None:
-        args.steps = 20 if args.config in (3, 5) else 500
+        args.steps = 20 if args.config in (3, 5) else (200 if args.config == 1 else 500)
+    rng = args.rng if args.rng != "auto" else ("torch" if args.config == 1 else "philox")
+    if args.bank is None:
+        args.bank = 39 if args.config == 1 else 0
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -223,10 +391,20 @@ def main():
     P_total = WORKLOAD["P_per_gpu"] * world
     from gpmdm_amd import synthetic
     T = torch.from_numpy(synthetic.markov_matrix(WORKLOAD["C"]))
-    torch.manual_seed(11)
-    pf = GPMDM_PF(model, T, P_total, rng="philox", seed=11, process_group=group)
     n_breakdown = min(args.steps, 10)
-    zs = data.observation_stream(args.warmup + args.steps + n_breakdown + 64, seed=1)
+    n_frames = args.warmup + args.steps + n_breakdown + 64
+
+    def new_filter(**kw):
+        torch.manual_seed(11)
+        return GPMDM_PF(model, T, P_total, rng=rng, seed=11 if rng == "philox" else None,
+                        process_group=group, **kw)
+
+    stream_check = None
+    if args.stream == "predictive":
+        zs, stream_check = predictive_stream(new_filter(), model, args.warmup + args.steps + n_breakdown)
+    else:
+        zs = data.observation_stream(n_frames, seed=1)
+    pf = new_filter()
     log(f"[bench] rank {rank}/{world} setup {time.perf_counter() - t_setup:.1f}s, P_total={P_total}")
 
     def one(k):
@@ -266,39 +444,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     post = pf.class_probabilities().numpy()
+    if stream_check is not None:     # the timed filter followed the stream's own trajectory
+        stream_check["replay_matches"] = bool(np.array_equal(post, stream_check.pop("posterior")))
     dyn_rows = pf.dynamics_rows()
     w_last = pf.export_state()["w"]
     ess = float(1.0 / np.sum(w_last * w_last))
-    # the same step without ancestor de-duplication (every particle's dynamics GP evaluated)
-    n_nd = min(args.steps, 20)
-    pf_nd = GPMDM_PF(model, T, P_total, rng="philox", seed=11, process_group=group, dedup=False)
-    for k in range(3):
-        pf_nd.update(zs[k])
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    t_nd = time.perf_counter()
-    for k in range(n_nd):
-        pf_nd.update(zs[3 + k])
-        pf_nd.get_most_likely_class()
-        pf_nd.class_probabilities()
-        pf_nd.current_state_mean()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    el_nd = time.perf_counter() - t_nd
-    if dist is not None:
-        t = torch.tensor([el_nd], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el_nd = float(t.item())
-    pf_nd.enable_timing(True)
-    for k in range(min(n_nd, 10)):
-        pf_nd.update(zs[3 + n_nd + k])
-    torch.cuda.synchronize()
-    pf_nd.enable_timing(False)
-    nd_stages = pf_nd.stage_times()
-    del pf_nd
-
+    bank = bank_line(model, T, args.bank, P_total, zs, args.warmup, args.steps) if args.bank and world == 1 else None
+    nodedup = None if args.no_nodedup else nodedup_line(model, T, P_total, group, dist, device, zs, args.steps, rng)
     N, D, d = model.X.shape[0], model.D, model.d
     P_local = P_total // world
     alg, dense, executed = obs_kernel_flops(N, D)
@@ -321,7 +473,12 @@ def main():
         "dtype": "f64",
         "data": "synthetic (SURVEY §8(d) generator; random-phase sinusoid mocap surrogate, PCA latents)",
         "config": {"workload": f"configs[{WORKLOAD['cfg'] - 1}]: N={N} D={D} d={d} C={model.n_classes}, "
-                               f"P={P_local} particles per GPU, philox draws, multinomial resampling",
+                               f"P={P_local} particles per GPU, "
+                               f"{'philox (device) draws' if rng == 'philox' else 'torch (host) draws'}, "
+                               f"multinomial resampling"
+                               + (f", predictive observation stream" if args.stream == "predictive" else "")
+                               + (f", y_lambda={args.y_lambda}" if args.y_lambda != 1.0 else ""),
+                   "rng": rng, "stream": args.stream, "y_lambda": args.y_lambda,
                    "N": N, "D": D, "d": d, "C": model.n_classes, "P_per_gpu": P_local, "P_total": P_total,
                    "frames": args.warmup + args.steps,
                    "parallelism": f"particles sharded over {world} GPU(s), one all-gather per step"},
@@ -342,14 +499,9 @@ def main():
                      "dense_form_equivalent_tflops": dense * P_local / obs_launch_s / 1e12,
                      "launch_ms": obs_launch_s * 1e3},
         "stages_ms_per_step": {k: v[0] / max(v[1], 1) for k, v in breakdown.items()},
-        "nodedup": {"ms_per_step": el_nd / n_nd * 1e3, "value": P_total * n_nd / el_nd, "steps": n_nd,
-                    "stages_ms_per_step": {k: v[0] / max(v[1], 1) for k, v in nd_stages.items()},
-                    "dyn_gemm_tflops": dyn_row_flops(model) * P_local / max(nd_stages["dyn_gemm"][0] / max(nd_stages["dyn_gemm"][1], 1), 1e-9) / 1e9,
-                    "note": "dedup=False: the dynamics GP runs on every particle (the reference's work) on "
-                            "the wide dynamics tiles; the same filter as the headline's up to summation order; "
-                            "dyn_gemm_tflops = algorithmic N_c(N_c+1) + 2 N_c d FLOP per row (class mean) / "
-                            "launch time"},
+        "nodedup": nodedup,
         "ess_last": ess,
+        "stream_check": stream_check,
         "ess_frac_last": ess / P_total,
         "posterior_last": [float(x) for x in post],
         "dyn_rows_last": {"evaluated": dyn_rows, "particles": P_local,
@@ -360,6 +512,15 @@ def main():
                                   "identical ancestor de-duplication, DESIGN.md §3); breakdown_mean and "
                                   "dyn_gemm_tflops over the stage-breakdown pass"},
     }
+    if bank is not None:
+        rec["bank"] = bank
+    if args.config == 1:
+        ms = elapsed / args.steps * 1e3
+        rec["ms_per_frame"] = ms
+        rec["reference_ms_per_frame"] = {
+            "published": 78.2, "published_source": "test_gpmdm_pf.ipynb:259-260 (12.78 FPS, author's laptop CPU)",
+            "container": 16.3, "container_source": "BASELINE.md §2 (unmodified reference, 8 cores, N=500, P=100)",
+            "speedup_vs_published": 78.2 / ms, "speedup_vs_container": 16.3 / ms}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             rec["cpu_baseline"] = cpu_baseline(data)

@@ -702,12 +702,21 @@ __global__ __launch_bounds__(1024) void k_readout(ResampleArgs a) {
     }
     __syncthreads();
   }
-  if (tid == 0) {
-    double cl = 0.0;
-    for (int c = 0; c < a.C; ++c) cl += tot[c];
-    for (int c = 0; c < a.C; ++c) readout[c] = tot[c] / cl;   // class_probabilities
-    for (int j = 0; j < a.d; ++j) readout[a.C + j] = tot[a.C + 1 + j];  // current_state_mean
-    readout[a.C + a.d] = tot[a.C];                                       // log_likelihood()
+  // one value per lane, so every store is 8 bytes: a one-lane loop was vectorised into
+  // 16-byte stores (the >8-byte store-data hazard; tests/test_isa_guard.py)
+  const int nro = a.C + a.d + 1;
+  if (tid < nro) {
+    double v;
+    if (tid < a.C) {                                     // class_probabilities
+      double cl = 0.0;
+      for (int c = 0; c < a.C; ++c) cl += tot[c];
+      v = tot[tid] / cl;
+    } else if (tid < a.C + a.d) {
+      v = tot[tid + 1];                                  // current_state_mean
+    } else {
+      v = tot[a.C];                                      // log_likelihood()
+    }
+    readout[tid] = v;
   }
 }
 

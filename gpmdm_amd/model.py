@@ -631,8 +631,46 @@ class GPMDM:
             self._precompute_kernel_inverses()
 
     def save(self, file_path) -> None:
-        """Save to a pickle-free ``.npz`` (the reference's torch.save dict holds numpy
-        arrays that torch>=2.6 refuses to load with weights_only=True)."""
+        """gpmdm.py:1307-1346.  Writes exactly ``file_path``:
+
+        * any suffix but ``.npz``: the reference's own layout, ``torch.save({'state_dict':
+          <the 8 parameters in registration order>, 'config_dict': <the reference's 17 keys,
+          observations as the arrays add_data received>})`` -- a file the reference's
+          ``GPMDM.load`` and this class's ``load`` both read;
+        * ``.npz``: a pickle-free archive (the torch layout holds numpy arrays, which
+          ``torch.load(weights_only=True)`` reads only with numpy allow-listed)."""
+        if Path(file_path).suffix != ".npz":
+            return self._save_reference_layout(file_path)
+        return self._save_npz(file_path)
+
+    def _reference_config_dict(self):
+        """The reference's config_dict (gpmdm.py:1317-1336), keys in its order."""
+        def ex(t):
+            return t.detach().exp()
+        return {
+            "class_aware_observations_list": [list(c) for c in self.class_aware_observations_list],
+            "dyn_target": self.dyn_target,
+            "dyn_back_step": self.dyn_back_step,
+            "D": self.D, "d": self.d, "n_classes": self.n_classes,
+            "sigma_n_num_X": self.sigma_n_num_X, "sigma_n_num_Y": self.sigma_n_num_Y,
+            "dtype": str(self.dtype),
+            "device": str(self.device),
+            "y_lengthscales_init": ex(self.y_log_lengthscales).tolist(),
+            "y_lambdas_init": ex(self.y_log_lambdas).tolist(),
+            "y_sigma_n_init": ex(self.y_log_sigma_n).item(),
+            "x_lengthscales_init": ex(self.x_log_lengthscales).tolist(),
+            "x_lambdas_init": ex(self.x_log_lambdas).tolist(),
+            "x_sigma_n_init": ex(self.x_log_sigma_n).item(),
+            "x_lin_coeff_init": ex(self.x_log_lin_coeff).tolist(),
+        }
+
+    def _save_reference_layout(self, file_path):
+        sd = self.state_dict()
+        sd._metadata = {"": {"version": 1}}   # what nn.Module.state_dict attaches (and pickles)
+        with open(file_path, "wb") as fh:     # a file object: torch.save adds no suffix
+            torch.save({"state_dict": sd, "config_dict": self._reference_config_dict()}, fh)
+
+    def _save_npz(self, file_path):
         arrays = {"X": self.X.numpy()}
         seq_len = []
         for c, cls in enumerate(self.class_aware_observations_list):
@@ -647,17 +685,31 @@ class GPMDM:
         arrays["cfg_int"] = np.asarray([cfg["D"], cfg["d"], cfg["n_classes"], cfg["dyn_back_step"]], dtype=np.int64)
         arrays["cfg_target"] = np.asarray([0 if cfg["dyn_target"] == "full" else 1], dtype=np.int64)
         arrays["cfg_num"] = np.asarray([cfg["sigma_n_num_X"], cfg["sigma_n_num_Y"]], dtype=np.float64)
-        np.savez(file_path, **arrays)
+        with open(file_path, "wb") as fh:     # a file object: np.savez adds no suffix
+            np.savez(fh, **arrays)
+
+    @staticmethod
+    def _is_npz(path) -> bool:
+        """True for a numpy archive (a zip of ``.npy`` members), False for a torch archive
+        (a zip holding ``<name>/data.pkl``) or torch's legacy non-zip pickle stream; the
+        file's content decides, not its suffix."""
+        import zipfile
+        if not zipfile.is_zipfile(path):
+            return False
+        with zipfile.ZipFile(path) as z:
+            names = z.namelist()
+        return bool(names) and all(n.endswith(".npy") for n in names)
 
     @classmethod
     def load(cls, file_path, flg_print: bool = False, device=None, upload: bool = True) -> "GPMDM":
-        """Load a model saved by ``save`` (.npz), or a reference ``.pth`` (gpmdm.py:1349-1414)
-        through ``torch.load(weights_only=True)`` with numpy arrays allow-listed.
-        ``upload=False`` stops before the device precompute (host-side inspection)."""
+        """gpmdm.py:1349-1414.  Reads either format ``save`` writes -- the reference's torch
+        layout (also any file the reference itself wrote) through ``torch.load(weights_only
+        =True)`` with numpy arrays allow-listed, or the pickle-free ``.npz`` -- chosen by the
+        file's content.  ``upload=False`` stops before the device precompute."""
         path = Path(file_path)
         names = ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n", "x_log_lengthscales",
                  "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff")
-        if path.suffix == ".npz":
+        if cls._is_npz(path):
             f = np.load(path, allow_pickle=False)
             D, d, C, bs = (int(v) for v in f["cfg_int"])
             target = "full" if int(f["cfg_target"][0]) == 0 else "delta"

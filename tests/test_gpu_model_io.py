@@ -97,3 +97,56 @@ def test_load_state_dict_rebuilds_the_device_model():
     assert nrel(var1.numpy(), var0.numpy() * np.exp(-0.2)) < 1e-12
     pf.update(np.zeros(m.D))                                 # rebinds to the rebuilt model
     assert np.isfinite(pf.class_probabilities().numpy()).all()
+
+
+def test_notebook_train_save_load_filter_chain(tmp_path):
+    """train_gpmdm.ipynb cells 3-5 (construct, add_data, init_X, train_adam, save to .pth)
+    -> test_gpmdm_pf.ipynb / view_gpmdm_pf.ipynb (GPMDM.load of that .pth, GPMDM_PF with
+    100 particles, the per-frame update / get_most_likely_class / class_probabilities /
+    current_state_mean loop writing into a torch tensor), unchanged but for the import
+    line.  The loaded model is the trained one bit for bit: its maps and a filter run under
+    the same torch seed equal the trained model's."""
+    from gpmdm_amd import GPMDM, GPMDM_PF, synthetic
+    data = synthetic.make_sequences(C=2, S=3, L=40, D=12, d=4, seed=5)
+    d, DOFs = 4, 12
+    gpdm = GPMDM(D=DOFs, d=d, n_classes=2, dyn_target='full', dyn_back_step=1,
+                 y_lambdas_init=np.ones(DOFs), y_lengthscales_init=np.ones(d), y_sigma_n_init=1e-2,
+                 x_lambdas_init=np.ones(d), x_lengthscales_init=np.ones(d), x_sigma_n_init=1e-2,
+                 x_lin_coeff_init=np.ones(d + 1))
+    for c, seqs in enumerate(data.sequences):
+        for arr in seqs:
+            gpdm.add_data(np.asarray(arr, dtype=np.float32), c)
+    gpdm.init_X()
+    gpdm.train_adam(num_opt_steps=5, num_print_steps=0, lr=0.01)
+    path = tmp_path / "gpmdm_4d_30fps.pth"
+    gpdm.save(f"{path}")
+    assert path.exists()
+
+    loaded = GPMDM.load(path)
+    assert torch.equal(loaded.X, gpdm.X)
+    xs = torch.tensor(np.random.RandomState(2).randn(50, d))
+    for c in range(2):
+        a, b = gpdm.map_x_dynamics_for_class(xs, c), loaded.map_x_dynamics_for_class(xs, c)
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert torch.equal(gpdm.map_x_to_y(xs)[1], loaded.map_x_to_y(xs)[1])
+
+    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
+    frames = data.observation_stream(30, seed=1).astype(np.float32)
+
+    def run(model):
+        torch.manual_seed(0)
+        gpdm_pf = GPMDM_PF(model, markov_switching_model=T, num_particles=100)
+        gpdm_pf.reset()
+        states = torch.zeros((len(frames), gpdm_pf.latent_dim))
+        labels, probs = [], []
+        for total, z in enumerate(frames):
+            gpdm_pf.update(z)
+            labels.append(gpdm_pf.get_most_likely_class())
+            probs.append(gpdm_pf.class_probabilities().numpy().copy())
+            states[total] = gpdm_pf.current_state_mean()
+        return labels, np.array(probs), states
+
+    l1, p1, s1 = run(gpdm)
+    l2, p2, s2 = run(loaded)
+    assert l1 == l2 and np.array_equal(p1, p2) and torch.equal(s1, s2)
+    assert np.all(np.isfinite(p1)) and np.allclose(p1.sum(1), 1.0)

@@ -116,3 +116,68 @@ def test_state_dict_matches_reference_checkpoint():
         assert "missing keys" in str(e)
     else:
         raise AssertionError("strict load_state_dict accepted a partial state")
+
+
+def _structure(cfg, sd):
+    """Keys, types, dtypes and shapes of a checkpoint (values aside)."""
+    def desc(v):
+        if isinstance(v, torch.Tensor):
+            return ("tensor", str(v.dtype), tuple(v.shape))
+        if isinstance(v, np.ndarray):
+            return ("ndarray", str(v.dtype), v.ndim)
+        if isinstance(v, list):
+            return ("list", desc(v[0]) if v else None)
+        return (type(v).__name__,)
+    return ([(k, desc(v)) for k, v in sd.items()],
+            [(k, desc(v)) for k, v in cfg.items() if k not in ("class_aware_observations_list", "device")],
+            [[desc(s) for s in c] for c in cfg["class_aware_observations_list"]])
+
+
+def test_pth_round_trip_exact_path(tmp_path):
+    """save("m.pth") writes the reference's torch layout to exactly that path (gpmdm.py:
+    1307-1345) and load("m.pth") gives X, the log-parameters and the observations back bit
+    for bit (train_gpmdm.ipynb:366 -> test_gpmdm_pf.ipynb:38)."""
+    from conftest import GOLDEN
+    m = GPMDM.load(GOLDEN / "ref_checkpoint_config1.pth", upload=False)
+    p = tmp_path / "gpmdm_4d_30fps.pth"
+    m.save(str(p))
+    assert p.exists() and not (tmp_path / "gpmdm_4d_30fps.pth.npz").exists()
+    assert not GPMDM._is_npz(p)
+    m2 = GPMDM.load(p, upload=False)
+    assert torch.equal(m2.X, m.X)
+    for k, v in m.state_dict().items():
+        assert torch.equal(m2.state_dict()[k], v), k
+    assert (m2.D, m2.d, m2.n_classes, m2.dyn_target, m2.dyn_back_step) == (m.D, m.d, m.n_classes, "full", 1)
+    for c1, c2 in zip(m.class_aware_observations_list, m2.class_aware_observations_list):
+        assert len(c1) == len(c2)
+        for a, b in zip(c1, c2):
+            assert a.dtype == b.dtype and np.array_equal(a, b)
+    # .npz stays the pickle-free option, written to exactly its path, also found by content
+    q = tmp_path / "m.npz"
+    m.save(q)
+    assert GPMDM._is_npz(q)
+    r = tmp_path / "renamed.pth"
+    q.rename(r)
+    m3 = GPMDM.load(r, upload=False)
+    assert torch.equal(m3.X, m.X) and np.array_equal(m3.get_Y(), m.get_Y())
+
+
+def test_pth_layout_matches_reference_written_file(tmp_path):
+    """Our .pth and the reference-written checkpoint have the same keys (in order), types,
+    dtypes and shapes, read with the same safe loader; the config values the reference
+    derives from the parameters agree."""
+    from conftest import GOLDEN
+    ref = GOLDEN / "ref_checkpoint_config1.pth"
+    cfg_r, sd_r = read_reference_checkpoint(ref)
+    m = GPMDM.load(ref, upload=False)
+    p = tmp_path / "ours.pth"
+    m.save(p)
+    cfg_o, sd_o = read_reference_checkpoint(p)
+    assert list(cfg_o.keys()) == list(cfg_r.keys())
+    assert list(sd_o.keys()) == list(sd_r.keys())
+    assert _structure(cfg_o, sd_o) == _structure(cfg_r, sd_r)
+    assert getattr(sd_o, "_metadata", None) == getattr(sd_r, "_metadata", None)
+    for k in ("y_lengthscales_init", "y_lambdas_init", "y_sigma_n_init", "x_lengthscales_init",
+              "x_lambdas_init", "x_sigma_n_init", "x_lin_coeff_init", "dtype", "D", "d", "n_classes",
+              "dyn_target", "dyn_back_step", "sigma_n_num_X", "sigma_n_num_Y"):
+        assert cfg_o[k] == cfg_r[k], k
