@@ -23,6 +23,8 @@ GPMDM_RNG_PHILOX = 1
 GPMDM_RESAMPLE_MULTINOMIAL = 0
 GPMDM_RESAMPLE_SYSTEMATIC = 1
 GPMDM_PACK_ALL, GPMDM_PACK_STATES, GPMDM_PACK_LL = 0, 1, 2
+GPMDM_COMM_PAD_ROWS = 1
+GPMDM_COMM_ID_BYTES = 128
 DYN_TILES = {"auto": 0, "narrow": 1, "wide": 2}
 STAGES = ("switch", "dyn_gemm", "dyn_finish", "obs_gemm", "obs_finish", "resample")
 HEALTH = ("obs_var_nonpositive", "obs_ll_nonfinite", "dyn_var_nonpositive", "dyn_state_nonfinite")
@@ -76,6 +78,10 @@ _SIGS = {
     "gpmdm_pf_set_model": (c_int, [c_void_p, c_void_p]),
     "gpmdm_pf_health": (c_int, [c_void_p, _i64p, c_int, c_void_p]),
     "gpmdm_pf_predict": (c_int, [c_void_p, _dp, c_void_p]),
+    "gpmdm_pf_set_comm": (c_int, [c_void_p, c_void_p, c_int]),
+    "gpmdm_comm_unique_id": (c_int, [c_void_p]),
+    "gpmdm_comm_init": (c_int, [c_int, c_int, c_void_p, c_int, POINTER(c_void_p)]),
+    "gpmdm_comm_destroy": (c_int, [c_void_p]),
     "gpmdm_gp_factor": (c_int, [c_int, _dp, c_int64, c_int32, _dp, _dp, c_double, c_double, c_double,
                                 _dp, c_int64, _dp, _dp]),
     "gpmdm_spd_inverse": (c_int, [c_int, c_void_p, c_int64, _dp, c_void_p]),

@@ -94,7 +94,7 @@ def _build_lib(force: bool = False, verbose: bool = False) -> Path:
     objs = [str(OBJ / (s + ".o")) for s in SOURCES]
     if force or jobs or not LIB.exists():
         run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *objs,
-             "-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"])
+             "-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
     return LIB
 
 

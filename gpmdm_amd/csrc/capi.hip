@@ -9,6 +9,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/gpmdm_hip.h"
 #include "common.h"
 #include "host_image.h"
@@ -196,6 +198,31 @@ struct gpmdm_pf {
   unsigned long long* gmax = nullptr;
   double *e = nullptr, *local = nullptr, *blocksum = nullptr, *blockoffw = nullptr, *total = nullptr,
          *cum = nullptr, *partials = nullptr, *readout = nullptr;
+  // library-driven exchange (gpmdm_pf_set_comm): an RCCL communicator of n_ranks ranks, a
+  // library-owned stream for the collectives, and the packed rows.  pad = rows per rank in
+  // the collective (the largest shard; ranks' shards differ by at most one row).  When the
+  // shards are uneven (or GPMDM_COMM_PAD_ROWS asks for it) the gather lands in *_stage and
+  // each rank's rows are copied down to their shard offset.
+  ncclComm_t comm = nullptr;
+  hipStream_t cstream = nullptr;
+  hipEvent_t cev[3] = {nullptr, nullptr, nullptr};
+  long long pad = 0;
+  bool padded = false;
+  double *xs_send = nullptr, *xs_recv = nullptr, *xs_stage = nullptr;
+  double *xl_send = nullptr, *xl_recv = nullptr, *xl_stage = nullptr;
+  void release_comm() {
+    if (cstream) (void)hipStreamSynchronize(cstream);
+    double* bufs[] = {xs_send, xs_recv, xs_stage, xl_send, xl_recv, xl_stage};
+    for (double* b : bufs) dfree(b);
+    xs_send = xs_recv = xs_stage = xl_send = xl_recv = xl_stage = nullptr;
+    for (auto& e : cev) {
+      if (e) (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+    if (cstream) (void)hipStreamDestroy(cstream);
+    cstream = nullptr;
+    comm = nullptr;                    // the caller owns the communicator
+  }
   // timing
   bool timing = false;
   std::vector<hipEvent_t> pool;
@@ -216,6 +243,7 @@ struct gpmdm_pf {
   const int* own_order() const { return own_valid ? own : nullptr; }
 
   ~gpmdm_pf() {
+    release_comm();
     double* ds[] = {T, X, X_prop, ll, qdyn, mudyn, qobs, sobs, z, E, normals, U,
                     e, local, blocksum, blockoffw, total, cum, partials, readout,
                     pred_q, pred_mu, pred_mu_p, pred_out};
@@ -946,13 +974,134 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
   return GPMDM_OK;
 }
 
+static int pack_part(gpmdm_pf* pf, double* send, int part, hipStream_t s);
+static int unpack_part(gpmdm_pf* pf, const double* recv, int part, hipStream_t s);
+
+static int nccl_fail(ncclResult_t r, const char* what) {
+  return fail(GPMDM_E_HIP, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+// rows [0, pad) of every rank's send buffer -> recv (even shards) or the staging buffer,
+// whose rank-k rows are then copied to [lo_k, hi_k) of recv (uneven shards), on cstream
+static int gather_rows(gpmdm_pf* pf, const double* send, double* recv, double* stage, int width) {
+  const size_t cnt = (size_t)pf->pad * width;
+  const ncclResult_t r = ncclAllGather(send, pf->padded ? stage : recv, cnt, ncclDouble, pf->comm, pf->cstream);
+  if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
+  if (pf->padded) {
+    for (int k = 0; k < pf->n_ranks; ++k) {
+      const long long lo = pf->P * k / pf->n_ranks, hi = pf->P * (k + 1) / pf->n_ranks;
+      if (hi > lo)
+        HIPCHK(hipMemcpyAsync(recv + lo * width, stage + (size_t)k * cnt, sizeof(double) * (hi - lo) * width,
+                              hipMemcpyDeviceToDevice, pf->cstream));
+    }
+  }
+  return GPMDM_OK;
+}
+
+// propagate with the library's own exchange (gpmdm_pf_set_comm), the schedule of
+// gpmdm_amd/pf.py's process-group path: {class, state} all-gathered on the library stream
+// while the observation GP runs on the caller's stream, then {ll}; the caller's stream
+// waits for both gathers before unpacking (replaces the reference's single-process
+// normalise/resample inputs, gpmdm_pf.py:194-213).
+static int propagate_exchange(gpmdm_pf* pf, const double* zh, const double* normals, hipStream_t s) {
+  const int d = pf->m->d;
+  TRY(propagate_dynamics(pf, normals, s));
+  TRY(pack_part(pf, pf->xs_send, GPMDM_PACK_STATES, s));
+  HIPCHK(hipEventRecord(pf->cev[0], s));
+  HIPCHK(hipStreamWaitEvent(pf->cstream, pf->cev[0], 0));
+  TRY(gather_rows(pf, pf->xs_send, pf->xs_recv, pf->xs_stage, d + 1));
+  TRY(weigh(pf, zh, s));
+  TRY(pack_part(pf, pf->xl_send, GPMDM_PACK_LL, s));
+  HIPCHK(hipEventRecord(pf->cev[1], s));
+  HIPCHK(hipStreamWaitEvent(pf->cstream, pf->cev[1], 0));
+  TRY(gather_rows(pf, pf->xl_send, pf->xl_recv, pf->xl_stage, 1));
+  HIPCHK(hipEventRecord(pf->cev[2], pf->cstream));
+  HIPCHK(hipStreamWaitEvent(s, pf->cev[2], 0));
+  TRY(unpack_part(pf, pf->xs_recv, GPMDM_PACK_STATES, s));
+  TRY(unpack_part(pf, pf->xl_recv, GPMDM_PACK_LL, s));
+  return GPMDM_OK;
+}
+
 int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, void* stream) {
   CHECK(pf && zh, "null argument");
   if (!pf->switched) return fail(GPMDM_E_STATE, "propagate called before switch");
   if (pf->rng_mode == GPMDM_RNG_REPLAY) CHECK(normals, "replay mode needs the dynamics normals");
   HIPCHK(hipSetDevice(pf->m->device));
+  if (pf->comm) return propagate_exchange(pf, zh, normals, (hipStream_t)stream);
   const int rc = propagate_dynamics(pf, normals, (hipStream_t)stream);
   return rc ? rc : weigh(pf, zh, (hipStream_t)stream);
+}
+
+int gpmdm_pf_set_comm(gpmdm_pf_t pf, void* rccl_comm, int flags) {
+  CHECK(pf, "null handle");
+  CHECK((flags & ~GPMDM_COMM_PAD_ROWS) == 0, "bad flags");
+  CHECK(!pf->switched && !pf->propagated, "set_comm between switch and resample");
+  HIPCHK(hipSetDevice(pf->m->device));
+  pf->release_comm();
+  if (!rccl_comm) return GPMDM_OK;
+  CHECK(pf->F == 1, "filter banks shard filters, not particles: no communicator");
+  ncclComm_t comm = (ncclComm_t)rccl_comm;
+  int n = 0, r = 0, dev = -1;
+  ncclResult_t e = ncclCommCount(comm, &n);
+  if (e != ncclSuccess) return nccl_fail(e, "ncclCommCount");
+  e = ncclCommUserRank(comm, &r);
+  if (e != ncclSuccess) return nccl_fail(e, "ncclCommUserRank");
+  e = ncclCommCuDevice(comm, &dev);
+  if (e != ncclSuccess) return nccl_fail(e, "ncclCommCuDevice");
+  CHECK(n == pf->n_ranks && r == pf->rank, "communicator size/rank differ from the filter's n_ranks/rank");
+  CHECK(dev == pf->m->device, "communicator is on another device than the model");
+  const int d = pf->m->d;
+  const long long mx = cdiv(pf->P, pf->n_ranks);            // largest shard
+  pf->padded = (pf->P % pf->n_ranks) != 0 || (flags & GPMDM_COMM_PAD_ROWS);
+  pf->pad = mx + ((flags & GPMDM_COMM_PAD_ROWS) ? 1 : 0);
+  const long long rows = pf->pad * pf->n_ranks;
+  int rc = 0;
+  auto fail_out = [&](int code) { pf->release_comm(); return code; };
+  if ((rc = dalloc(&pf->xs_send, (size_t)pf->pad * (d + 1))) || (rc = dalloc(&pf->xl_send, (size_t)pf->pad)) ||
+      (rc = dalloc(&pf->xs_recv, (size_t)pf->P * (d + 1))) || (rc = dalloc(&pf->xl_recv, (size_t)pf->P)))
+    return fail_out(rc);
+  if (pf->padded &&
+      ((rc = dalloc(&pf->xs_stage, (size_t)rows * (d + 1))) || (rc = dalloc(&pf->xl_stage, (size_t)rows))))
+    return fail_out(rc);
+  // padding rows of the send buffers travel but are dropped: keep them defined
+  if (hipMemset(pf->xs_send, 0, sizeof(double) * pf->pad * (d + 1)) != hipSuccess ||
+      hipMemset(pf->xl_send, 0, sizeof(double) * pf->pad) != hipSuccess ||
+      hipStreamCreateWithFlags(&pf->cstream, hipStreamNonBlocking) != hipSuccess)
+    return fail_out(fail(GPMDM_E_HIP, "communicator stream / buffers"));
+  for (auto& ev : pf->cev)
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+      return fail_out(fail(GPMDM_E_HIP, "communicator events"));
+  pf->comm = comm;
+  return GPMDM_OK;
+}
+
+int gpmdm_comm_unique_id(void* id) {
+  CHECK(id, "null argument");
+  ncclUniqueId u;
+  const ncclResult_t e = ncclGetUniqueId(&u);
+  if (e != ncclSuccess) return nccl_fail(e, "ncclGetUniqueId");
+  static_assert(sizeof(ncclUniqueId) == GPMDM_COMM_ID_BYTES, "ncclUniqueId size");
+  std::memcpy(id, &u, sizeof(u));
+  return GPMDM_OK;
+}
+
+int gpmdm_comm_init(int n_ranks, int rank, const void* id, int device, void** comm) {
+  CHECK(id && comm && n_ranks >= 1 && rank >= 0 && rank < n_ranks, "bad argument");
+  *comm = nullptr;
+  HIPCHK(hipSetDevice(device));
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  ncclComm_t c = nullptr;
+  const ncclResult_t e = ncclCommInitRank(&c, n_ranks, u, rank);
+  if (e != ncclSuccess) return nccl_fail(e, "ncclCommInitRank");
+  *comm = c;
+  return GPMDM_OK;
+}
+
+int gpmdm_comm_destroy(void* comm) {
+  if (!comm) return GPMDM_OK;
+  const ncclResult_t e = ncclCommDestroy((ncclComm_t)comm);
+  return e == ncclSuccess ? GPMDM_OK : nccl_fail(e, "ncclCommDestroy");
 }
 
 int gpmdm_pf_propagate_dynamics(gpmdm_pf_t pf, const double* normals, void* stream) {
@@ -990,6 +1139,10 @@ int gpmdm_pf_pack_part(gpmdm_pf_t pf, double* send, int part, void* stream) {
   CHECK(pf && send, "null argument");
   CHECK(part >= GPMDM_PACK_ALL && part <= GPMDM_PACK_LL, "part must be GPMDM_PACK_*");
   HIPCHK(hipSetDevice(pf->m->device));
+  return pack_part(pf, send, part, (hipStream_t)stream);
+}
+
+static int pack_part(gpmdm_pf* pf, double* send, int part, hipStream_t s) {
   PackArgs a{};
   a.n = pf->nloc;
   a.lo = pf->lo;
@@ -1000,7 +1153,7 @@ int gpmdm_pf_pack_part(gpmdm_pf_t pf, double* send, int part, void* stream) {
   a.ll = pf->ll;
   a.cls = pf->cls_new;
   a.X = pf->X_prop;
-  launch_pack(a, (hipStream_t)stream);
+  launch_pack(a, s);
   HIPCHK(hipGetLastError());
   return GPMDM_OK;
 }
@@ -1009,6 +1162,10 @@ int gpmdm_pf_unpack_part(gpmdm_pf_t pf, const double* recv, int part, void* stre
   CHECK(pf && recv, "null argument");
   CHECK(part >= GPMDM_PACK_ALL && part <= GPMDM_PACK_LL, "part must be GPMDM_PACK_*");
   HIPCHK(hipSetDevice(pf->m->device));
+  return unpack_part(pf, recv, part, (hipStream_t)stream);
+}
+
+static int unpack_part(gpmdm_pf* pf, const double* recv, int part, hipStream_t s) {
   PackArgs a{};
   a.n = pf->P;
   a.lo = 0;
@@ -1020,7 +1177,7 @@ int gpmdm_pf_unpack_part(gpmdm_pf_t pf, const double* recv, int part, void* stre
   a.ll = pf->ll;
   a.cls = pf->cls_new;
   a.X = pf->X_prop;
-  launch_unpack(a, (hipStream_t)stream);
+  launch_unpack(a, s);
   HIPCHK(hipGetLastError());
   return GPMDM_OK;
 }
@@ -1059,7 +1216,8 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
 int gpmdm_pf_step(gpmdm_pf_t pf, const double* zh, const double* E, const double* normals,
                   const double* uniforms, void* stream) {
   CHECK(pf, "null handle");
-  CHECK(pf->n_ranks == 1, "gpmdm_pf_step is single-rank; use switch/propagate/pack/unpack/resample");
+  CHECK(pf->n_ranks == 1 || pf->comm, "gpmdm_pf_step on several ranks needs a communicator (gpmdm_pf_set_comm) "
+        "or the staged calls switch/propagate/pack/unpack/resample");
   TRY(gpmdm_pf_switch(pf, E, nullptr, stream));
   TRY(gpmdm_pf_propagate(pf, zh, normals, stream));
   TRY(gpmdm_pf_resample(pf, uniforms, stream));

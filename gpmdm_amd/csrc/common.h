@@ -11,8 +11,6 @@ namespace gpmdm {
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 struct SegDesc {                  // one GP: the observation GP, or the class-c dynamics GP
-  const double* Xs;               // n_rows x d : training inputs / lengthscales
-  const double* Xsq;              // n_rows     : |Xs_i|^2 * 64/ln2 (pre-scaled for exp2)
   const double* Xrec;             // row_cap(n_rows) x (d + 1): row records [Xs_i, |Xs_i|^2 * 64/ln2]
   const double* Hf;               // dyn only: H = (Xin C^2)^T B, (d+1) x cols, fragment order
   const double* Bf;               // B = [triu(R) | M] in fragment order (see capi.hip)
@@ -43,15 +41,9 @@ struct TileParams {
   // holding mean columns write spart[J][out] = sum_j (z_j - mu_j)^2 lam2_j over their mean
   // columns (z = the observation of the particle's filter, pos / Pf).
   double* spart;                  // nullptr: store mu
-  const double* rec128;           // A/B (gp_tile.h VAR bit 22): row records scaled by 128/ln2
   const double* z;                // F x n_m
   const double* lam2;             // n_m: exp(y_log_lambdas)^2 = 1 / il2
   long long Pf;                   // particles per filter
-  // K* cache (observation GP, gp_tile.h VAR bits 28/29): the full-K block's workgroups
-  // store each K-step's A fragments here (tile-major, fragment order); the other blocks'
-  // workgroups, launched after them, load them instead of generating K* again.
-  double* kcache;
-  int j_skip;                     // blocks skipped from the top: J = n_j_max - 1 - j_skip - b / tiles_ub
 };
 
 void launch_gp_tile(const TileParams& p, int d, bool dyn, hipStream_t stream);

@@ -48,6 +48,19 @@ def shard_range(P: int, world: int, rank: int):
     return P * rank // world, P * (rank + 1) // world
 
 
+def gather_plan(P: int, world: int, pad_rows=None):
+    """(shard sizes, rows per rank in the collective, padded?) for an all-gather of P rows
+    over ``world`` ranks.  Shards differ by at most one row; the collective carries the
+    largest shard's rows per rank, or ``pad_rows`` (>= the largest shard; a larger value
+    forces the padded path even for even shards -- tests)."""
+    sizes = [shard_range(P, world, r)[1] - shard_range(P, world, r)[0] for r in range(world)]
+    mx = max(sizes)
+    rows = mx if pad_rows is None else int(pad_rows)
+    if rows < mx:
+        raise ValueError(f"pad_rows {rows} is smaller than the largest shard {mx}")
+    return sizes, rows, rows != mx or any(s != mx for s in sizes)
+
+
 def allgather_rows(recv: torch.Tensor, send: torch.Tensor, group=None) -> None:
     """recv (P x W) <- concatenation over ranks of each rank's send (P_r x W).
 
@@ -56,41 +69,40 @@ def allgather_rows(recv: torch.Tensor, send: torch.Tensor, group=None) -> None:
     import torch.distributed as dist
     world = dist.get_world_size(group)
     P, W = recv.shape
-    sizes = [shard_range(P, world, r)[1] - shard_range(P, world, r)[0] for r in range(world)]
-    mx = max(sizes)
-    if all(s == mx for s in sizes) and dist.get_backend(group) != "gloo":
+    sizes, mx, uneven = gather_plan(P, world)
+    if not uneven and dist.get_backend(group) != "gloo":
         dist.all_gather_into_tensor(recv, send, group=group)
         return
-    padded = torch.zeros((mx, W), dtype=send.dtype, device=send.device)
-    padded[: send.shape[0]] = send
-    parts = [torch.empty_like(padded) for _ in range(world)]
-    dist.all_gather(parts, padded, group=group)
+    pbuf = torch.zeros((mx, W), dtype=send.dtype, device=send.device)
+    pbuf[: send.shape[0]] = send
+    parts = [torch.empty_like(pbuf) for _ in range(world)]
+    dist.all_gather(parts, pbuf, group=group)
     off = 0
     for r, s in enumerate(sizes):
         recv[off: off + s] = parts[r][:s]
         off += s
 
 
-def allgather_rows_start(recv: torch.Tensor, send: torch.Tensor, group=None):
+def allgather_rows_start(recv: torch.Tensor, send: torch.Tensor, group=None, pad_rows=None):
     """Start allgather_rows(recv, send); returns ``wait()``, after which recv is valid on the
     current stream.  nccl: asynchronous (the collective overlaps the kernels the caller
     launches before wait(); wait() orders the current stream after it, without blocking the
-    host).  gloo: done before returning (wait() is a no-op)."""
+    host).  gloo: done before returning (wait() is a no-op).  ``pad_rows``: see
+    gather_plan (a world-1 test forces the padded gather and copy-back with it)."""
     import torch.distributed as dist
     if dist.get_backend(group) == "gloo":
         allgather_rows(recv, send, group)
         return lambda: None
     world = dist.get_world_size(group)
     P, W = recv.shape
-    sizes = [shard_range(P, world, r)[1] - shard_range(P, world, r)[0] for r in range(world)]
-    mx = max(sizes)
-    if all(s == mx for s in sizes):
+    sizes, mx, uneven = gather_plan(P, world, pad_rows)
+    if not uneven:
         work = dist.all_gather_into_tensor(recv, send, group=group, async_op=True)
         return work.wait
-    padded = torch.zeros((mx, W), dtype=send.dtype, device=send.device)
-    padded[: send.shape[0]] = send
-    parts = [torch.empty_like(padded) for _ in range(world)]
-    work = dist.all_gather(parts, padded, group=group, async_op=True)
+    pbuf = torch.zeros((mx, W), dtype=send.dtype, device=send.device)
+    pbuf[: send.shape[0]] = send
+    parts = [torch.empty_like(pbuf) for _ in range(world)]
+    work = dist.all_gather(parts, pbuf, group=group, async_op=True)
 
     def wait():
         work.wait()
@@ -99,3 +111,41 @@ def allgather_rows_start(recv: torch.Tensor, send: torch.Tensor, group=None):
             recv[off: off + s] = parts[r][:s]
             off += s
     return wait
+
+
+class RcclComm:
+    """An RCCL communicator made by the library (gpmdm_comm_unique_id / gpmdm_comm_init),
+    for ``GPMDM_PF.set_comm``.  ``RcclComm.single(device)`` is a one-rank communicator;
+    for several ranks, rank 0's ``unique_id()`` bytes reach every rank out of band
+    (e.g. a torch.distributed broadcast) and each calls ``RcclComm(world, rank, uid,
+    device)`` (collective).  ``destroy()`` after the filters using it."""
+
+    def __init__(self, world: int, rank: int, uid: bytes, device: int):
+        import ctypes
+        from . import _lib
+        if len(uid) != _lib.GPMDM_COMM_ID_BYTES:
+            raise ValueError("unique id must be GPMDM_COMM_ID_BYTES bytes")
+        buf = ctypes.create_string_buffer(bytes(uid), len(uid))
+        h = ctypes.c_void_p()
+        _lib.check(_lib.load().gpmdm_comm_init(int(world), int(rank), buf, int(device), ctypes.byref(h)),
+                   "gpmdm_comm_init")
+        self.ptr = h.value
+        self.world, self.rank, self.device = int(world), int(rank), int(device)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes
+        from . import _lib
+        buf = ctypes.create_string_buffer(_lib.GPMDM_COMM_ID_BYTES)
+        _lib.check(_lib.load().gpmdm_comm_unique_id(buf), "gpmdm_comm_unique_id")
+        return buf.raw
+
+    @classmethod
+    def single(cls, device: int = 0) -> "RcclComm":
+        return cls(1, 0, cls.unique_id(), device)
+
+    def destroy(self) -> None:
+        from . import _lib
+        if self.ptr:
+            _lib.check(_lib.load().gpmdm_comm_destroy(self.ptr), "gpmdm_comm_destroy")
+            self.ptr = None

@@ -25,6 +25,10 @@ every per-frame computation runs in the HIP library.  Extra keyword options:
 * ``shard_order`` (default True; multi-rank philox filters): each rank evaluates a slice of
   the particles ordered by resampling ancestor rather than a slice of particle indices, so
   de-duplication keeps ~1/R of the distinct keys per rank; bitwise identical either way.
+* ``set_comm(comm)``: hand the library an RCCL communicator (``gpmdm_amd.RcclComm`` or
+  any ncclComm_t of ``shard=(world, rank)``'s ranks); ``update`` then exchanges the rows
+  itself (``gpmdm_pf_set_comm``: both all-gathers on a library-owned stream, the first
+  overlapping the observation GP), the native hosts' path -- no torch.distributed.
 * ``dyn_tiles`` (``'auto'``): tile shape of the dynamics-GP pass (``gpmdm_pf_set_dyn_tiles``):
   narrow tiles for de-duplicated rows, wide ones when every particle is evaluated; the
   shapes differ only in floating-point summation order.
@@ -110,6 +114,7 @@ class GPMDM_PF:
             raise ValueError("dyn_tiles must be 'auto', 'narrow' or 'wide'")
         _lib.check(lib.gpmdm_pf_set_dyn_tiles(h, _lib.DYN_TILES[dyn_tiles]), "dyn_tiles")
         self._readout = None
+        self._comm = None
         if self._world > 1:
             w, lo, hi = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
             lib.gpmdm_pf_exchange_width(h, ctypes.byref(w), ctypes.byref(lo), ctypes.byref(hi))
@@ -211,13 +216,25 @@ class GPMDM_PF:
         _lib.check(lib.gpmdm_pf_resample(h, _lib.dptr(U), s), "resample")
         self._readout = None
 
+    def set_comm(self, comm, pad_rows: bool = False):
+        """Let the library run the per-frame exchange over an RCCL communicator
+        (``gpmdm_pf_set_comm``; ``comm``: an ``RcclComm`` or a raw ncclComm_t address of
+        this filter's (world, rank), on the model's device; ``None`` detaches).
+        ``pad_rows`` forces the uneven-shard gather path (tests).  The communicator must
+        outlive the filter's use of it."""
+        ptr = getattr(comm, "ptr", comm)
+        _lib.check(_lib.load().gpmdm_pf_set_comm(self._h, ctypes.c_void_p(ptr) if ptr else None,
+                                                 _lib.GPMDM_COMM_PAD_ROWS if pad_rows else 0), "set_comm")
+        self._comm = comm
+
     def _propagate(self, z, normals, s):
         """gpmdm_pf.py:153-192 for this rank's particles, and on several ranks the exchange:
         the new {class, state} rows are all-gathered while the observation GP runs (they are
-        final once the dynamics GP is done), the likelihoods after it."""
+        final once the dynamics GP is done), the likelihoods after it -- by the library over
+        its communicator (set_comm), or here over the process group / exchange callback."""
         lib, h = _lib.load(), self._h
         nrm = None if normals is None else _lib.dptr(normals)
-        if self._world == 1:
+        if self._world == 1 or self._comm is not None:
             _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), nrm, s), "propagate")
             return
         _lib.check(lib.gpmdm_pf_propagate_dynamics(h, nrm, s), "propagate_dynamics")

@@ -107,8 +107,10 @@ int gpmdm_predict_dyn(gpmdm_model_t model, int c, const double* Xs_dev, int64_t 
 
 /* GPMDM_PF(gpmdm, markov_switching_model, num_particles)  (gpmdm_pf.py:47-85).
  * T: C x C host.  Ranks own the contiguous particle range
- * [rank*P/n_ranks, (rank+1)*P/n_ranks); particle state is replicated on every rank
- * (the exchange is done by the caller: gpmdm_pf_pack / gpmdm_pf_unpack). */
+ * [rank*P/n_ranks, (rank+1)*P/n_ranks); particle state is replicated on every rank.
+ * The per-frame exchange is done either by the library over an RCCL communicator
+ * (gpmdm_pf_set_comm; then gpmdm_pf_propagate / gpmdm_pf_step exchange by themselves) or
+ * by the caller with the staged calls (gpmdm_pf_pack / gpmdm_pf_unpack). */
 int gpmdm_pf_create(gpmdm_model_t model, const double* T, int64_t P, int rng_mode,
                     uint64_t seed, int resample_mode, int n_ranks, int rank,
                     gpmdm_pf_t* out);
@@ -159,13 +161,38 @@ int gpmdm_pf_unpack(gpmdm_pf_t pf, const double* recv_dev, void* stream);
 int gpmdm_pf_pack_part(gpmdm_pf_t pf, double* send_dev, int part, void* stream);
 int gpmdm_pf_unpack_part(gpmdm_pf_t pf, const double* recv_dev, int part, void* stream);
 
+/* Library-driven exchange over RCCL (SURVEY.md §8(b)'s rccl_comm; it replaces the
+ * reference's single-process hand-over from _update_weights to _resample,
+ * gpmdm_pf.py:194-213).  rccl_comm: an ncclComm_t of n_ranks ranks in which this process is
+ * `rank`, on the model's device (from gpmdm_comm_init or the caller's own
+ * ncclCommInitRank); the caller keeps ownership and destroys it after the filter.  While
+ * set, gpmdm_pf_propagate (and gpmdm_pf_step) all-gather every rank's new {class, state}
+ * rows on a library-owned stream while the observation GP runs on the caller's stream, then
+ * the {ll} column; the caller's stream waits for both gathers (events, no host wait) and
+ * every rank holds the full replicated filter before gpmdm_pf_resample.  NULL detaches.
+ * Also valid with n_ranks = 1 (the exchange then moves this rank's rows only).
+ * flags: 0, or GPMDM_COMM_PAD_ROWS -- gather one padding row per rank more than needed,
+ * through the uneven-shard path (staging buffer + copy-down; diagnostics and tests).
+ * Not between switch and resample; not for filter banks (they shard filters). */
+#define GPMDM_COMM_PAD_ROWS 1
+#define GPMDM_COMM_ID_BYTES 128   /* sizeof(ncclUniqueId) */
+int gpmdm_pf_set_comm(gpmdm_pf_t pf, void* rccl_comm, int flags);
+
+/* RCCL communicator helpers for native hosts that do not link RCCL themselves: rank 0
+ * creates a unique id (GPMDM_COMM_ID_BYTES bytes) and hands it to every rank out of band;
+ * each rank calls gpmdm_comm_init on its device (ncclCommInitRank: collective over the
+ * ranks); gpmdm_comm_destroy after the filters using it are destroyed. */
+int gpmdm_comm_unique_id(void* id);
+int gpmdm_comm_init(int n_ranks, int rank, const void* id, int device, void** comm);
+int gpmdm_comm_destroy(void* comm);
+
 /* _update_weights' normalisation + _resample + the read-outs  (gpmdm_pf.py:194-262,
  * 302-312).  uniforms: P host (replay, multinomial), 1 host (replay, systematic) or NULL. */
 int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream);
 
 /* update(z) in one call  (gpmdm_pf.py:117-135): switch + propagate + resample.
- * Single-rank only; replay draws must all be given (use the staged calls when the
- * per-class normal counts are not known in advance). */
+ * One rank, or several with a communicator (gpmdm_pf_set_comm); replay draws must all be
+ * given (use the staged calls when the per-class normal counts are not known in advance). */
 int gpmdm_pf_step(gpmdm_pf_t pf, const double* z, const double* exp_draws,
                   const double* normals, const double* uniforms, void* stream);
 

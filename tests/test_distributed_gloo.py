@@ -108,3 +108,16 @@ def test_broadcast_and_consistency_check_two_ranks():
     for rank, b, seed, same, differ in res:
         assert np.array_equal(b, np.arange(12, dtype=np.float64).reshape(3, 4)), rank
         assert seed == 1000 and same and not differ
+
+
+def test_gather_plan():
+    """The branch choice of the all-gather (even shards -> one all_gather_into_tensor;
+    uneven, or padding forced -> padded gather + copy-back) as a pure function."""
+    from gpmdm_amd.distributed import gather_plan
+    assert gather_plan(8, 2) == ([4, 4], 4, False)
+    assert gather_plan(7, 2) == ([3, 4], 4, True)
+    assert gather_plan(7, 1) == ([7], 7, False)
+    assert gather_plan(7, 1, pad_rows=9) == ([7], 9, True)
+    assert gather_plan(10, 3)[0] == [3, 3, 4]
+    with pytest.raises(ValueError):
+        gather_plan(7, 2, pad_rows=3)

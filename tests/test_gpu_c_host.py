@@ -41,8 +41,10 @@ def _write_input(path, m, T, st, Z, P, seed, resample):
         fh.write(f64(Z))
 
 
-@pytest.mark.parametrize("resample", [0, 1])
-def test_native_c_host_matches_python(fx_config2, tmp_path, resample):
+@pytest.mark.parametrize("resample,ranks", [(0, 0), (1, 0), (0, 1)])
+def test_native_c_host_matches_python(fx_config2, tmp_path, resample, ranks):
+    """ranks=1: the host's --ranks mode (RCCL communicator through gpmdm_comm_init, the
+    library's own exchange, gpmdm_pf_set_comm) on this box's one GPU."""
     from gpmdm_amd import GPMDM_PF, build
     exe = build.build_c_host()
     m = product_model(fx_config2)
@@ -57,7 +59,8 @@ def test_native_c_host_matches_python(fx_config2, tmp_path, resample):
     Y = m.get_Y()
     Z = np.stack([np.asarray(Y[40 + 3 * k], dtype=np.float64) for k in range(F)])
     _write_input(tmp_path / "in.bin", m, T, st, Z, P, seed, resample)
-    r = subprocess.run([str(exe), str(tmp_path / "in.bin"), str(tmp_path / "out.bin")],
+    extra = ["--ranks", str(ranks), "--rank", "0", "--id", str(tmp_path / "rccl.id")] if ranks else []
+    r = subprocess.run([str(exe), str(tmp_path / "in.bin"), str(tmp_path / "out.bin"), *extra],
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr
     C, d = m.n_classes, m.d

@@ -128,7 +128,9 @@ def test_process_group_replay_refuses_different_torch_states():
 def _nccl_worker(port, out_q):
     """World-size-1 RCCL group: the asynchronous all-gather GPMDM_PF overlaps with the
     observation GP (distributed.allgather_rows_start, nccl branch), with kernels queued on
-    the current stream between start and wait, and the uneven-shard (padded) branch."""
+    the current stream between start and wait.  Both branches run: the even
+    all_gather_into_tensor and -- forced with pad_rows, since one rank's shard is never
+    uneven -- the padded gather with its copy-back in wait()."""
     import torch.distributed as dist
     from gpmdm_amd.distributed import allgather_rows_start
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -138,10 +140,10 @@ def _nccl_worker(port, out_q):
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     try:
         ok = True
-        for P, W in ((100_000, 4), (7, 1)):
+        for P, W, pad in ((100_000, 4, None), (7, 1, None), (100_000, 4, 100_001), (7, 1, 9)):
             send = torch.arange(P * W, dtype=torch.float64, device=dev).reshape(P, W)
             recv = torch.full((P, W), -1.0, dtype=torch.float64, device=dev)
-            wait = allgather_rows_start(recv, send)
+            wait = allgather_rows_start(recv, send, pad_rows=pad)
             busy = torch.randn(2048, 2048, dtype=torch.float64, device=dev)
             for _ in range(4):                     # work on the current stream meanwhile
                 busy = busy @ busy * 1e-3

@@ -81,8 +81,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(B, hB.data(), total * 8, hipMemcpyHostToDevice));
     TileParams& p = pp[v];
     p = TileParams{};
-    p.seg[0].Xs = Xs; p.seg[0].Xsq = Xsq; p.seg[0].Xrec = Xrec; p.seg[0].Bf = B;
-    p.rec128 = Xrec128;
+    p.seg[0].Xrec = Xrec; p.seg[0].Bf = B;
     p.seg[0].n_rows = N; p.seg[0].n_m = D; p.seg[0].n_j = n_j; p.seg[0].coff = coff;
     p.n_seg = 1; p.tiles_ub = ntiles; p.n_j_max = n_j; p.geo = TileGeo{nw, geos[v].mt, geos[v].ntw};
     int* tab = tabs + 8 * v;
@@ -133,6 +132,22 @@ int main(int argc, char** argv) {
       for (size_t i = 0; i < nq; ++i) { md = std::max(md, std::abs(q1[i] - q0[i])); mx = std::max(mx, std::abs(q0[i])); }
       printf("check %-30s max |q - q_production| = %.3g (max |q| %.3g)\n", vars[v].name, md, mx);
     }
+  }
+  // cross-revision bitwise check (tile_ab.sh): a hash of the production variant's q partials and means
+  if (getenv("TB_QHASH") && *getenv("TB_QHASH")) {
+    const size_t nq = (size_t)P * (pp[vars[0].pi].n_j_max), nm = (size_t)P * D;
+    std::vector<double> q0(nq), m0(nm);
+    CK(hipMemset(q, 0, nq * 8));
+    CK(hipMemset(mu, 0, nm * 8));
+    vars[0].fn(pp[vars[0].pi], s);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(q0.data(), q, nq * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(m0.data(), mu, nm * 8, hipMemcpyDeviceToHost));
+    unsigned long long h = 1469598103934665603ull;   // FNV-1a over the bytes
+    for (auto* v : {&q0, &m0})
+      for (const unsigned char* c = (const unsigned char*)v->data(), *e = c + v->size() * 8; c < e; ++c)
+        h = (h ^ *c) * 1099511628211ull;
+    printf("qhash %016llx\n", h);
   }
   double rows = 0;   // per 16-column tile: rows up to its diagonal (or all, for mean tiles)
   for (int tc = 0; tc * 16 < N + D; ++tc) {

@@ -1,5 +1,5 @@
 // A/B timing of k_gp_tile variants on the config-2 observation GP shape (N=2000, D=62,
-// d=3, P=100k): template VAR bits (see gp_tile.hip) and NW (waves per workgroup).
+// d=3, P=100k): template VAR bits (see gp_tile_lab.h) and NW (waves per workgroup).
 // Variants run interleaved in one process (cdna_hip_programming.md §5.4 rule 24).
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/microbench/tile_bench.hip -o tools/microbench/tile_bench
 #include <algorithm>
@@ -10,7 +10,7 @@
 #include <string>
 #include <vector>
 
-#include "../../gpmdm_amd/csrc/gp_tile.h"
+#include "gp_tile_lab.h"
 
 using namespace gpmdm;
 
@@ -20,65 +20,65 @@ using namespace gpmdm;
 #define TB_D 3
 #endif
 template <int VAR, int NW, int MT = 4, int NTW = 4>
-void launch_var(const TileParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((k_gp_tile<TB_D, false, VAR, NW, MT, NTW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, p);
+void launch_var(const LabParams& p, hipStream_t s) {
+  hipLaunchKernelGGL((k_gp_tile_lab<TB_D, false, VAR, NW, MT, NTW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, p);
 }
 
-// K* cache pair (gp_tile.h VAR bits 28/29): the full-K block generates and stores K*, the
+// K* cache pair (gp_tile_lab.h VAR bits 28/29): the full-K block generates and stores K*, the
 // other blocks load it.  Chunked: particle tiles in CH chunks; producer of chunk k on the
 // main stream, consumer of chunk k on a second stream after an event, so the producers'
 // grid tail overlaps the consumers' work.
 static hipStream_t g_s2 = nullptr;
 static hipEvent_t g_ev[17];
-static std::vector<TileParams> g_chunk[9];    // per chunk count: one TileParams per chunk
+static std::vector<LabParams> g_chunk[9];    // per chunk count: one LabParams per chunk
 template <int NW, int MT, int NTW, int CH>
-void launch_kc(const TileParams& p, hipStream_t s) {
-  TileParams a = p, c = p;
+void launch_kc(const LabParams& p, hipStream_t s) {
+  LabParams a = p, c = p;
   a.j_skip = 0;
   c.j_skip = 1;
   if (CH == 1) {
-    hipLaunchKernelGGL((k_gp_tile<TB_D, false, 268435456, NW, MT, NTW>), dim3(p.tiles_ub), dim3(64 * NW), 0, s, a);
-    hipLaunchKernelGGL((k_gp_tile<TB_D, false, 536870912, NW, MT, NTW>), dim3((p.n_j_max - 1) * p.tiles_ub), dim3(64 * NW), 0, s, c);
+    hipLaunchKernelGGL((k_gp_tile_lab<TB_D, false, 268435456, NW, MT, NTW>), dim3(p.tiles_ub), dim3(64 * NW), 0, s, a);
+    hipLaunchKernelGGL((k_gp_tile_lab<TB_D, false, 536870912, NW, MT, NTW>), dim3((p.n_j_max - 1) * p.tiles_ub), dim3(64 * NW), 0, s, c);
     return;
   }
   for (int k = 0; k < CH; ++k) {
-    TileParams pa = g_chunk[CH][k], pc = g_chunk[CH][k];
+    LabParams pa = g_chunk[CH][k], pc = g_chunk[CH][k];
     pa.j_skip = 0;
     pc.j_skip = 1;
-    hipLaunchKernelGGL((k_gp_tile<TB_D, false, 268435456, NW, MT, NTW>), dim3(pa.tiles_ub), dim3(64 * NW), 0, s, pa);
+    hipLaunchKernelGGL((k_gp_tile_lab<TB_D, false, 268435456, NW, MT, NTW>), dim3(pa.tiles_ub), dim3(64 * NW), 0, s, pa);
     hipEventRecord(g_ev[k], s);
     hipStreamWaitEvent(g_s2, g_ev[k], 0);
-    hipLaunchKernelGGL((k_gp_tile<TB_D, false, 536870912, NW, MT, NTW>), dim3((pc.n_j_max - 1) * pc.tiles_ub), dim3(64 * NW), 0, g_s2, pc);
+    hipLaunchKernelGGL((k_gp_tile_lab<TB_D, false, 536870912, NW, MT, NTW>), dim3((pc.n_j_max - 1) * pc.tiles_ub), dim3(64 * NW), 0, g_s2, pc);
   }
   hipEventRecord(g_ev[16], g_s2);
   hipStreamWaitEvent(s, g_ev[16], 0);
 }
 
 template <int NW, int MT, int NTW, int XV = 0>
-void launch_kc_allcons(const TileParams& p, hipStream_t s) {   // producer, then consumers on every block
-  TileParams a = p, c = p;
+void launch_kc_allcons(const LabParams& p, hipStream_t s) {   // producer, then consumers on every block
+  LabParams a = p, c = p;
   a.j_skip = 0;
   c.j_skip = 0;
-  hipLaunchKernelGGL((k_gp_tile<TB_D, false, 268435456 | XV, NW, MT, NTW>), dim3(p.tiles_ub), dim3(64 * NW), 0, s, a);
-  hipLaunchKernelGGL((k_gp_tile<TB_D, false, 536870912 | XV, NW, MT, NTW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, c);
+  hipLaunchKernelGGL((k_gp_tile_lab<TB_D, false, 268435456 | XV, NW, MT, NTW>), dim3(p.tiles_ub), dim3(64 * NW), 0, s, a);
+  hipLaunchKernelGGL((k_gp_tile_lab<TB_D, false, 536870912 | XV, NW, MT, NTW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, c);
 }
 template <int NW, int MT, int NTW>
-void launch_kc_allprod(const TileParams& p, hipStream_t s) {   // every block a producer (same values stored)
-  TileParams a = p;
+void launch_kc_allprod(const LabParams& p, hipStream_t s) {   // every block a producer (same values stored)
+  LabParams a = p;
   a.j_skip = 0;
-  hipLaunchKernelGGL((k_gp_tile<TB_D, false, 268435456, NW, MT, NTW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, a);
+  hipLaunchKernelGGL((k_gp_tile_lab<TB_D, false, 268435456, NW, MT, NTW>), dim3(p.n_j_max * p.tiles_ub), dim3(64 * NW), 0, s, a);
 }
 template <int NW, int MT, int NTW>
-void launch_kc_prod(const TileParams& p, hipStream_t s) {
-  TileParams a = p;
+void launch_kc_prod(const LabParams& p, hipStream_t s) {
+  LabParams a = p;
   a.j_skip = 0;
-  hipLaunchKernelGGL((k_gp_tile<TB_D, false, 268435456, NW, MT, NTW>), dim3(p.tiles_ub), dim3(64 * NW), 0, s, a);
+  hipLaunchKernelGGL((k_gp_tile_lab<TB_D, false, 268435456, NW, MT, NTW>), dim3(p.tiles_ub), dim3(64 * NW), 0, s, a);
 }
 template <int NW, int MT, int NTW>
-void launch_kc_cons(const TileParams& p, hipStream_t s) {
-  TileParams c = p;
+void launch_kc_cons(const LabParams& p, hipStream_t s) {
+  LabParams c = p;
   c.j_skip = 1;
-  hipLaunchKernelGGL((k_gp_tile<TB_D, false, 536870912, NW, MT, NTW>), dim3((p.n_j_max - 1) * p.tiles_ub), dim3(64 * NW), 0, s, c);
+  hipLaunchKernelGGL((k_gp_tile_lab<TB_D, false, 536870912, NW, MT, NTW>), dim3((p.n_j_max - 1) * p.tiles_ub), dim3(64 * NW), 0, s, c);
 }
 
 int main(int argc, char** argv) {
@@ -115,7 +115,7 @@ int main(int argc, char** argv) {
   struct Geo { int nw, mt, ntw; };
   const Geo geos[] = {{4, 4, 4}, {8, 4, 4}, {4, 2, 8}, {4, 1, 16}, {4, 1, 8}, {4, 2, 6}, {8, 2, 8}, {4, 1, 4}, {4, 2, 4}};
   const int NGEO = sizeof(geos) / sizeof(geos[0]);
-  TileParams pp[NGEO];
+  LabParams pp[NGEO];
   int* tabs;
   CK(hipMalloc(&tabs, NGEO * 8 * sizeof(int)));
   for (int v = 0; v < NGEO; ++v) {
@@ -132,8 +132,8 @@ int main(int argc, char** argv) {
     double* B;
     CK(hipMalloc(&B, total * 8));
     CK(hipMemcpy(B, hB.data(), total * 8, hipMemcpyHostToDevice));
-    TileParams& p = pp[v];
-    p = TileParams{};
+    LabParams& p = pp[v];
+    p = LabParams{};
     p.seg[0].Xs = Xs; p.seg[0].Xsq = Xsq; p.seg[0].Xrec = Xrec; p.seg[0].Bf = B;
     p.rec128 = Xrec128;
     p.seg[0].n_rows = N; p.seg[0].n_m = D; p.seg[0].n_j = n_j; p.seg[0].coff = coff;
@@ -152,7 +152,7 @@ int main(int argc, char** argv) {
           const int t0 = (int)((long long)ntiles * k / CH), t1 = (int)((long long)ntiles * (k + 1) / CH);
           int h[5] = {t0 * pt, std::min(P, t1 * pt), t0 * pt, 0, t1 - t0};
           CK(hipMemcpy(ct + 8 * k, h, sizeof(h), hipMemcpyHostToDevice));
-          TileParams c = p;
+          LabParams c = p;
           c.tiles_ub = t1 - t0;
           c.seg_pos_begin = ct + 8 * k; c.seg_pos_end = ct + 8 * k + 1; c.seg_out_base = ct + 8 * k + 2;
           c.seg_tile_start = ct + 8 * k + 3;
@@ -168,7 +168,7 @@ int main(int argc, char** argv) {
   for (int i = 0; i < 17; ++i) CK(hipEventCreateWithFlags(&g_ev[i], hipEventDisableTiming));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  typedef void (*L)(const TileParams&, hipStream_t);
+  typedef void (*L)(const LabParams&, hipStream_t);
   struct V { L fn; int pi; const char* name; };
 #if defined(TB_SHAPES)
   // tile shapes on a small-row problem (the de-duplicated dynamics GP: a few thousand rows

@@ -19,4 +19,7 @@ for lam in 1.0 0.3 0.1; do
     || { echo "bench predictive $lam failed rc=$?"; tail -20 $out/pred_$lam.err; exit 1; }
   python -c "import json;d=json.load(open('$out/pred_$lam.json'));print('lambda $lam', round(d['ms_per_step'],3), 'ms', 'ess_frac', d['ess_frac_last'], 'rows', d['dyn_rows_last'], d['stream_check'], d['stages_ms_per_step'])"
 done
+timeout -k 10 900 bash tools/microbench/tile_ab.sh run > $out/tile_ab.txt 2>&1 \
+  || { echo "tile_ab failed rc=$?"; tail -20 $out/tile_ab.txt; exit 1; }
+cat $out/tile_ab.txt
 echo done
