@@ -229,12 +229,16 @@ struct gpmdm_pf {
   struct Rec { int stage; hipEvent_t a, b; };
   std::vector<Rec> recs;
 
-  int* class_start() const { return small; }
-  int* counts() const { return small + 40; }
-  int* seg_begin() const { return small + 80; }
-  int* seg_end() const { return small + 120; }
-  int* seg_out() const { return small + 160; }
-  int* seg_tiles() const { return small + 200; }
+  // class tables of the step's grouping (small[0, 240)); predict() groups into its own
+  // copy (small[256, 496), base 256) so the step's tables -- which gpmdm_pf_dyn_rows
+  // reads -- survive a predict between steps
+  int* class_start(int base = 0) const { return small + base; }
+  int* counts(int base = 0) const { return small + base + 40; }
+  int* seg_begin(int base = 0) const { return small + base + 80; }
+  int* seg_end(int base = 0) const { return small + base + 120; }
+  int* seg_out(int base = 0) const { return small + base + 160; }
+  int* seg_tiles(int base = 0) const { return small + base + 200; }
+  static constexpr int kPredictTables = 256;
   // leader segment tables (same shape as the full ones)
   int* lseg_begin() const { return ltab; }
   int* lseg_end() const { return ltab + 40; }
@@ -390,6 +394,16 @@ static void fill_tile_common(TileParams& tp, const gpmdm_model* m, bool dyn) {
   for (int j = 0; j < d; ++j) tp.ls[j] = dyn ? m->x_ls[j] : m->y_ls[j];
 }
 
+// The predictive maps' per-call scratch is released in stream order on every exit after
+// its allocation, a failed launch included (the launch error is what the call reports).
+static int finish_scratch(double* q, hipStream_t s) {
+  const hipError_t launch = hipGetLastError();
+  const hipError_t freed = hipFreeAsync(q, s);
+  if (launch != hipSuccess) return fail(GPMDM_E_HIP, std::string("predictive-map launch: ") + hipGetErrorString(launch));
+  if (freed != hipSuccess) return fail(GPMDM_E_HIP, std::string("hipFreeAsync: ") + hipGetErrorString(freed));
+  return GPMDM_OK;
+}
+
 int gpmdm_predict_obs(gpmdm_model_t m, const double* Xs, int64_t n, double* mu, double* var, void* stream) {
   CHECK(m, "null model");
   CHECK(n >= 0 && n < (1ll << 31), "bad n");
@@ -433,9 +447,7 @@ int gpmdm_predict_obs(gpmdm_model_t m, const double* Xs, int64_t n, double* mu, 
   fa.il2 = m->y_il2_dev;
   fa.var_out = var;
   launch_obs_finish(fa, s);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipFreeAsync(q, s));
-  return GPMDM_OK;
+  return finish_scratch(q, s);
 }
 
 int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, double* mu, double* var, void* stream) {
@@ -483,9 +495,7 @@ int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, doubl
   for (int j = 0; j < m->d; ++j) fa.il2[j] = m->x_il2[j];
   fa.var_out = var;
   launch_dyn_finish(fa, s);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipFreeAsync(q, s));
-  return GPMDM_OK;
+  return finish_scratch(q, s);
 }
 
 // ------------------------------------------------------------------------------------
@@ -535,7 +545,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   ALLOC(ridx, P);
   ALLOC(blockcounts, (long long)pf->nb * C);
   ALLOC(blockoff, (long long)pf->nb * C);
-  ALLOC(small, 256);
+  ALLOC(small, 512);
   ALLOC(obs_tab, 8);
   ALLOC(owner, (long long)C * P);
   ALLOC(slot, (long long)C * P);
@@ -833,6 +843,15 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
     // ---- dynamics GP per class (segments of at most kMaxSeg classes per launch) ----
     // narrow tiles for the de-duplicated rows, the wide image when every particle is evaluated
     const std::vector<GpImage>& dset = m->dyn_set(pf->wide_dyn());
+    // Diagnostic (GPMDM_DYN_EXACT_GRID=1): read the leader tile counts back (a host sync)
+    // and launch exactly the non-empty tiles instead of the device-unknown upper bound --
+    // measures what the empty workgroups of the bound cost.  Not the production schedule.
+    static const bool exact_grid = std::getenv("GPMDM_DYN_EXACT_GRID") != nullptr;
+    int ltiles[kMaxClasses + 1] = {0};
+    if (exact_grid && pf->dedup) {
+      HIPCHK(hipMemcpyAsync(ltiles, pf->lseg_tiles(), sizeof(int) * (C + 1), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+    }
     hipEvent_t t0;
     pf->mark_begin(s, GPMDM_STAGE_DYN_GEMM, t0);
     for (int c0 = 0; c0 < C; c0 += kMaxSeg) {
@@ -846,6 +865,7 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
       tp.n_seg = ns;
       tp.geo = dset[c0].geo;           // tile starts computed on the device in units of pt
       tp.tiles_ub = (int)(cdiv(nl, tp.geo.pt()) + ns);
+      if (exact_grid && pf->dedup) tp.tiles_ub = std::max(ltiles[c0 + ns] - ltiles[c0], 1);
       tp.n_j_max = njm;
       if (pf->dedup) {                  // one row per (ancestor, class) leader
         tp.seg_pos_begin = pf->lseg_begin() + c0;
@@ -1431,8 +1451,9 @@ int gpmdm_pf_predict(gpmdm_pf_t pf, double* mean, void* stream) {
     TRY(dalloc(&pf->pred_mu_p, (size_t)P * d));
     TRY(dalloc(&pf->pred_out, (size_t)pf->F * d));
   }
-  // group the current particles by their current class (the grouping tables are the
-  // switch's; the next switch rebuilds them)
+  // group the current particles by their current class (perm / block tables are the
+  // switch's scratch, rebuilt by the next switch; the class tables are predict's own)
+  const int tb = gpmdm_pf::kPredictTables;
   const int nbs = (int)cdiv(P, 256);
   launch_class_hist(pf->cls, P, C, pf->blockcounts, s);
   ScanArgs sc{};
@@ -1444,19 +1465,19 @@ int gpmdm_pf_predict(gpmdm_pf_t pf, double* mean, void* stream) {
   sc.blockcounts = pf->blockcounts;
   sc.cls_new = pf->cls;
   sc.blockoff = pf->blockoff;
-  sc.class_start = pf->class_start();
-  sc.counts = pf->counts();
-  sc.seg_pos_begin = pf->seg_begin();
-  sc.seg_pos_end = pf->seg_end();
-  sc.seg_out_base = pf->seg_out();
-  sc.seg_tile_start = pf->seg_tiles();
+  sc.class_start = pf->class_start(tb);
+  sc.counts = pf->counts(tb);
+  sc.seg_pos_begin = pf->seg_begin(tb);
+  sc.seg_pos_end = pf->seg_end(tb);
+  sc.seg_out_base = pf->seg_out(tb);
+  sc.seg_tile_start = pf->seg_tiles(tb);
   launch_scan_counts(sc, s);
   GroupArgs ga{};
   ga.P = P;
   ga.n = P;
   ga.C = C;
   ga.cls_new = pf->cls;
-  ga.class_start = pf->class_start();
+  ga.class_start = pf->class_start(tb);
   ga.blockoff = pf->blockoff;
   ga.perm = pf->perm;
   launch_group(ga, s);
@@ -1473,10 +1494,10 @@ int gpmdm_pf_predict(gpmdm_pf_t pf, double* mean, void* stream) {
     tp.geo = m->dyn_set(true)[c0].geo;
     tp.tiles_ub = (int)(cdiv(P, tp.geo.pt()) + ns);
     tp.n_j_max = njm;
-    tp.seg_pos_begin = pf->seg_begin() + c0;
-    tp.seg_pos_end = pf->seg_end() + c0;
-    tp.seg_out_base = pf->seg_out() + c0;
-    tp.seg_tile_start = pf->seg_tiles() + c0;
+    tp.seg_pos_begin = pf->seg_begin(tb) + c0;
+    tp.seg_pos_end = pf->seg_end(tb) + c0;
+    tp.seg_out_base = pf->seg_out(tb) + c0;
+    tp.seg_tile_start = pf->seg_tiles(tb) + c0;
     tp.perm = pf->perm;
     tp.X = pf->X;
     fill_tile_common(tp, m, true);

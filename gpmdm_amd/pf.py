@@ -17,7 +17,10 @@ every per-frame computation runs in the HIP library.  Extra keyword options:
   consumes the host generator on every rank and therefore requires identical torch RNG
   states on all ranks (checked at construction: ``ValueError`` otherwise);
 * ``shard=(world, rank)``: sharding with a caller-driven exchange (``exchange=`` or the
-  staged calls); a Philox filter then needs an explicit ``seed`` (nothing to broadcast);
+  staged calls); a Philox filter then needs an explicit ``seed`` (nothing to broadcast).
+  ``exchange(recv, send)`` is called twice per frame: with the (P x (d+1)) / (P_r x (d+1))
+  ``{class, state[d]}`` rows after the dynamics GP, then with the (P x 1) / (P_r x 1)
+  ``{ll}`` column after the observation GP;
 * ``dedup`` (default True): evaluate the dynamics GP once per distinct (resampling
   ancestor, new class) pair -- offspring of one ancestor hold bit-identical states -- and
   share the result; bitwise identical to ``dedup=False`` (every particle evaluated) with

@@ -19,13 +19,15 @@ gpmdm.py:923-963, 1032-1068; gpmdm_pf.py:137-262):
   classes exact, then ``conftest.assert_step_matches`` (weights 1e-4 -- see the test --,
   resample indices of
   the GPU's weights exact up to 2 CDF ties, states 1e-6, posterior 1e-6 abs, mean 1e-6);
-* configs[3]: 8 logical shards of P = 10^6 on one GPU, bitwise equal to one rank.
+* configs[3]: 8 logical shards of P = 10^6 on one GPU, bitwise equal to one rank, and one
+  single-rank Philox step at P = 10^6 against the oracle (classes exact, ll and states on a
+  random subset, every resample index, read-outs).
 """
 import numpy as np
 import pytest
 import torch
 
-from conftest import assert_step_matches, nrel, product_model
+from conftest import assert_step_matches, nrel, oracle_model, product_model
 
 pytestmark = pytest.mark.gpu
 
@@ -127,3 +129,67 @@ def test_config4_one_million_particles_8_shards(fx_config2):
             assert np.array_equal(ref.class_probabilities().numpy(), pf.class_probabilities().numpy())
             assert np.array_equal(ref.current_state_mean().numpy(), pf.current_state_mean().numpy())
         del full
+
+
+@pytest.mark.timeout(600)
+def test_one_million_particles_single_rank_vs_oracle(fx_config2):
+    """configs[3]'s particle count (P = 10^6, config-2 model) on ONE rank with Philox draws,
+    against the oracle (gpmdm_pf.py:137-262) -- not only shard invariance.  One warm-up
+    step (shared ancestors: the de-duplicated dynamics path and the guided inverse-CDF
+    search over int32 index buffers at 10^6), then one resynced step:
+      * every switched class exact (O.switch_classes with the restated Exp(1) draws);
+      * log-likelihoods and propagated states on a 2,000-particle random subset against
+        the oracle's dynamics map and observation map (the oracle cannot hold the whole
+        2000 x 10^6 kernel matrix), weights-tolerance 1e-5 on ll;
+      * every resample index against O.multinomial_resample_indices of the GPU's own
+        weights with the restated uniforms (<= 2 last-ulp CDF ties);
+      * posterior and state mean against the oracle read-outs at the GPU's indices."""
+    from gpmdm_amd import GPMDM_PF
+    from oracle import gpmdm_oracle as O
+    from oracle import philox as X
+    m = product_model(fx_config2)
+    om = oracle_model(fx_config2)
+    T = np.asarray(fx_config2["T"], dtype=np.float64)
+    P, C, d, seed = 1_000_000, 2, 3, 11
+    pf = GPMDM_PF(m, torch.tensor(T), P, rng="philox", seed=seed)
+    Y = m.get_Y()
+    pf.update(Y[10])
+    pre = pf.export_state()
+    frame = pf.frame
+    z = Y[11] + 0.01
+    pf.update(z)
+    post = pf.export_state()
+    idx = post["resample_idx"]
+    # classes: exact
+    cls1 = O.switch_classes(pre["classes"], T, X.switch_draws(seed, frame, P, C))
+    assert np.array_equal(post["classes"], cls1[idx])
+    # dynamics + likelihood on a random subset of particles
+    rng = np.random.RandomState(4)
+    sub = np.sort(rng.choice(P, 2000, replace=False))
+    nrm = X.dynamics_normals(seed, frame, P, d)[sub]
+    st1 = np.empty((sub.size, d))
+    for c in range(C):
+        sel = cls1[sub] == c
+        if sel.any():
+            mu, var = om.map_x_dynamics_for_class(pre["states"][sub[sel]], c)
+            st1[sel] = nrm[sel] * np.sqrt(var) + mu
+    ll_sub = O.log_likelihoods(om, st1, z)
+    assert np.max(np.abs(post["ll"][sub] - ll_sub)) < 1e-5, np.max(np.abs(post["ll"][sub] - ll_sub))
+    # propagated states: post-resample slots whose ancestor is in the subset
+    where = np.searchsorted(sub, idx)
+    hit = (where < sub.size) & (sub[np.minimum(where, sub.size - 1)] == idx)
+    if hit.any():
+        assert nrel(post["states"][hit], st1[where[hit]]) < 1e-6
+    # weights are the normalisation of the GPU's ll (gpmdm_pf.py:200-204)
+    log_w, w = O.normalise(post["ll"])
+    assert nrel(post["w"], w) < 1e-12
+    # resample indices: the oracle's search of the GPU's weights with the restated uniforms
+    u = X.resample_uniforms(seed, frame, P)
+    ref_idx = O.multinomial_resample_indices(post["w"], u)
+    assert int(np.sum(ref_idx != idx)) <= 2, int(np.sum(ref_idx != idx))
+    # read-outs at the GPU's indices
+    post_c = O.class_probabilities(post["ll"], post["log_w"], post["classes"], C)
+    assert np.max(np.abs(pf.class_probabilities().numpy() - post_c)) < 1e-6
+    assert nrel(pf.current_state_mean().numpy(), O.current_state_mean(post["states"], post["w"])) < 1e-6
+    assert abs(pf.log_likelihood() - O.log_likelihood_readout(post["ll"], post["log_w"])) <= 1e-9 * pf.log_likelihood()
+    assert pf.health() == {k: 0 for k in pf.health()}

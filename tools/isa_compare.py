@@ -2,8 +2,10 @@
 
     python tools/isa_compare.py OLD.so NEW.so [kernel-substring]
 
-Kernel-argument offsets (s_load immediates, struct-size multipliers) are normalised, so a
-change to the argument structs alone reads as "same".  Used to show that splitting the A/B
+Kernel-argument offsets (s_load immediates, struct-size multipliers) and the PC-relative
+offset right after s_getpc_b64 (the address of a __constant__ table, which moves when other
+data of the code object changes) are normalised, so a change to the argument structs or to
+unrelated constant data alone reads as "same".  Used to show that splitting the A/B
 laboratory out of gp_tile.h left every production tile instantiation's code unchanged
 (profiles/r03/isa_compare_lab_split.txt)."""
 import re
@@ -44,7 +46,7 @@ def kernels(lib):
         for co in code_objects(lib, tmp):
             asm = subprocess.run([str(LLVM / "llvm-objdump"), "-d", str(co)], check=True, capture_output=True,
                                  text=True).stdout
-            fn = None
+            fn, after_pc = None, False
             for line in asm.splitlines():
                 m = re.match(r"^[0-9a-f]+ <(.*)>:$", line)
                 if m:
@@ -53,8 +55,9 @@ def kernels(lib):
                     continue
                 if fn and line.strip():
                     ins = re.sub(r"\s+", " ", line.split("//")[0].strip())
-                    if ins.startswith(("s_load", "s_mul")):
+                    if ins.startswith(("s_load", "s_mul")) or (after_pc and ins.startswith("s_add_u32")):
                         ins = re.sub(r"0x[0-9a-f]+|\b\d+\b", "N", ins)
+                    after_pc = ins.startswith("s_getpc_b64")
                     out[fn].append(ins)
     return out
 

@@ -19,6 +19,16 @@ for lam in 1.0 0.3 0.1; do
     || { echo "bench predictive $lam failed rc=$?"; tail -20 $out/pred_$lam.err; exit 1; }
   python -c "import json;d=json.load(open('$out/pred_$lam.json'));print('lambda $lam', round(d['ms_per_step'],3), 'ms', 'ess_frac', d['ess_frac_last'], 'rows', d['dyn_rows_last'], d['stream_check'], d['stages_ms_per_step'])"
 done
+timeout -k 10 120 tools/microbench/store_hazard > $out/store_hazard.txt 2>&1 \
+  || { echo "store_hazard failed rc=$?"; cat $out/store_hazard.txt; exit 1; }
+cat $out/store_hazard.txt
+for g in 0 1; do
+  if [ $g = 1 ]; then export GPMDM_DYN_EXACT_GRID=1; fi
+  timeout -k 10 300 python -u bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-nodedup > $out/grid_$g.json 2> $out/grid_$g.err \
+    || { echo "bench grid $g failed rc=$?"; tail -20 $out/grid_$g.err; exit 1; }
+  python -c "import json;d=json.load(open('$out/grid_$g.json'));print('exact_grid $g', round(d['ms_per_step'],3), d['stages_ms_per_step'], d['dyn_rows_last'])"
+done
+unset GPMDM_DYN_EXACT_GRID
 timeout -k 10 900 bash tools/microbench/tile_ab.sh run > $out/tile_ab.txt 2>&1 \
   || { echo "tile_ab failed rc=$?"; tail -20 $out/tile_ab.txt; exit 1; }
 cat $out/tile_ab.txt
