@@ -346,6 +346,8 @@ def main():
     ap.add_argument("--bank", type=int, default=None,
                     help="filters of the bank line (config 1: 39, the notebook's test trials)")
     ap.add_argument("--no-nodedup", action="store_true")
+    ap.add_argument("--dyn-tiles", default="auto", choices=("auto", "narrow", "wide"),
+                    help="dynamics tile shape of the headline filter (gpmdm_pf_set_dyn_tiles)")
     args = ap.parse_args()
     global WORKLOAD
     WORKLOAD = workload(args.config)
@@ -397,7 +399,7 @@ def main():
     def new_filter(**kw):
         torch.manual_seed(11)
         return GPMDM_PF(model, T, P_total, rng=rng, seed=11 if rng == "philox" else None,
-                        process_group=group, **kw)
+                        process_group=group, dyn_tiles=args.dyn_tiles, **kw)
 
     stream_check = None
     if args.stream == "predictive":

@@ -93,8 +93,12 @@ def _build_lib(force: bool = False, verbose: bool = False) -> Path:
         list(ex.map(run, jobs))
     objs = [str(OBJ / (s + ".o")) for s in SOURCES]
     if force or jobs or not LIB.exists():
-        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(LIB), *objs,
+        # link to a temporary name, then rename: a reader (a process loading the library, a
+        # snapshot of the tree) never sees a partly written file
+        tmp = LIB.with_suffix(".so.tmp")
+        run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs,
              "-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
+        os.replace(tmp, LIB)
     return LIB
 
 

@@ -343,6 +343,27 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
     case GPMDM_TILE_32x512: obs_geo = kGeo32x512; break;
     default: break;   // rejected by check_model_desc
   }
+  // A/B override of the dynamics shapes ("nw,mt,ntw"; d <= 8): 16x256 (4,1,4), 16x512
+  // (4,1,8), 32x256 (4,2,4), 32x512 (4,2,8), 32x1024 (8,2,8), 64x256 (4,4,4), 64x512 (8,4,4)
+  auto geo_env = [&](const char* name, TileGeo& g) -> bool {
+    const char* v = std::getenv(name);
+    if (!v) return true;
+    TileGeo t{};
+    if (std::sscanf(v, "%d,%d,%d", &t.nw, &t.mt, &t.ntw) != 3) return false;
+    const TileGeo ok[] = {kGeo16x256, {4, 1, 8}, kGeo32x256, kGeo32x512, {8, 2, 8}, kGeo64x256, kGeo64x512};
+    for (const TileGeo& o : ok) {
+      if (o.nw != t.nw || o.mt != t.mt || o.ntw != t.ntw) continue;
+      const bool ab_only = (t.nw == 8 && t.mt == 2) || (t.mt == 1 && t.ntw == 8);   // launch_d: d <= 8
+      if (ab_only && d > 8) return false;
+      g = t;
+      return true;
+    }
+    return false;
+  };
+  if (!geo_env("GPMDM_DYN_GEO", dyn_geo) || !geo_env("GPMDM_DYNW_GEO", dynw_geo)) {
+    delete m;
+    return fail(GPMDM_E_INVALID, "GPMDM_DYN_GEO / GPMDM_DYNW_GEO: not a dynamics tile shape for this d");
+  }
   int rc = build_image(m->obs, (int)m->N, d, m->D, desc->X, desc->y_lengthscales, nullptr,
                        desc->obs_R, desc->obs_beta, obs_geo);
   if (rc) { delete m; return rc; }

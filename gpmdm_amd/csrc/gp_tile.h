@@ -555,6 +555,18 @@ void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
   // 1037 ms; the default 64 x 512 shape: 760 ms; profiles/r02/ablations/tb9, tb10)
   constexpr int kCoordVar = DI > 12 ? kTileCoordLDS : 0;
   if (dyn) {
+    // A/B shapes for the dynamics GPs (GPMDM_DYN_GEO / GPMDM_DYNW_GEO, capi.hip; d <= 8):
+    // 32 x 1024 (8 waves) and 16 x 512
+    if constexpr (DI <= 8) {
+      if (g.nw == 8 && g.mt == 2) {
+        hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 8, 2, 8>), grid, dim3(512), 0, stream, p);
+        return;
+      }
+      if (g.nw == 4 && g.mt == 1 && g.ntw == 8) {
+        hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 1, 8>), grid, dim3(256), 0, stream, p);
+        return;
+      }
+    }
     if (g.nw == 8)
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 8>), grid, dim3(512), 0, stream, p);
     else if (g.mt == 2 && g.ntw == 8)

@@ -29,7 +29,4 @@ for g in 0 1; do
   python -c "import json;d=json.load(open('$out/grid_$g.json'));print('exact_grid $g', round(d['ms_per_step'],3), d['stages_ms_per_step'], d['dyn_rows_last'])"
 done
 unset GPMDM_DYN_EXACT_GRID
-timeout -k 10 900 bash tools/microbench/tile_ab.sh run > $out/tile_ab.txt 2>&1 \
-  || { echo "tile_ab failed rc=$?"; tail -20 $out/tile_ab.txt; exit 1; }
-cat $out/tile_ab.txt
 echo done
