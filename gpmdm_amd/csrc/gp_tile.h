@@ -151,13 +151,21 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   const int lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = blockIdx.x;
-  const int J = prm.n_j_max - 1 - b / prm.tiles_ub;
+  // Dynamics launches size their grid by an upper bound (the de-duplicated row count is
+  // only known on the device): the real tile count tu is read from the segment table and
+  // workgroups map real-first -- J-major over the tu real tiles, heavy blocks first -- so
+  // the empty workgroups trail the real work instead of sitting between the column blocks.
+  // The observation GP's grid is exact (tu = tiles_ub).
+  const int tu = DYN ? __builtin_amdgcn_readfirstlane(prm.seg_tile_start[prm.n_seg] - prm.seg_tile_start[0])
+                     : prm.tiles_ub;
+  if (DYN && (tu <= 0 || b >= prm.n_j_max * tu)) return;
+  const int J = prm.n_j_max - 1 - b / tu;
   // tile index within this launch's segments (a launch may cover classes c0..c0+7)
   // segment tables live in device memory (the filter computes them on the device; the
   // predictive maps write theirs with k_seg_table).  A by-value table with a per-thread
   // select cost the d = 16 64x512 tile 6.7% through register allocation (tools/microbench/
   // tile_ab.sh: 760 -> 811 ms per config-5 launch)
-  const int t = b - (b / prm.tiles_ub) * prm.tiles_ub + prm.seg_tile_start[0];
+  const int t = b - (b / tu) * tu + prm.seg_tile_start[0];
 
   int c = -1;
   for (int s = 0; s < prm.n_seg; ++s)

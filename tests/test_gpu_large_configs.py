@@ -15,8 +15,9 @@ O(N^3) three times over and would dominate the run at N = 2 x 10^4; the two agre
 gpmdm.py:923-963, 1032-1068; gpmdm_pf.py:137-262):
 
 * predictive maps at 500 query points: means 1e-8, variances 1e-6 normwise;
-* one resynced filter step at P = 2000 with explicit draws (update_with_draws): switched
-  classes exact, then ``conftest.assert_step_matches`` (weights 1e-4 -- see the test --,
+* two resynced filter steps at P = 2000 with explicit draws (update_with_draws): switched
+  classes exact, every log-likelihood to 1e-5 of its terms' magnitude, then
+  ``conftest.assert_step_matches`` (weights 1e-4 -- see the test --,
   resample indices of
   the GPU's weights exact up to 2 CDF ties, states 1e-6, posterior 1e-6 abs, mean 1e-6);
 * configs[3]: 8 logical shards of P = 10^6 on one GPU, bitwise equal to one rank, and one
@@ -71,29 +72,36 @@ def test_large_config_maps_and_step_vs_oracle(cfg):
         omu, ovar = om.map_x_dynamics_for_class(xs, k)
         assert nrel(mu.numpy(), omu) < 1e-8, k
         assert nrel(var.numpy(), ovar) < 1e-6, k
-    # one resynced filter step from a spread-out cloud (two warm-up steps on the device)
+    # two resynced filter steps from a spread-out cloud (two warm-up steps on the device)
     P = 2000
     T = synthetic.markov_matrix(C)
     pf = GPMDM_PF(m, torch.tensor(T), P, rng="torch")
     torch.manual_seed(cfg)
-    zs = data.observation_stream(3, seed=1)
+    zs = data.observation_stream(4, seed=1)
     pf.update(zs[0])
     pf.update(zs[1])
-    st0 = pf.export_state()
-    E = rng.exponential(size=(P, C))
-    cls1 = O.switch_classes(st0["classes"], T, E)
-    nrm = rng.randn(P, d)
-    u = rng.rand(P)
-    pf.update_with_draws(zs[2], E, nrm, u)
-    r = O.step(om, T, st0["states"], st0["classes"], zs[2], E, nrm, u)
-    st = pf.export_state()
-    assert np.array_equal(cls1, r.classes_switched)
-    # weights 1e-4: at N = 10^4 / 2 x 10^4 the variance 1 - k^T K^-1 k (cond(K_y) ~ 1e6, vc ~
-    # 1e-2) carries ~1e-8 relative rounding in any fp64 evaluation, the log-likelihood
-    # (|ll| ~ 500) ~1e-5 absolute, so the normalised weights differ at ~1e-5 between two
-    # correct fp64 evaluations (measured 0.3-1.6e-5 GPU vs oracle across boxes)
-    assert_step_matches(st, r, pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), u,
-                        what=f"config {cfg}", w_tol=1e-4)
+    for k in (2, 3):
+        st0 = pf.export_state()
+        E = rng.exponential(size=(P, C))
+        cls1 = O.switch_classes(st0["classes"], T, E)
+        nrm = rng.randn(P, d)
+        u = rng.rand(P)
+        pf.update_with_draws(zs[k], E, nrm, u)
+        r = O.step(om, T, st0["states"], st0["classes"], zs[k], E, nrm, u)
+        st = pf.export_state()
+        assert np.array_equal(cls1, r.classes_switched)
+        # weights 1e-4: at N = 10^4 / 2 x 10^4 the variance 1 - k^T K^-1 k (cond(K_y) ~ 1e6,
+        # vc ~ 1e-2) carries ~1e-8 relative rounding in any fp64 evaluation, the
+        # log-likelihood (|ll| ~ 500) ~1e-5 absolute, so the normalised weights differ at
+        # ~1e-5 between two correct fp64 evaluations (measured 0.3-1.6e-5 GPU vs oracle
+        # across boxes).  The log-likelihoods themselves: 1e-5 of the magnitude of the terms
+        # they sum, for every particle.
+        mu_s, var_s = om.map_x_to_y(r.states_propagated)
+        terms = (np.sum((np.asarray(zs[k], dtype=np.float64)[None, :] - mu_s) ** 2 / var_s
+                        + 2.0 * np.abs(np.log(var_s)), axis=1) + abs(O.loglik_const(m.D)))
+        assert np.max(np.abs(st["ll"] - r.ll) / terms) < 1e-5, (cfg, k)
+        assert_step_matches(st, r, pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), u,
+                            what=f"config {cfg} step {k}", w_tol=1e-4)
     assert all(v == 0 for v in pf.health().values())
 
 
