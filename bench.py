@@ -46,6 +46,9 @@ Prints ONE JSON line (rank 0) with the contract fields plus:
                 headline's dynamics stage is cheap partly because resampling collapses the
                 cloud onto few ancestors; this line does not depend on that
   ess_last      effective sample size 1 / sum w^2 of the last timed step's weights
+  spread        (config 2, one GPU) the same step on a cloud that stays spread out
+                (spread_line: less peaked observation GP + predictive stream), with its
+                ESS, dynamics rows per frame, stage times and dynamics-tile TF/s
 """
 from __future__ import annotations
 
@@ -152,6 +155,9 @@ def host_cores():
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = nproc
+    quota = cgroup_cpu_quota()          # a CFS quota caps the CPUs this process really gets
+    if quota:
+        usable = max(1, min(usable, int(np.ceil(quota))))
     capped = None
     for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
         v = os.environ.get(k)
@@ -220,7 +226,7 @@ def cpu_baseline(data, budget_s=12.0):
            "nproc": nproc, "sched_affinity_cores": usable, "cgroup_cpu_quota": cgroup_cpu_quota(), "torch_threads": int(torch.get_num_threads()),
            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
            "sample": f"oracle (numpy fp64 restatement of gpmdm_pf.py's step, BLAS pool set to all {usable} usable "
-                     f"cores) N={N} D={w['D']} d={w['d']} C={w['C']}, P={Ps} particles x {steps} frames in "
+                     f"cores: CPU affinity capped by the cgroup CPU quota) N={N} D={w['D']} d={w['d']} C={w['C']}, P={Ps} particles x {steps} frames in "
                      f"{el:.1f} s (model precompute excluded)",
            "calibration": "port vs the unmodified reference on 8 threads of the build container: "
                           "profiles/r03/cpu_calibration.txt, BASELINE.md §2"}
@@ -254,6 +260,67 @@ def predictive_stream(pf, model, frames, seed=5):
                 "note": "z_f = mu(x_r) + sqrt(var(x_r)) eps, r a uniform particle of the cloud after frame "
                         "f-1, from an untimed pass of the same filter (same seed); the timed pass replays "
                         "the stream"}
+
+
+SPREAD_LAMBDA = 0.05   # observation-GP output scale of the spread-cloud line (see spread_line)
+
+
+def spread_line(device, steps, warmup=5, y_lambda=SPREAD_LAMBDA):
+    """The headline step on a cloud that stays spread out: the same configuration with the
+    observation GP's output scales exp(y_log_lambdas) = y_lambda (a less peaked likelihood)
+    and the predictive observation stream (predictive_stream), so resampling keeps many
+    distinct ancestors and the dynamics GP evaluates tens of thousands of rows per frame.
+    Times `steps` frames after `warmup`; per-stage times, ESS and dynamics rows come from the
+    same frames (every stage's events on: two event records per stage)."""
+    import torch
+    from gpmdm_amd import GPMDM_PF, synthetic
+    saved = WORKLOAD["y_lambda"]
+    WORKLOAD["y_lambda"] = y_lambda
+    try:
+        model, _ = build_model(device)
+    finally:
+        WORKLOAD["y_lambda"] = saved
+    T = torch.from_numpy(synthetic.markov_matrix(WORKLOAD["C"]))
+    P = WORKLOAD["P_per_gpu"]
+
+    def new_filter():
+        torch.manual_seed(11)
+        return GPMDM_PF(model, T, P, rng="philox", seed=11)
+
+    zs, check = predictive_stream(new_filter(), model, warmup + steps)
+    pf = new_filter()
+    for k in range(warmup):
+        pf.update(zs[k])
+        pf.class_probabilities()
+    torch.cuda.synchronize()
+    pf.stage_times()
+    pf.enable_timing(True)
+    ess, rows = [], []
+    t0 = time.perf_counter()
+    for k in range(steps):
+        pf.update(zs[warmup + k])
+        pf.get_most_likely_class()
+        pf.class_probabilities()
+        pf.current_state_mean()
+        rows.append(pf.dynamics_rows())
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    pf.enable_timing(False)
+    st = pf.stage_times()
+    w = pf.export_state()["w"]
+    ess_last = float(1.0 / np.sum(w * w))
+    dyn_ms = st["dyn_gemm"][0] / max(st["dyn_gemm"][1], 1)
+    mean_rows = float(np.mean(rows))
+    return {"y_lambda": y_lambda, "stream": "predictive", "steps": steps, "ms_per_step": el / steps * 1e3,
+            "value": P * steps / el, "ess_frac_last": ess_last / P,
+            "generator_ess_last10_mean": check["generator_ess_last10_mean"],
+            "replay_matches": bool(np.array_equal(pf.class_probabilities().numpy(), check["posterior"])),
+            "dyn_rows_mean": mean_rows, "dyn_rows_frac": mean_rows / P,
+            "stages_ms_per_step": {k: v[0] / max(v[1], 1) for k, v in st.items()},
+            "dyn_gemm_tflops": dyn_row_flops(model) * mean_rows / max(dyn_ms, 1e-9) / 1e9,
+            "note": "same N/D/d/C/P as the headline; exp(y_log_lambdas) = y_lambda and the predictive "
+                    "observation stream keep the cloud spread out; timed with every stage's events on "
+                    "(ms_per_step includes them)"}
 
 
 def nodedup_line(model, T, P_total, group, dist, device, zs, steps, rng):
@@ -346,6 +413,8 @@ def main():
     ap.add_argument("--bank", type=int, default=None,
                     help="filters of the bank line (config 1: 39, the notebook's test trials)")
     ap.add_argument("--no-nodedup", action="store_true")
+    ap.add_argument("--spread-steps", type=int, default=None,
+                    help="frames of the spread-cloud line (config 2, one GPU; default 30, 0 = off)")
     ap.add_argument("--dyn-tiles", default="auto", choices=("auto", "narrow", "wide"),
                     help="dynamics tile shape of the headline filter (gpmdm_pf_set_dyn_tiles)")
     args = ap.parse_args()
@@ -453,6 +522,9 @@ def main():
     ess = float(1.0 / np.sum(w_last * w_last))
     bank = bank_line(model, T, args.bank, P_total, zs, args.warmup, args.steps) if args.bank and world == 1 else None
     nodedup = None if args.no_nodedup else nodedup_line(model, T, P_total, group, dist, device, zs, args.steps, rng)
+    if args.spread_steps is None:
+        args.spread_steps = 30 if (args.config == 2 and args.stream == "mocap" and args.y_lambda == 1.0) else 0
+    spread = spread_line(device, args.spread_steps) if args.spread_steps and world == 1 else None
     N, D, d = model.X.shape[0], model.D, model.d
     P_local = P_total // world
     alg, dense, executed = obs_kernel_flops(N, D)
@@ -516,6 +588,8 @@ def main():
     }
     if bank is not None:
         rec["bank"] = bank
+    if spread is not None:
+        rec["spread"] = spread
     if args.config == 1:
         ms = elapsed / args.steps * 1e3
         rec["ms_per_frame"] = ms

@@ -20,7 +20,7 @@ else
   # timings alternate between the builds; the first round also prints a hash of each
   # build's production-variant q partials and means (TB_QHASH): equal hashes = bitwise equal
   for r in 1 2; do
-    h=$([ $r = 1 ] && echo 1)
+    h=$([ $r = 1 ] && echo 1 || true)
     for b in $out/tile_ab_d16_*; do echo "== $b"; TB_QHASH=$h timeout -k 10 170 $b 125000 20000 256 | grep -E "median|qhash"; done
     for b in $out/tile_ab_d8_*; do echo "== $b"; TB_QHASH=$h timeout -k 10 120 $b 100000 10000 128 | grep -E "median|qhash"; done
     for b in $out/tile_ab_d3_*; do echo "== $b"; TB_QHASH=$h timeout -k 10 60 $b | grep -E "median|qhash"; done

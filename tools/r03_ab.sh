@@ -5,9 +5,11 @@ set -o pipefail
 out=gpurun_out/r03_ab
 mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 700 bash tools/microbench/tile_ab.sh run > $out/tile_ab.txt 2>&1 \
-  || { echo "tile_ab failed rc=$?"; tail -20 $out/tile_ab.txt; exit 1; }
-cat $out/tile_ab.txt
+if [ -n "${TILE_AB:-}" ]; then
+  timeout -k 10 700 bash tools/microbench/tile_ab.sh run > $out/tile_ab.txt 2>&1 \
+    || { echo "tile_ab failed rc=$?"; tail -20 $out/tile_ab.txt; exit 1; }
+  cat $out/tile_ab.txt
+fi
 timeout -k 10 600 bash tools/dyn_ab.sh $out/dynab 2>&1 | tee $out/dyn_ab.txt
 for lam in 0.05 0.03; do
   timeout -k 10 300 python -u bench.py --stream predictive --y-lambda $lam --steps 30 --warmup 5 --no-cpu-baseline > $out/pred_$lam.json 2> $out/pred_$lam.err \
