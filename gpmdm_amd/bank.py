@@ -94,6 +94,7 @@ class GPMDM_PF_Bank:
 
     def _sync_model(self):
         """Rebind to the GPMDM's current device image (see GPMDM_PF._sync_model)."""
+        self._gpmdm._refresh()
         if self._h is not None and self._gpmdm.generation != self._model_gen:
             _lib.check(_lib.load().gpmdm_pf_set_model(self._h, self._gpmdm.handle), "rebind to the rebuilt model")
             self._model_gen = self._gpmdm.generation
@@ -105,7 +106,7 @@ class GPMDM_PF_Bank:
         C, P = self.num_classes, self._num_particles
         g, r = divmod(P, C)
         counts = [g + (1 if i < r else 0) for i in range(C)]
-        Xc = [self._gpmdm.get_X_for_class(c).numpy() for c in range(C)]
+        Xc = [self._gpmdm.get_X_for_class(c).detach().cpu().numpy() for c in range(C)]
         sizes = [x.shape[0] for x in Xc]
         states, classes = [], []
         for f in range(self._f_lo, self._f_hi):

@@ -5,9 +5,9 @@ data registry, latent initialisation, kernel-inverse precompute, persistence and
 predictive maps; the predictive maps and everything per frame run in libgpmdm_hip.so.
 Training (``gpdm_loss`` / ``train_adam``, gpmdm.py:550-885) runs
 on the model's GPU in ``gpmdm_amd/training.py`` and re-uploads the device model when it
-finishes; ``set_training_mode`` (gpmdm.py:247-279) selects which parameters the loss
-functions treat as trainable (``_trainable``), and the ``flg_train_*`` constructor flags
-are recorded there as the reference records them in ``flg_trainable_list``.
+finishes; ``set_training_mode`` / ``set_evaluation_mode`` (gpmdm.py:239-279) set the
+parameters' ``requires_grad`` as the reference does.  ``GPMDM`` is a ``torch.nn.Module``
+with the reference's parameters (see the class docstring).
 
 Precompute follows the reference recipe (gpmdm.py:1284-1305) on class blocks only:
 ``U = chol(K, upper)``, ``R = U^-1``, ``K^-1 = R R^T``.  The library keeps ``R`` (upper
@@ -81,16 +81,29 @@ def read_reference_checkpoint(path):
     return save_dict["config_dict"], save_dict["state_dict"]
 
 
-class GPMDM:
+class GPMDM(torch.nn.Module):
     """Gaussian Process Multi-Dynamical Model -- inference-side mirror of gpmdm.py:GPMDM.
+
+    A ``torch.nn.Module`` like the reference's (gpmdm.py:18): the seven log-hyperparameters
+    and the latents ``X`` are ``nn.Parameter``s registered in the reference's order
+    (gpmdm.py:201-230, 773), so ``state_dict`` / ``load_state_dict`` / ``parameters`` /
+    ``named_parameters`` / ``train()`` / ``eval()`` / ``requires_grad`` and external
+    optimisers over ``parameters()`` behave as there.  The parameters live on the host
+    (``.to()`` moves them as for any module); the device model -- factors and packed tile
+    images in libgpmdm_hip -- lives on ``device`` and is rebuilt whenever the parameters
+    change, including in-place updates by an optimiser (detected through the parameters'
+    version counters on the next use).
 
     Constructor arguments are those of the reference (gpmdm.py:96-109).  ``dtype`` must be
     float64 (the reference default, required for parity: SURVEY.md §8(c)).  ``device`` is
-    the GPU the model lives on (default: the current HIP device, as torch's ``"cuda"``
-    resolves it); ``flg_train_*`` record which parameters training updates (gpmdm.py:
-    96-107, 239-279; ``train_adam`` itself trains every parameter, as the reference's
-    does after ``set_training_mode('all')``).
+    the GPU the device model lives on (default: the current HIP device, as torch's
+    ``"cuda"`` resolves it); ``flg_train_*`` are the parameters' ``requires_grad`` flags
+    (gpmdm.py:96-107; ``train_adam`` trains every parameter, as the reference's does after
+    ``set_training_mode('all')``).
     """
+
+    _PARAMS = ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n", "x_log_lengthscales",
+               "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff", "X")
 
     def __init__(self, D, d, n_classes, dyn_target, dyn_back_step,
                  y_lambdas_init, y_lengthscales_init, y_sigma_n_init,
@@ -100,6 +113,7 @@ class GPMDM:
                  flg_train_x_sigma_n=True, flg_train_x_lin_coeff=True,
                  sigma_n_num_Y=0., sigma_n_num_X=0.,
                  dtype=torch.float64, device=None):
+        super().__init__()
         if dtype != torch.float64:
             raise NotImplementedError("gpmdm_amd computes in float64 only (reference default, gpmdm.py:109)")
         if dyn_target not in ("full", "delta") or dyn_back_step not in (1, 2):
@@ -114,18 +128,25 @@ class GPMDM:
         self.D, self.d, self.n_classes = int(D), int(d), int(n_classes)
         self.dyn_target, self.dyn_back_step = dyn_target, int(dyn_back_step)
         f64 = dict(dtype=torch.float64)
-        self.y_log_lengthscales = torch.log(torch.as_tensor(_to_np(y_lengthscales_init), **f64)).reshape(-1)
-        self.y_log_lambdas = torch.log(torch.as_tensor(_to_np(y_lambdas_init), **f64)).reshape(-1)
-        self.y_log_sigma_n = torch.log(torch.as_tensor(float(y_sigma_n_init), **f64))
-        self.x_log_lengthscales = torch.log(torch.as_tensor(_to_np(x_lengthscales_init), **f64)).reshape(-1)
-        self.x_log_lambdas = torch.log(torch.as_tensor(_to_np(x_lambdas_init), **f64)).reshape(-1)
-        self.x_log_sigma_n = torch.log(torch.as_tensor(float(x_sigma_n_init), **f64))
-        self.x_log_lin_coeff = torch.log(torch.as_tensor(_to_np(x_lin_coeff_init), **f64)).reshape(-1)
+
+        def param(v, grad, vec=True):
+            t = torch.log(torch.as_tensor(_to_np(v) if vec else float(v), **f64))
+            return torch.nn.Parameter(t.reshape(-1) if vec else t, requires_grad=bool(grad))
+
+        # registration order = the reference's (its state_dict order)
+        self.y_log_lengthscales = param(y_lengthscales_init, flg_train_y_lengthscales)
+        self.y_log_lambdas = param(y_lambdas_init, flg_train_y_lambdas)
+        self.y_log_sigma_n = param(y_sigma_n_init, flg_train_y_sigma_n, vec=False)
+        self.x_log_lengthscales = param(x_lengthscales_init, flg_train_x_lengthscales)
+        self.x_log_lambdas = param(x_lambdas_init, flg_train_x_lambdas)
+        self.x_log_sigma_n = param(x_sigma_n_init, flg_train_x_sigma_n, vec=False)
+        self.x_log_lin_coeff = param(x_lin_coeff_init, flg_train_x_lin_coeff)
+        self.register_parameter("X", None)          # set by init_X / set_latents / load
         self.sigma_n_num_Y = float(sigma_n_num_Y)
         self.sigma_n_num_X = float(sigma_n_num_X)
         self.class_aware_observations_list = [[] for _ in range(self.n_classes)]
-        self.X = None
         self._handle = None
+        self._uploaded = None       # parameter versions the device model was built from
         # where _precompute_kernel_inverses runs: None = torch on the CPU for N <= 4096 (the
         # reference's own arithmetic), the library's device factor (gpmdm_gp_factor:
         # rocSOLVER potrf/trtri) above; or force "cpu" / "device"
@@ -141,10 +162,38 @@ class GPMDM:
         self.flg_trainable_list = [k for k, v in flags.items() if v]
         self.generation = 0         # bumped by every device upload (filters rebind to it)
 
+    # ---- parameters ---------------------------------------------------------------
+    def _host(self, name: str) -> torch.Tensor:
+        """A detached host (CPU) view of a parameter."""
+        return getattr(self, name).detach().cpu()
+
+    def _set_param(self, name: str, value) -> None:
+        """Install a parameter value: in place when the shape matches (keeps requires_grad
+        and any optimiser's reference), a new Parameter otherwise."""
+        t = torch.as_tensor(_to_np(value), dtype=torch.float64)
+        cur = getattr(self, name, None)
+        if isinstance(cur, torch.nn.Parameter) and cur.shape == t.shape:
+            with torch.no_grad():
+                cur.copy_(t.to(cur.device))
+        else:
+            grad = cur.requires_grad if isinstance(cur, torch.nn.Parameter) else True
+            setattr(self, name, torch.nn.Parameter(t.clone(), requires_grad=grad))
+
+    def _param_versions(self):
+        return tuple((n, p.data_ptr(), p._version) for n, p in self.named_parameters())
+
+    def _refresh(self) -> None:
+        """Rebuild the device model when the parameters changed since it was built (an
+        optimiser step over parameters(), a .to(), an in-place edit)."""
+        if self.X is not None and self._handle is not None and self._uploaded != self._param_versions():
+            self._precompute_kernel_inverses()
+
     # ---- reference API: data registry (gpmdm.py:239-309) -------------------------
     def set_evaluation_mode(self):
-        """gpmdm.py:239-245 (no autograd state is kept here)."""
+        """gpmdm.py:239-245: every parameter's requires_grad off."""
         self.flg_trainable_list = []
+        for prm in self.parameters():
+            prm.requires_grad = False
 
     # ---- reference API: training (gpmdm.py:247-279, 550-628, 721-885) ---------------
     _Y_PARAMS = ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n")
@@ -155,11 +204,15 @@ class GPMDM:
         if model == 'all':
             self._trainable = {n: True for n in self._Y_PARAMS + self._X_PARAMS + ("X",)}
         elif model == 'latent':
-            self._trainable = {**{n: True for n in self._Y_PARAMS}, **{n: False for n in self._X_PARAMS}, "X": True}
+            self._trainable = {**{n: True for n in self._Y_PARAMS}, **{n: False for n in self._X_PARAMS}}
         elif model == 'dynamics':
-            self._trainable = {**{n: False for n in self._Y_PARAMS}, **{n: True for n in self._X_PARAMS}, "X": True}
+            self._trainable = {**{n: False for n in self._Y_PARAMS}, **{n: True for n in self._X_PARAMS}}
         else:
             raise ValueError('model must be \'all\', \'latent\' or \'dynamics\'')
+        for n, flag in self._trainable.items():       # X keeps its flag for 'latent' / 'dynamics'
+            prm = getattr(self, n, None)
+            if prm is not None:
+                prm.requires_grad = flag
 
     def get_y_neg_log_likelihood(self, Y, X, N):
         """gpmdm.py:550-590 on the model's device (fp64 Cholesky + triangular solve); returns
@@ -222,7 +275,7 @@ class GPMDM:
 
     def get_latent_sequences(self):
         """gpmdm.py:887-904."""
-        X = self.X.numpy()
+        X = self._host("X").numpy()
         out, s = [], 0
         for seq in self.observations_list:
             out.append(X[s:s + len(seq)])
@@ -260,12 +313,12 @@ class GPMDM:
         """PCA initialisation of the latents (gpmdm.py:762-777), then the precompute."""
         from sklearn.decomposition import PCA   # the reference's own dependency (gpmdm.py:12)
         X0 = PCA(n_components=self.d).fit_transform(self.get_Y())
-        self.X = torch.tensor(X0, dtype=torch.float64)
+        self._set_param("X", X0)
         self._precompute_kernel_inverses()
 
     def set_latents(self, X):
         """Install trained latents (e.g. from a saved model) and rebuild the device model."""
-        self.X = torch.as_tensor(_to_np(X), dtype=torch.float64).clone()
+        self._set_param("X", X)
         self._precompute_kernel_inverses()
 
     def _class_dynamics_rows(self):
@@ -279,17 +332,20 @@ class GPMDM:
                                       "reference PF does, gpmdm_pf.py:164)")
         N = self.X.shape[0]
         where = self._precompute_device or ("cpu" if N <= 4096 else "device")
+        versions = self._param_versions()
         if where == "device":
-            return self._precompute_on_device()
+            self._precompute_on_device()
+            self._uploaded = versions
+            return
         dev = torch.device("cpu")
         f64 = dict(dtype=torch.float64, device=dev)
-        X = self.X.to(**f64)
+        X = self._host("X").to(**f64)
         Y = torch.as_tensor(self.get_Y(), **f64)
         eye = lambda n: torch.eye(n, **f64)  # noqa: E731
-        ylog_ls, xlog_ls = self.y_log_lengthscales.to(dev), self.x_log_lengthscales.to(dev)
-        xlog_c = self.x_log_lin_coeff.to(dev)
+        ylog_ls, xlog_ls = self._host("y_log_lengthscales"), self._host("x_log_lengthscales")
+        xlog_c = self._host("x_log_lin_coeff")
         with torch.no_grad():
-            Ky = torch.exp(-_sq_dist(X, X, ylog_ls)) + torch.exp(self.y_log_sigma_n.to(dev)) ** 2 * eye(N) \
+            Ky = torch.exp(-_sq_dist(X, X, ylog_ls)) + torch.exp(self._host("y_log_sigma_n")) ** 2 * eye(N) \
                 + self.sigma_n_num_Y ** 2 * eye(N)
             Ry = _chol_inv_factor(Ky, "K_y")
             del Ky
@@ -305,7 +361,7 @@ class GPMDM:
                     raise ValueError(f"class {c} has no dynamics pairs")
                 xi, xo = Xin[off:off + n_c], Xout[off:off + n_c]
                 off += n_c
-                K = torch.exp(-_sq_dist(xi, xi, xlog_ls)) + torch.exp(self.x_log_sigma_n.to(dev)) ** 2 * eye(n_c) \
+                K = torch.exp(-_sq_dist(xi, xi, xlog_ls)) + torch.exp(self._host("x_log_sigma_n")) ** 2 * eye(n_c) \
                     + self.sigma_n_num_X ** 2 * eye(n_c)
                 K = K + _lin(xi, xi, xlog_c)
                 K = K + 1e-6 * eye(n_c)
@@ -314,6 +370,7 @@ class GPMDM:
                 dyn.append((xi.cpu().numpy().copy(), Rc.cpu().numpy().copy(), alpha.cpu().numpy().copy()))
             obs = (Ry.cpu().numpy().copy(), beta.cpu().numpy().copy())
         self._upload(obs, dyn)
+        self._uploaded = versions
 
     def _precompute_on_device(self):
         """The same factors through gpmdm_gp_factor (device Gram matrix, rocSOLVER potrf +
@@ -333,21 +390,21 @@ class GPMDM:
                                            a, b, c, _lib.dptr(B), B.shape[1], _lib.dptr(R), _lib.dptr(M)), what)
             return R, M
 
-        X = self.X.numpy()
+        X = self._host("X").numpy()
         Y = np.asarray(self.get_Y(), dtype=np.float64)
-        sy2 = float(torch.exp(self.y_log_sigma_n)) ** 2
-        sx2 = float(torch.exp(self.x_log_sigma_n)) ** 2
-        Ry, beta = factor(X, self.y_log_lengthscales, None, sy2, self.sigma_n_num_Y ** 2, 0.0, Y, "K_y")
-        Xin, Xout, _ = self.get_Xin_Xout_matrices(X=self.X)
+        sy2 = float(torch.exp(self._host("y_log_sigma_n"))) ** 2
+        sx2 = float(torch.exp(self._host("x_log_sigma_n"))) ** 2
+        Ry, beta = factor(X, self._host("y_log_lengthscales"), None, sy2, self.sigma_n_num_Y ** 2, 0.0, Y, "K_y")
+        Xin, Xout, _ = self.get_Xin_Xout_matrices(X=self._host("X"))
         Xin, Xout = _to_np(Xin), _to_np(Xout)
-        c2 = _to_np(torch.exp(self.x_log_lin_coeff) ** 2)
+        c2 = _to_np(torch.exp(self._host("x_log_lin_coeff")) ** 2)
         dyn, off = [], 0
         for c, n_c in enumerate(self._class_dynamics_rows()):
             if n_c <= 0:
                 raise ValueError(f"class {c} has no dynamics pairs")
             xi, xo = Xin[off:off + n_c], Xout[off:off + n_c]
             off += n_c
-            Rc, alpha = factor(xi, self.x_log_lengthscales, c2, sx2, self.sigma_n_num_X ** 2, 1e-6, xo,
+            Rc, alpha = factor(xi, self._host("x_log_lengthscales"), c2, sx2, self.sigma_n_num_X ** 2, 1e-6, xo,
                                f"K_x class {c}")
             dyn.append((np.ascontiguousarray(xi), Rc, alpha))
         self._upload((Ry, beta), dyn)
@@ -366,11 +423,11 @@ class GPMDM:
         desc = _lib.ModelDesc()
         desc.N, desc.D, desc.d, desc.C = self.X.shape[0], D, d, C
         desc.tile_shape = self.tile_shape
-        desc.X = arr(self.X.numpy())
+        desc.X = arr(self._host("X").numpy())
         desc.obs_R = arr(Ry)
         desc.obs_beta = arr(beta)
-        desc.y_lengthscales = arr(torch.exp(self.y_log_lengthscales).numpy())
-        desc.y_inv_lambda2 = arr((torch.exp(self.y_log_lambdas) ** -2).numpy())
+        desc.y_lengthscales = arr(torch.exp(self._host("y_log_lengthscales")).numpy())
+        desc.y_inv_lambda2 = arr((torch.exp(self._host("y_log_lambdas")) ** -2).numpy())
         nc = np.asarray([x[0].shape[0] for x in dyn], dtype=np.int64)
         keep.append(nc)
         desc.Nc = _lib.i64ptr(nc)
@@ -380,9 +437,9 @@ class GPMDM:
         a_p = PtrArr(*[arr(x[2]) for x in dyn])
         keep += [xin_p, r_p, a_p]
         desc.Xin, desc.dyn_R, desc.dyn_alpha = xin_p, r_p, a_p
-        desc.x_lengthscales = arr(torch.exp(self.x_log_lengthscales).numpy())
-        desc.x_lin_coeff2 = arr((torch.exp(self.x_log_lin_coeff) ** 2).numpy())
-        desc.x_inv_lambda2 = arr((torch.exp(self.x_log_lambdas) ** -2).numpy())
+        desc.x_lengthscales = arr(torch.exp(self._host("x_log_lengthscales")).numpy())
+        desc.x_lin_coeff2 = arr((torch.exp(self._host("x_log_lin_coeff")) ** 2).numpy())
+        desc.x_inv_lambda2 = arr((torch.exp(self._host("x_log_lambdas")) ** -2).numpy())
         handle = ctypes.c_void_p()
         self._release()
         _lib.check(lib.gpmdm_model_create(ctypes.byref(desc), self.device.index, ctypes.byref(handle)),
@@ -405,6 +462,7 @@ class GPMDM:
     def handle(self):
         if self._handle is None:
             raise RuntimeError("model not initialised: call init_X() (or load a saved model)")
+        self._refresh()
         return self._handle
 
     # ---- predictive maps (gpmdm.py:923-963, 1032-1068) --------------------------
@@ -431,8 +489,8 @@ class GPMDM:
         """gpmdm.py:923-963: mean and diagonal variance of the observation GP at Xstar."""
         mu, var = self._predict(Xstar)
         if flg_noise:   # gpmdm.py:988-989
-            extra = float(torch.exp(self.y_log_sigma_n) ** 2) + self.sigma_n_num_Y ** 2
-            var = var + extra * (torch.exp(self.y_log_lambdas) ** -2).to(var.device)[None, :]
+            extra = float(torch.exp(self._host("y_log_sigma_n")) ** 2) + self.sigma_n_num_Y ** 2
+            var = var + extra * (torch.exp(self._host("y_log_lambdas")) ** -2).to(var.device)[None, :]
         return mu, var
 
     def map_x_dynamics_for_class(self, Xstar, class_index: int, flg_noise: bool = False):
@@ -441,8 +499,8 @@ class GPMDM:
             raise ValueError("class_index out of range")
         mu, var = self._predict(Xstar, class_index)
         if flg_noise:   # gpmdm.py:1095-1098
-            extra = float(torch.exp(self.x_log_sigma_n) ** 2) + self.sigma_n_num_X ** 2
-            var = var + extra * (torch.exp(self.x_log_lambdas) ** -2).to(var.device)[None, :]
+            extra = float(torch.exp(self._host("x_log_sigma_n")) ** 2) + self.sigma_n_num_X ** 2
+            var = var + extra * (torch.exp(self._host("x_log_lambdas")) ** -2).to(var.device)[None, :]
         return mu, var
 
     # ---- kernel helpers (gpmdm.py:311-378, 381-548, 965-991, 1070-1101) ------------
@@ -517,6 +575,10 @@ class GPMDM:
         Torch fp64 on the model's device, class blocks only (not on the per-frame path)."""
         if self.dyn_back_step != 1:
             raise NotImplementedError("dyn_back_step=2 models are not supported (as in the reference filter)")
+        with torch.no_grad():       # a read-out, like the library's maps (no autograd graph)
+            return self._map_x_dynamics(Xstar, flg_noise)
+
+    def _map_x_dynamics(self, Xstar, flg_noise):
         dev = self.device
         xs = torch.as_tensor(Xstar, dtype=torch.float64)
         out_dev = xs.device
@@ -536,7 +598,7 @@ class GPMDM:
             quad = quad + torch.sum((ks.T @ A) * ks.T, dim=1)
             o += n
         vc = self.get_x_diag_kernel(xs, flg_noise) - quad
-        lam = torch.exp(self.x_log_lambdas.to(dev)) ** -2
+        lam = torch.exp(self._host("x_log_lambdas").to(dev)) ** -2
         return mean.to(out_dev), (vc[:, None] * lam[None, :]).to(out_dev)
 
     # ---- map read-outs used by train_gpmdm.ipynb (gpmdm.py:1103-1273) -------------
@@ -558,7 +620,7 @@ class GPMDM:
         """gpmdm.py:1147-1196: class c's dynamics GP on every Xin row (all classes' rows,
         as the reference does) -> (mean, var, Xout, Xin, NMSE) as numpy arrays."""
         with torch.no_grad():
-            Xin, Xout, _ = self.get_Xin_Xout_matrices()
+            Xin, Xout, _ = self.get_Xin_Xout_matrices(X=self._host("X"))
             mu, var = self.map_x_dynamics_for_class(Xin, class_index, flg_noise=flg_noise)
             mu, var, Xout, Xin = _to_np(mu), _to_np(var), _to_np(Xout), _to_np(Xin)
         return mu, var, Xout, Xin, self._nmse(Xout, mu, var)
@@ -567,7 +629,7 @@ class GPMDM:
         """gpmdm.py:1199-1239: the observation GP at the training latents ->
         (mean, var, Y, NMSE) as numpy arrays."""
         with torch.no_grad():
-            mu, var = self.map_x_to_y(self.X, flg_noise=flg_noise)
+            mu, var = self.map_x_to_y(self._host("X"), flg_noise=flg_noise)
             mu, var = _to_np(mu), _to_np(var)
             Y = self.get_Y() + self.meanY
         return mu, var, Y, self._nmse(Y, mu, var)
@@ -575,7 +637,7 @@ class GPMDM:
     def get_latent_map_performance_for_class(self, class_index: int, flg_noise: bool = False):
         """gpmdm.py:1241-1273: as get_latent_map_performance on class c's latents."""
         with torch.no_grad():
-            mu, var = self.map_x_to_y(self.get_X_for_class(class_index), flg_noise=flg_noise)
+            mu, var = self.map_x_to_y(self.get_X_for_class(class_index).detach(), flg_noise=flg_noise)
             mu, var = _to_np(mu), _to_np(var)
             Y = self.get_Y_for_class(class_index) + self.meanY
         return mu, var, Y, self._nmse(Y, mu, var)
@@ -586,49 +648,33 @@ class GPMDM:
             "D": self.D, "d": self.d, "n_classes": self.n_classes,
             "dyn_target": self.dyn_target, "dyn_back_step": self.dyn_back_step,
             "sigma_n_num_X": self.sigma_n_num_X, "sigma_n_num_Y": self.sigma_n_num_Y,
-            "y_lengthscales_init": torch.exp(self.y_log_lengthscales).tolist(),
-            "y_lambdas_init": torch.exp(self.y_log_lambdas).tolist(),
-            "y_sigma_n_init": float(torch.exp(self.y_log_sigma_n)),
-            "x_lengthscales_init": torch.exp(self.x_log_lengthscales).tolist(),
-            "x_lambdas_init": torch.exp(self.x_log_lambdas).tolist(),
-            "x_sigma_n_init": float(torch.exp(self.x_log_sigma_n)),
-            "x_lin_coeff_init": torch.exp(self.x_log_lin_coeff).tolist(),
+            "y_lengthscales_init": torch.exp(self._host("y_log_lengthscales")).tolist(),
+            "y_lambdas_init": torch.exp(self._host("y_log_lambdas")).tolist(),
+            "y_sigma_n_init": float(torch.exp(self._host("y_log_sigma_n"))),
+            "x_lengthscales_init": torch.exp(self._host("x_log_lengthscales")).tolist(),
+            "x_lambdas_init": torch.exp(self._host("x_log_lambdas")).tolist(),
+            "x_sigma_n_init": float(torch.exp(self._host("x_log_sigma_n"))),
+            "x_lin_coeff_init": torch.exp(self._host("x_log_lin_coeff")).tolist(),
         }
 
-    # ---- torch.nn.Module-style parameter access (the reference class is an nn.Module whose
-    # parameters are registered in this order, gpmdm.py:201-230, 773) ----------------------
-    _PARAMS = ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n", "x_log_lengthscales",
-               "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff", "X")
-
-    def named_parameters(self):
-        for k in self._PARAMS:
-            if getattr(self, k, None) is not None:
-                yield k, getattr(self, k)
-
-    def parameters(self):
-        for _, v in self.named_parameters():
-            yield v
-
-    def state_dict(self):
-        """The reference's state_dict keys (as ``GPMDM.save`` stores them), float64 copies."""
-        import collections
-        return collections.OrderedDict((k, v.detach().clone()) for k, v in self.named_parameters())
-
-    def load_state_dict(self, state_dict, strict: bool = True):
-        """Install parameters by the reference's names; the device model is rebuilt (and
-        filters built on this model rebind on their next call)."""
+    # ---- torch.nn.Module parameter access: state_dict / parameters / named_parameters come
+    # from nn.Module (registration order = the reference's, gpmdm.py:201-230, 773) -----------
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        """nn.Module.load_state_dict by the reference's names (gpmdm.py:1402), then the device
+        model is rebuilt (filters built on this model rebind on their next call).  A model
+        without latents yet takes X's shape from the state dict."""
+        if self.X is None and "X" in state_dict:
+            self._set_param("X", state_dict["X"])
         missing = [k for k in self._PARAMS if k not in state_dict]
         unexpected = [k for k in state_dict if k not in self._PARAMS]
         if strict and (missing or unexpected):
             raise RuntimeError(f"load_state_dict: missing keys {missing}, unexpected keys {unexpected}")
-        for k in self._PARAMS[:-1]:
+        for k in self._PARAMS:
             if k in state_dict:
-                setattr(self, k, torch.as_tensor(_to_np(state_dict[k]), dtype=torch.float64).reshape(
-                    getattr(self, k).shape).clone())
-        if "X" in state_dict:
-            self.set_latents(state_dict["X"])
-        elif self.X is not None:
+                self._set_param(k, torch.as_tensor(_to_np(state_dict[k])).reshape(getattr(self, k).shape))
+        if self.X is not None:
             self._precompute_kernel_inverses()
+        return torch.nn.modules.module._IncompatibleKeys(missing, unexpected)
 
     def save(self, file_path) -> None:
         """gpmdm.py:1307-1346.  Writes exactly ``file_path``:
@@ -665,13 +711,12 @@ class GPMDM:
         }
 
     def _save_reference_layout(self, file_path):
-        sd = self.state_dict()
-        sd._metadata = {"": {"version": 1}}   # what nn.Module.state_dict attaches (and pickles)
+        sd = self.state_dict()                 # nn.Module's: detached tensors + _metadata
         with open(file_path, "wb") as fh:     # a file object: torch.save adds no suffix
             torch.save({"state_dict": sd, "config_dict": self._reference_config_dict()}, fh)
 
     def _save_npz(self, file_path):
-        arrays = {"X": self.X.numpy()}
+        arrays = {"X": self._host("X").numpy()}
         seq_len = []
         for c, cls in enumerate(self.class_aware_observations_list):
             for k, y in enumerate(cls):
@@ -680,7 +725,7 @@ class GPMDM:
         arrays["n_seq"] = np.asarray(seq_len, dtype=np.int64)
         for k in ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n", "x_log_lengthscales",
                   "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff"):
-            arrays[k] = getattr(self, k).numpy()
+            arrays[k] = self._host(k).numpy()
         cfg = self.config_dict()
         arrays["cfg_int"] = np.asarray([cfg["D"], cfg["d"], cfg["n_classes"], cfg["dyn_back_step"]], dtype=np.int64)
         arrays["cfg_target"] = np.asarray([0 if cfg["dyn_target"] == "full" else 1], dtype=np.int64)
@@ -721,7 +766,7 @@ class GPMDM:
                     x_lin_coeff_init=np.exp(f["x_log_lin_coeff"]),
                     sigma_n_num_X=float(f["cfg_num"][0]), sigma_n_num_Y=float(f["cfg_num"][1]), device=device)
             for k in names:   # exact log-parameters (exp/log round trips can move an ulp)
-                setattr(m, k, torch.as_tensor(np.asarray(f[k], dtype=np.float64)))
+                m._set_param(k, np.asarray(f[k], dtype=np.float64))
             for c in range(C):
                 for k in range(int(f["n_seq"][c])):
                     m.add_data(f[f"obs_{c}_{k}"], c)
@@ -736,7 +781,7 @@ class GPMDM:
                     sigma_n_num_X=cfg["sigma_n_num_X"], sigma_n_num_Y=cfg["sigma_n_num_Y"], device=device)
             m.class_aware_observations_list = [list(c) for c in cfg["class_aware_observations_list"]]
             for k in names:
-                setattr(m, k, sd[k].to(torch.float64).detach().clone())
+                m._set_param(k, sd[k].to(torch.float64))
             X = sd["X"]
         if flg_print:
             for k in names:
@@ -744,7 +789,7 @@ class GPMDM:
         if upload:
             m.set_latents(X)
         else:
-            m.X = torch.as_tensor(_to_np(X), dtype=torch.float64).clone()
+            m._set_param("X", X)
         return m
 
     @classmethod
@@ -761,13 +806,13 @@ class GPMDM:
                 x_lin_coeff_init=np.exp(x_log_lin_coeff), sigma_n_num_X=sigma_n_num_X,
                 sigma_n_num_Y=sigma_n_num_Y, device=device)
         # keep the exact log parameters (exp/log round trips can move an ulp)
-        m.y_log_lengthscales = torch.as_tensor(np.asarray(y_log_lengthscales, dtype=np.float64))
-        m.y_log_lambdas = torch.as_tensor(np.asarray(y_log_lambdas, dtype=np.float64))
-        m.y_log_sigma_n = torch.as_tensor(float(y_log_sigma_n), dtype=torch.float64)
-        m.x_log_lengthscales = torch.as_tensor(np.asarray(x_log_lengthscales, dtype=np.float64))
-        m.x_log_lambdas = torch.as_tensor(np.asarray(x_log_lambdas, dtype=np.float64))
-        m.x_log_sigma_n = torch.as_tensor(float(x_log_sigma_n), dtype=torch.float64)
-        m.x_log_lin_coeff = torch.as_tensor(np.asarray(x_log_lin_coeff, dtype=np.float64))
+        m._set_param("y_log_lengthscales", np.asarray(y_log_lengthscales, dtype=np.float64))
+        m._set_param("y_log_lambdas", np.asarray(y_log_lambdas, dtype=np.float64))
+        m._set_param("y_log_sigma_n", np.float64(y_log_sigma_n))
+        m._set_param("x_log_lengthscales", np.asarray(x_log_lengthscales, dtype=np.float64))
+        m._set_param("x_log_lambdas", np.asarray(x_log_lambdas, dtype=np.float64))
+        m._set_param("x_log_sigma_n", np.float64(x_log_sigma_n))
+        m._set_param("x_log_lin_coeff", np.asarray(x_log_lin_coeff, dtype=np.float64))
         for c, seqs in enumerate(Y_sequences):
             for y in seqs:
                 m.add_data(np.asarray(y), c)

@@ -148,6 +148,7 @@ class GPMDM_PF:
         """The reference filter reads its GPMDM's current state on every call
         (gpmdm_pf.py:164, 183): after the model was rebuilt (set_latents, train_adam,
         a reload into the same object) rebind the device filter to the new image."""
+        self._gpmdm._refresh()                  # parameters changed in place (an optimiser step)?
         if self._gpmdm.generation != self._model_gen:
             _lib.check(_lib.load().gpmdm_pf_set_model(self._h, self._gpmdm.handle), "rebind to the rebuilt model")
             self._model_gen = self._gpmdm.generation
@@ -163,7 +164,7 @@ class GPMDM_PF:
         counts = self._divide_into_n_parts(self._num_particles, self.num_classes)
         sizes = [self._gpmdm.get_X_for_class(c).shape[0] for c in range(self.num_classes)]
         idx = replay.init_draws(sizes, counts)
-        states = np.concatenate([self._gpmdm.get_X_for_class(c).numpy()[idx[c]] for c in range(self.num_classes)], 0)
+        states = np.concatenate([self._gpmdm.get_X_for_class(c).detach().cpu().numpy()[idx[c]] for c in range(self.num_classes)], 0)
         classes = np.concatenate([np.full(counts[c], c, dtype=np.int64) for c in range(self.num_classes)])
         states = np.ascontiguousarray(states, dtype=np.float64)
         if self._collective:                    # one replicated filter: rank 0's particles

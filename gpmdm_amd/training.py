@@ -175,7 +175,7 @@ class Trainer:
         m = self.model
         with torch.no_grad():
             for n in PARAM_NAMES:
-                setattr(m, n, self.p[n].detach().to("cpu").clone())
+                m._set_param(n, self.p[n].detach().to("cpu"))
 
 
 def train_adam(model, num_opt_steps, num_print_steps=0, lr=0.01, balance=1.0):

@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 
 def _write_input(path, m, T, st, Z, P, seed, resample):
     C, d, D = m.n_classes, m.d, m.D
-    X = m.X.numpy()
+    X = m.X.detach().numpy()
     Y = np.asarray(m.get_Y(), dtype=np.float64)
     Xin, Xout, _ = m.get_Xin_Xout_matrices(X=m.X)
     Nc = np.asarray(m._class_dynamics_rows(), dtype=np.int64)
@@ -32,9 +32,9 @@ def _write_input(path, m, T, st, Z, P, seed, resample):
         fh.write(struct.pack("<8q", X.shape[0], D, d, C, P, Z.shape[0], seed, resample))
         fh.write(Nc.tobytes())
         for a in (X, Y, np.asarray(Xin), np.asarray(Xout),
-                  torch.exp(m.y_log_lengthscales).numpy(), (torch.exp(m.y_log_lambdas) ** -2).numpy(),
-                  torch.exp(m.x_log_lengthscales).numpy(), (torch.exp(m.x_log_lin_coeff) ** 2).numpy(),
-                  (torch.exp(m.x_log_lambdas) ** -2).numpy(),
+                  torch.exp(m.y_log_lengthscales).detach().numpy(), (torch.exp(m.y_log_lambdas) ** -2).detach().numpy(),
+                  torch.exp(m.x_log_lengthscales).detach().numpy(), (torch.exp(m.x_log_lin_coeff) ** 2).detach().numpy(),
+                  (torch.exp(m.x_log_lambdas) ** -2).detach().numpy(),
                   [sy2, m.sigma_n_num_Y ** 2, sx2, m.sigma_n_num_X ** 2], T, st["states"]):
             fh.write(f64(a))
         fh.write(np.ascontiguousarray(st["classes"], dtype=np.int64).tobytes())

@@ -44,10 +44,10 @@ def _synthetic(cfg):
         for y in data.sequences[k]:
             m.add_data(y, k)
     m.init_X()
-    lp = {k: (getattr(m, k).numpy() if getattr(m, k).dim() else float(getattr(m, k)))
+    lp = {k: (getattr(m, k).detach().numpy() if getattr(m, k).dim() else float(getattr(m, k)))
           for k in ("y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n", "x_log_lengthscales",
                     "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff")}
-    om = O.OracleModel(X=m.X.numpy().copy(), Y=m.get_Y().astype(np.float64),
+    om = O.OracleModel(X=m.X.detach().numpy().copy(), Y=m.get_Y().astype(np.float64),
                        seq_lengths=[[c["L"]] * c["S"]] * c["C"], **lp).precompute("cholesky")
     return m, om, data, c
 
@@ -61,7 +61,7 @@ def test_large_config_maps_and_step_vs_oracle(cfg):
     C, d = c["C"], c["d"]
     assert m.X.shape[0] == C * c["S"] * c["L"]
     rng = np.random.RandomState(100 + cfg)
-    X = m.X.numpy()
+    X = m.X.detach().numpy()
     xs = X[rng.randint(0, X.shape[0], 500)] + 0.05 * rng.randn(500, d)
     mu, var = m.map_x_to_y(torch.tensor(xs))
     omu, ovar = om.map_x_to_y(xs)

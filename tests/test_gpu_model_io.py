@@ -150,3 +150,29 @@ def test_notebook_train_save_load_filter_chain(tmp_path):
     l2, p2, s2 = run(loaded)
     assert l1 == l2 and np.array_equal(p1, p2) and torch.equal(s1, s2)
     assert np.all(np.isfinite(p1)) and np.allclose(p1.sum(1), 1.0)
+
+
+def test_external_optimizer_step_rebuilds_device_model():
+    """An optimiser over GPMDM.parameters() on the reference's loss (gpdm_loss, gpmdm.py:
+    721-760, differentiable through the model's parameters): after opt.step() the next use
+    rebuilds the device model from the new parameters -- the maps equal those of a model
+    freshly loaded from the updated state_dict, and a filter built before the step rebinds."""
+    from gpmdm_amd import GPMDM, GPMDM_PF, synthetic
+    m = GPMDM.load(GOLDEN / "ref_checkpoint_config1.pth")
+    pf = GPMDM_PF(m, torch.tensor(synthetic.markov_matrix(2)), 500, rng="philox", seed=2)
+    m.set_training_mode("all")
+    gen0 = m.generation
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    loss = m.gpdm_loss(m.get_Y(), m.X.shape[0])
+    loss.backward()
+    assert m.X.grad is not None and torch.isfinite(m.X.grad).all()
+    opt.step()
+    xs = torch.tensor(np.random.RandomState(1).randn(40, 3))
+    mu, var = m.map_x_to_y(xs)                   # triggers the rebuild
+    assert m.generation == gen0 + 1
+    fresh = GPMDM.load(GOLDEN / "ref_checkpoint_config1.pth")
+    fresh.load_state_dict(m.state_dict())
+    mu2, var2 = fresh.map_x_to_y(xs)
+    assert torch.equal(mu, mu2) and torch.equal(var, var2)
+    pf.update(np.zeros(m.D))                     # rebinds to the rebuilt model
+    assert pf._model_gen == m.generation

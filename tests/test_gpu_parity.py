@@ -176,7 +176,7 @@ def test_full_size_obs_vs_oracle_subset(m2):
     f = load_fixture("config2_n2000_p1000")
     om = oracle_model(f)
     rng = np.random.RandomState(1)
-    X = m2.X.numpy()
+    X = m2.X.detach().numpy()
     xs = X[rng.randint(0, X.shape[0], 100_000)] + 0.1 * rng.randn(100_000, X.shape[1])
     mu, var = m2.map_x_to_y(torch.tensor(xs))
     sel = rng.choice(100_000, 1000, replace=False)

@@ -28,7 +28,7 @@ def test_filter_survives_model_rebuild(fx_config1):
     torch.manual_seed(1)
     pf.update(f["z"][0])
     old_gen = m.generation
-    m.set_latents(m.X.numpy() * 1.01)          # destroys the old handle, uploads a new model
+    m.set_latents(m.X.detach().numpy() * 1.01)          # destroys the old handle, uploads a new model
     assert m.generation == old_gen + 1
     st0 = pf.export_state()
     rng = np.random.RandomState(2)
@@ -91,7 +91,7 @@ def test_predictive_maps_on_concurrent_streams(fx_config2):
     results equal the one-stream results bitwise (VERDICT r01 weak #10)."""
     m = product_model(fx_config2)
     rng = np.random.RandomState(5)
-    X = m.X.numpy()
+    X = m.X.detach().numpy()
     xa = torch.tensor(X[rng.randint(0, X.shape[0], 20_000)] + 0.1 * rng.randn(20_000, m.d)).cuda()
     xb = torch.tensor(X[rng.randint(0, X.shape[0], 7_000)] + 0.1 * rng.randn(7_000, m.d)).cuda()
     ref = [m.map_x_to_y(xa), m.map_x_to_y(xb), m.map_x_dynamics_for_class(xa, 0), m.map_x_dynamics_for_class(xb, 1)]

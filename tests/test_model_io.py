@@ -63,9 +63,9 @@ def test_reference_written_checkpoint_loads(tmp_path):
     from conftest import GOLDEN
     f = np.load(GOLDEN / "ref_checkpoint_config1.npz", allow_pickle=False)
     m = GPMDM.load(GOLDEN / "ref_checkpoint_config1.pth", upload=False)
-    assert np.array_equal(m.X.numpy(), f["X"])
+    assert np.array_equal(m.X.detach().numpy(), f["X"])
     for k in ("y_log_lengthscales", "y_log_lambdas", "x_log_lengthscales", "x_log_lambdas", "x_log_lin_coeff"):
-        assert np.array_equal(getattr(m, k).numpy(), f[k]), k
+        assert np.array_equal(getattr(m, k).detach().numpy(), f[k]), k
     for k in ("y_log_sigma_n", "x_log_sigma_n"):
         assert float(getattr(m, k)) == float(f[k]), k
     assert np.array_equal(m.get_Y(), f["Y"])
@@ -74,7 +74,7 @@ def test_reference_written_checkpoint_loads(tmp_path):
     q = tmp_path / "m.npz"
     m.save(q)
     m2 = GPMDM.load(q, upload=False)
-    assert np.array_equal(m2.X.numpy(), f["X"]) and np.array_equal(m2.get_Y(), f["Y"])
+    assert np.array_equal(m2.X.detach().numpy(), f["X"]) and np.array_equal(m2.get_Y(), f["Y"])
 
 
 def test_kernel_helpers_match_reference():
@@ -87,7 +87,7 @@ def test_kernel_helpers_match_reference():
     m = GPMDM.load(golden / "ref_checkpoint_config1.pth", upload=False)
     Xin, _, _ = m.get_Xin_Xout_matrices()
     xq = torch.tensor(g["alldyn_xs"])
-    close = lambda a, b: np.testing.assert_allclose(a.numpy(), b, rtol=1e-12, atol=1e-13)
+    close = lambda a, b: np.testing.assert_allclose(a.detach().numpy(), b, rtol=1e-12, atol=1e-13)
     close(m.get_x_kernel(Xin[:7], Xin[3:10]), g["k_x_noise"])
     close(m.get_x_kernel(Xin[:7], xq[:4], False), g["k_x"])
     close(m.get_y_kernel(m.X[:6], m.X[2:8]), g["k_y_noise"])
@@ -181,3 +181,41 @@ def test_pth_layout_matches_reference_written_file(tmp_path):
               "x_lambdas_init", "x_sigma_n_init", "x_lin_coeff_init", "dtype", "D", "d", "n_classes",
               "dyn_target", "dyn_back_step", "sigma_n_num_X", "sigma_n_num_Y"):
         assert cfg_o[k] == cfg_r[k], k
+
+
+def test_gpmdm_is_an_nn_module_with_the_reference_parameters():
+    """GPMDM is a torch.nn.Module like the reference's (gpmdm.py:18): nn.Parameters in the
+    reference's registration order, requires_grad from the flg_train_* flags and from
+    set_training_mode / set_evaluation_mode (gpmdm.py:239-279), train()/eval(), and
+    parameter versions that tell the model its device factors are stale after an in-place
+    update (an optimiser step)."""
+    from conftest import GOLDEN
+    m = GPMDM.load(GOLDEN / "ref_checkpoint_config1.pth", upload=False)
+    assert isinstance(m, torch.nn.Module)
+    names = [n for n, _ in m.named_parameters()]
+    assert names == ["y_log_lengthscales", "y_log_lambdas", "y_log_sigma_n", "x_log_lengthscales",
+                     "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff", "X"]
+    assert all(isinstance(p, torch.nn.Parameter) and p.requires_grad for p in m.parameters())
+    m.set_training_mode("latent")
+    assert m.y_log_lambdas.requires_grad and not m.x_log_lambdas.requires_grad and m.X.requires_grad
+    m.set_training_mode("dynamics")
+    assert not m.y_log_lambdas.requires_grad and m.x_log_lin_coeff.requires_grad
+    m.set_evaluation_mode()
+    assert not any(p.requires_grad for p in m.parameters())
+    assert m.eval() is m and not m.training and m.train().training
+    # constructor flags are requires_grad flags
+    m2 = GPMDM(D=4, d=2, n_classes=1, dyn_target="full", dyn_back_step=1, y_lambdas_init=np.ones(4),
+               y_lengthscales_init=np.ones(2), y_sigma_n_init=0.1, x_lambdas_init=np.ones(2),
+               x_lengthscales_init=np.ones(2), x_sigma_n_init=0.1, x_lin_coeff_init=np.ones(3),
+               flg_train_y_lambdas=False, device="cuda:0")
+    assert not m2.y_log_lambdas.requires_grad and m2.y_log_lengthscales.requires_grad
+    assert m2.X is None and "X" not in m2.state_dict()
+    # an optimiser step over parameters() changes the parameter versions the device model
+    # was built from (GPMDM._refresh rebuilds it on the next use)
+    m.set_training_mode("all")
+    before = m._param_versions()
+    opt = torch.optim.SGD(m.parameters(), lr=1e-3)
+    loss = (m.y_log_lambdas ** 2).sum() + (m.X ** 2).sum()
+    loss.backward()
+    opt.step()
+    assert m._param_versions() != before

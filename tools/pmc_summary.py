@@ -34,7 +34,10 @@ def load(root):
 
 def short(name):
     if "k_gp_tile" in name:
-        return "obs_gemm" if "false" in name else "dyn_gemm"
+        if "false" in name:
+            return "obs_gemm"
+        # the dynamics GP's narrow (de-duplicated rows, 16x256: MT 1) and wide images
+        return "dyn_gemm_narrow" if ", 1, 4>" in name else "dyn_gemm"
     return name.split("(")[0].split("::")[-1]
 
 
