@@ -343,17 +343,19 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
     case GPMDM_TILE_32x512: obs_geo = kGeo32x512; break;
     default: break;   // rejected by check_model_desc
   }
-  // A/B override of the dynamics shapes ("nw,mt,ntw"; d <= 8): 16x256 (4,1,4), 16x512
-  // (4,1,8), 32x256 (4,2,4), 32x512 (4,2,8), 32x1024 (8,2,8), 64x256 (4,4,4), 64x512 (8,4,4)
+  // A/B override of the dynamics shapes ("nw,mt,ntw"; the extra ones need d <= 8): 16x256
+  // (4,1,4), 16x512 (4,1,8), 16x1024 (4,1,16), 32x256 (4,2,4), 32x512 (4,2,8),
+  // 32x1024 (8,2,8), 64x256 (4,4,4), 64x512 (8,4,4)
   auto geo_env = [&](const char* name, TileGeo& g) -> bool {
     const char* v = std::getenv(name);
     if (!v) return true;
     TileGeo t{};
     if (std::sscanf(v, "%d,%d,%d", &t.nw, &t.mt, &t.ntw) != 3) return false;
-    const TileGeo ok[] = {kGeo16x256, {4, 1, 8}, kGeo32x256, kGeo32x512, {8, 2, 8}, kGeo64x256, kGeo64x512};
+    const TileGeo ok[] = {kGeo16x256, {4, 1, 8}, {4, 1, 16}, kGeo32x256, kGeo32x512, {8, 2, 8},
+                          kGeo64x256, kGeo64x512};
     for (const TileGeo& o : ok) {
       if (o.nw != t.nw || o.mt != t.mt || o.ntw != t.ntw) continue;
-      const bool ab_only = (t.nw == 8 && t.mt == 2) || (t.mt == 1 && t.ntw == 8);   // launch_d: d <= 8
+      const bool ab_only = (t.nw == 8 && t.mt <= 2) || (t.mt == 1 && t.ntw >= 8);   // launch_d: d <= 8
       if (ab_only && d > 8) return false;
       g = t;
       return true;
@@ -724,12 +726,11 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   const std::vector<unsigned long long> neg(pf->F, 0x000fffffffffffffull);   // ord_enc(-inf)
   HIPCHK(hipMemcpy(pf->gmax, neg.data(), sizeof(unsigned long long) * pf->F, hipMemcpyHostToDevice));
   // read-outs of the initial state: ll = log_w = 0, w = 1/P (gpmdm_pf.py:102-104)
-  launch_normalise(norm_args(pf), nullptr);
   ResampleArgs ra = resample_args(pf);
   ra.identity = 1;
   ra.cls_src = pf->cls;
   ra.X_src = pf->X;
-  launch_resample(ra, nullptr);
+  launch_normalise_resample(norm_args(pf), ra, nullptr);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   pf->initialised = true;
@@ -751,8 +752,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   }
   hipEvent_t t0;
   pf->mark_begin(s, GPMDM_STAGE_SWITCH, t0);
-  if (pf->dedup && pf->nloc > 0)
-    HIPCHK(hipMemsetAsync(pf->owner, 0xff, sizeof(unsigned) * C * pf->P, s));
+  // (the owner preset of the leader election is launch_switch_group's)
   // Multi-rank Philox filters switch and group only their own slice (the classes of the
   // other particles arrive with the all-gather); otherwise all P (replay draws are indexed
   // by the global class grouping).
@@ -782,7 +782,6 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
     sa.hi = pf->hi;
   }
   sa.own = pf->own_order();
-  launch_switch(sa, s);
   ScanArgs sc{};
   sc.nb = nbs;
   sc.C = C;
@@ -800,7 +799,6 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   sc.seg_pos_end = pf->seg_end();
   sc.seg_out_base = pf->seg_out();
   sc.seg_tile_start = pf->seg_tiles();
-  launch_scan_counts(sc, s);
   GroupArgs ga{};
   ga.P = pf->P;
   ga.base = base;
@@ -811,9 +809,8 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   ga.blockoff = pf->blockoff;
   ga.own = pf->own_order();
   ga.perm = pf->perm;
-  launch_group(ga, s);
+  LeadArgs la{};
   if (pf->dedup && pf->nloc > 0) {
-    LeadArgs la{};
     la.P = pf->P;
     la.Pf = pf->Pf;
     la.lo = pf->lo;
@@ -836,8 +833,8 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
     la.lseg_tile_start = pf->lseg_tiles();
     la.lperm = pf->lperm;
     la.slot = pf->slot;
-    launch_lead(la, s);
   }
+  launch_switch_group(sa, sc, ga, sa.owner ? &la : nullptr, s);
   pf->mark_end(s, GPMDM_STAGE_SWITCH, t0);
   HIPCHK(hipGetLastError());
   if (class_counts) {
@@ -1236,10 +1233,9 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   }
   hipEvent_t t0;
   pf->mark_begin(s, GPMDM_STAGE_RESAMPLE, t0);
-  launch_normalise(norm_args(pf), s);
   ResampleArgs ra = resample_args(pf);
   ra.U = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->U : nullptr;
-  launch_resample(ra, s);
+  launch_normalise_resample(norm_args(pf), ra, s);
   // next frame's ownership order (identical on every rank: same replicated ancestors)
   pf->own_valid = false;
   if (pf->own && pf->dedup && pf->shard_order) {

@@ -564,7 +564,7 @@ void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
   constexpr int kCoordVar = DI > 12 ? kTileCoordLDS : 0;
   if (dyn) {
     // A/B shapes for the dynamics GPs (GPMDM_DYN_GEO / GPMDM_DYNW_GEO, capi.hip; d <= 8):
-    // 32 x 1024 (8 waves) and 16 x 512
+    // 32 x 1024 (8 waves), 16 x 512, 16 x 1024 (4 waves x 16 column tiles)
     if constexpr (DI <= 8) {
       if (g.nw == 8 && g.mt == 2) {
         hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 8, 2, 8>), grid, dim3(512), 0, stream, p);
@@ -572,6 +572,10 @@ void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
       }
       if (g.nw == 4 && g.mt == 1 && g.ntw == 8) {
         hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 1, 8>), grid, dim3(256), 0, stream, p);
+        return;
+      }
+      if (g.nw == 4 && g.mt == 1 && g.ntw == 16) {
+        hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 1, 16>), grid, dim3(256), 0, stream, p);
         return;
       }
     }

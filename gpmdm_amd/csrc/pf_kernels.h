@@ -228,6 +228,9 @@ void launch_dyn_finish(const DynFinishArgs& a, hipStream_t s);
 void launch_obs_finish(const ObsFinishArgs& a, hipStream_t s);
 void launch_normalise(const NormArgs& a, hipStream_t s);
 void launch_resample(const ResampleArgs& a, hipStream_t s);
+void launch_normalise_resample(const NormArgs& na, const ResampleArgs& ra, hipStream_t s);
+void launch_switch_group(const SwitchArgs& sa, const ScanArgs& sc, const GroupArgs& ga, const LeadArgs* la,
+                         hipStream_t s);
 void launch_pack(const PackArgs& a, hipStream_t s);
 // predict(): per-block class histogram of `cls` (blockcounts nb x C, nb = ceil(P / 256))
 // single-segment tile table {0, n, 0, 0, tiles} at t[0..4] (predictive maps)

@@ -11,6 +11,8 @@
 //                   and the read-out partial sums            gpmdm_pf.py:224-262, 302-312
 //   k_readout       read-out totals
 // All arithmetic is fp64; every reduction has a fixed order (bitwise run-to-run repeatable).
+#include <cstdlib>
+
 #include "common.h"
 #include "pf_kernels.h"
 
@@ -87,7 +89,8 @@ __global__ __launch_bounds__(kB) void k_switch(SwitchArgs a) {
 // ---------------------------------------------------------------------------------
 // One workgroup: exclusive scans of the per-block class counts, class starts, and the
 // segments (grouped position ranges) of this rank's particle slice [lo, hi).
-__global__ __launch_bounds__(1024) void k_scan_counts(ScanArgs a) {
+// (a device function: k_small_switch runs the same body inside its workgroup)
+__device__ __forceinline__ void scan_counts_body(const ScanArgs& a) {
   __shared__ int part[1024];
   __shared__ int tot[kMaxClasses];
   __shared__ int lo_cnt[kMaxClasses], hi_cnt[kMaxClasses];
@@ -156,6 +159,7 @@ __global__ __launch_bounds__(1024) void k_scan_counts(ScanArgs a) {
     a.seg_tile_start[a.C] = ts;
   }
 }
+__global__ __launch_bounds__(1024) void k_scan_counts(ScanArgs a) { scan_counts_body(a); }
 
 // ---------------------------------------------------------------------------------
 template <bool OWN>
@@ -218,7 +222,7 @@ __global__ __launch_bounds__(kB) void k_lead_flags(LeadArgs a) {
 }
 
 // One workgroup: lblock -> exclusive offsets (in place), then the leader segment tables.
-__global__ __launch_bounds__(1024) void k_lead_tables(LeadArgs a) {
+__device__ __forceinline__ void lead_tables_body(const LeadArgs& a) {
   __shared__ int part[1024];
   __shared__ int total;
   const int tid = threadIdx.x;
@@ -262,6 +266,7 @@ __global__ __launch_bounds__(1024) void k_lead_tables(LeadArgs a) {
     a.lseg_tile_start[a.C] = ts;
   }
 }
+__global__ __launch_bounds__(1024) void k_lead_tables(LeadArgs a) { lead_tables_body(a); }
 
 __global__ __launch_bounds__(kB) void k_lead_compact(LeadArgs a) {
   const long long pos = (long long)blockIdx.x * kB + threadIdx.x;
@@ -273,6 +278,119 @@ __global__ __launch_bounds__(kB) void k_lead_compact(LeadArgs a) {
   const long long f = p / a.Pf;
   a.lperm[r] = (int)p;
   a.slot[(long long)a.cls_new[p] * a.P + f * a.Pf + a.anc[p]] = r;
+}
+
+
+// ---------------------------------------------------------------------------------
+// Small single-shard filters (all P <= kSmallSwitchP particles switched by one rank, no
+// ownership order): one 1024-thread workgroup runs the switch, the class scan, the grouping
+// and the leader compaction in one launch instead of seven (with the owner preset).  Every
+// step is integer and deterministic (the leader of a key is its smallest particle index,
+// whatever the order of the atomics), the 256-thread blocks of k_switch / k_group /
+// k_lead_* are the workgroup's quarters and the one-workgroup kernels run as they are, so
+// every table is the multi-kernel path's exactly (tests/test_gpu_small_path.py).
+constexpr long long kSmallSwitchP = 1024;
+
+__global__ __launch_bounds__(1024) void k_small_switch(SwitchArgs sa, ScanArgs sc, GroupArgs ga, LeadArgs la,
+                                                       int dedup) {
+  __shared__ int hist[4][kMaxClasses];
+  __shared__ int wcount[4][4][kMaxClasses];
+  __shared__ int wc[4][4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, b = tid >> 8, wq = w & 3;
+  const long long P = sa.P;
+  const int C = sa.C;
+  const int nbs = (int)((P + kB - 1) / kB);
+  if (dedup)
+    for (long long i = tid; i < (long long)C * P; i += 1024) sa.owner[i] = 0xffffffffu;
+  if (tid < 4 * kMaxClasses) hist[tid / kMaxClasses][tid % kMaxClasses] = 0;
+  if (sa.gmax_reset && tid < sa.F) sa.gmax_reset[tid] = ord_enc(-INFINITY);
+  __syncthreads();
+  // ---- k_switch ----
+  const long long p = tid;
+  if (p < P) {
+    const int c0 = sa.cls[p];
+    const long long f = p / sa.Pf;
+    const uint2 key = filter_key(sa.seed_lo, sa.seed_hi, f);
+    const unsigned pl = (unsigned)(p - f * sa.Pf);
+    int best = 0;
+    double bestv = -INFINITY;
+    for (int j = 0; j < C; j += 2) {
+      double e0, e1 = 1.0;
+      if (sa.E) {
+        e0 = sa.E[p * C + j];
+        if (j + 1 < C) e1 = sa.E[p * C + j + 1];
+      } else {
+        const uint4 r = philox4x32_10(make_uint4(pl, sa.frame, kStreamSwitch, (unsigned)(j >> 1)), key);
+        e0 = -log(u01_oo(r.x, r.y));
+        e1 = -log(u01_oo(r.z, r.w));
+      }
+      const double v0 = sa.T[c0 * C + j] / e0;
+      if (v0 > bestv) { bestv = v0; best = j; }
+      if (j + 1 < C) {
+        const double v1 = sa.T[c0 * C + j + 1] / e1;
+        if (v1 > bestv) { bestv = v1; best = j + 1; }
+      }
+    }
+    sa.cls_new[p] = best;
+    atomicAdd(&hist[b][best], 1);
+    if (dedup && p >= sa.lo && p < sa.hi) atomicMin(&sa.owner[(long long)best * P + f * sa.Pf + sa.anc[p]], (unsigned)p);
+  }
+  __syncthreads();
+  if (tid < nbs * C) sa.blockcounts[tid] = hist[tid / C][tid % C];   // block bb, class c: bb * C + c
+  __syncthreads();
+  // ---- k_scan_counts ----
+  scan_counts_body(sc);
+  __syncthreads();
+  // ---- k_group ----
+  {
+    const int c = p < P ? sa.cls_new[p] : -1;
+    int rank = 0;
+    for (int k = 0; k < C; ++k) {
+      const unsigned long long m = __ballot(c == k);
+      if (c == k) rank = __popcll(m & ((1ull << lane) - 1ull));
+      if (lane == 0) wcount[b][wq][k] = __popcll(m);
+    }
+    __syncthreads();
+    if (c >= 0) {
+      int off = ga.class_start[c] + ga.blockoff[(long long)b * C + c];
+      for (int v = 0; v < wq; ++v) off += wcount[b][v][c];
+      ga.perm[off + rank] = (int)p;
+    }
+  }
+  __syncthreads();
+  if (!dedup) return;
+  // ---- k_lead_flags ----
+  {
+    const long long pos = p;
+    const int lf = lead_flag(la, pos);
+    const unsigned long long m = __ballot(lf);
+    const int excl = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wc[b][wq] = __popcll(m);
+    __syncthreads();
+    int base = 0;
+    for (int v = 0; v < wq; ++v) base += wc[b][v];
+    if (pos < la.npos) la.lflag_scan[pos] = ((base + excl) << 1) | lf;
+    if ((tid & (kB - 1)) == 0 && b < la.nb) {
+      int t = 0;
+      for (int v = 0; v < kB / 64; ++v) t += wc[b][v];
+      la.lblock[b] = t;
+    }
+  }
+  __syncthreads();
+  // ---- k_lead_tables ----
+  lead_tables_body(la);
+  __syncthreads();
+  // ---- k_lead_compact ----
+  if (p < la.npos) {
+    const int v = la.lflag_scan[p];
+    if (v & 1) {
+      const long long q = la.perm[p];
+      const int r = la.lblock[b] + (v >> 1);
+      const long long f = q / la.Pf;
+      la.lperm[r] = (int)q;
+      la.slot[(long long)la.cls_new[q] * la.P + f * la.Pf + la.anc[q]] = r;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -720,6 +838,200 @@ __global__ __launch_bounds__(1024) void k_readout(ResampleArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// Small filters (P <= kSmallP per filter, no guide table): one 1024-thread workgroup per
+// filter runs normalise + CDF + resample + read-out in one launch instead of six -- at the
+// notebook's P = 100 each launch of the multi-kernel path costs more than its work.  The
+// arithmetic is the multi-kernel path's, association for association: the 256-thread
+// blocks of k_norm_exp_scan / k_cdf / k_resample are the workgroup's four 256-thread
+// quarters (block b = waves 4b .. 4b+3, so every wave-level scan / sum sees the same lanes),
+// k_norm_total / k_readout run as they are, and intermediates go through the same buffers;
+// the max is exact in any order.  Systematic resampling takes the search form, whose indices
+// the scan form reproduces exactly (k_sys_marks).  Results are bitwise those of the
+// multi-kernel path (tests/test_gpu_small_path.py).
+constexpr long long kSmallP = 1024;
+
+__global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleArgs a) {
+  __shared__ double mx[16];
+  __shared__ double wsum[4][4];
+  __shared__ double part[1024];
+  __shared__ double cum_s[kSmallP];
+  __shared__ double red[4][4][kMaxReadout];
+  __shared__ double rred[8][16];
+  __shared__ double tot[kMaxReadout];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = tid >> 8, wq = w & 3;                 // block of the multi-kernel path, its wave
+  const long long f = blockIdx.x;
+  const long long P = na.P;
+  const int nb = na.nb;
+  const long long p = tid;                            // = b * 256 + (tid & 255)
+  const long long g0 = f * P;
+  // ---- k_norm_max: the largest ll (NaN ignored, as fmax does) ----
+  {
+    double v = p < P ? na.ll[g0 + p] : -INFINITY;
+    v = fmax(-INFINITY, v);
+    v = wave_max(v);
+    if (lane == 0) mx[w] = v;
+    __syncthreads();
+    if (tid == 0) {
+      double m = mx[0];
+      for (int i = 1; i < 16; ++i) m = fmax(m, mx[i]);
+      na.gmax[f] = ord_enc(m);
+    }
+    __syncthreads();
+  }
+  const double M = ord_dec(na.gmax[f]);
+  // ---- k_norm_exp_scan ----
+  const double e = p < P ? exp(na.ll[g0 + p] - M) : 0.0;
+  if (p < P) na.e[g0 + p] = e;
+  {
+    double x = e;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[b][wq] = x;
+    __syncthreads();
+    double base = 0.0;
+    for (int v = 0; v < wq; ++v) base += wsum[b][v];
+    x += base;
+    if (p < P) na.local[g0 + p] = x;
+    if ((tid & 255) == 255 && b < nb) na.blocksum[f * nb + b] = x;
+  }
+  __syncthreads();
+  // ---- k_norm_total ----
+  {
+    const int chunk = (nb + 1023) / 1024;
+    double sv = 0.0;
+    for (int i = 0; i < chunk; ++i) {
+      const int bb = tid * chunk + i;
+      if (bb < nb) sv += na.blocksum[f * nb + bb];
+    }
+    part[tid] = sv;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      const double v = tid >= off ? part[tid - off] : 0.0;
+      __syncthreads();
+      part[tid] += v;
+      __syncthreads();
+    }
+    double run = tid ? part[tid - 1] : 0.0;
+    for (int i = 0; i < chunk; ++i) {
+      const int bb = tid * chunk + i;
+      if (bb < nb) {
+        na.blockoff[f * nb + bb] = run;
+        run += na.blocksum[f * nb + bb];
+      }
+    }
+    if (tid == 1023) na.total[f] = part[1023];
+  }
+  __syncthreads();
+  const double S = na.total[f];
+  // ---- k_cdf ----
+  if (p < P) {
+    const double c = p == P - 1 ? 1.0 : (na.blockoff[f * nb + b] + na.local[g0 + p]) / S;
+    na.cum[g0 + p] = c;
+    cum_s[p] = c;
+  }
+  __syncthreads();
+  // ---- k_resample (slot s = p) ----
+  const uint2 key = filter_key(a.seed_lo, a.seed_hi, f);
+  const int C = a.C, d = a.d, nq = C + 1 + d;
+  const bool act = p < P;
+  long long idx = 0;
+  int cnew = -1;
+  double e2 = 0.0, wv = 0.0;
+  if (act) {
+    if (a.identity) {
+      idx = p;
+    } else {
+      double u;
+      if (a.systematic) {
+        u = sys_u(p, sys_u0(a, f), P);
+      } else if (a.U) {
+        u = a.U[p];
+      } else {
+        const uint4 r = philox4x32_10(make_uint4((unsigned)p, a.frame, kStreamResample, 0u), key);
+        u = u01_co(r.x, r.y);
+      }
+      long long lo = 0, hi = P;
+      while (hi - lo > 0) {
+        const long long mid = lo + (hi - lo) / 2;
+        if (cum_s[mid] < u) lo = mid + 1; else hi = mid;
+      }
+      idx = lo;
+    }
+    cnew = a.cls_src[g0 + idx];
+    if (!a.identity) {
+      a.ridx[g0 + p] = (int)idx;
+      a.cls_dst[g0 + p] = cnew;
+      for (int j = 0; j < d; ++j) a.X_dst[(g0 + p) * d + j] = a.X_src[(g0 + idx) * d + j];
+    }
+    const double llv = a.ll[g0 + p];
+    const double lw = llv - M;
+    e2 = exp((llv + lw) - M);
+    wv = e / S;
+  }
+  for (int k = 0; k < nq; ++k) {
+    double v = 0.0;
+    if (act) {
+      if (k < C) v = (cnew == k) ? e2 : 0.0;
+      else if (k == C) v = e2;
+      else v = a.X_src[(g0 + idx) * d + (k - C - 1)] * wv;
+    }
+    v = wave_sum(v);
+    if (lane == 0) red[b][wq][k] = v;
+  }
+  __syncthreads();
+  if ((tid & 255) < nq && b < nb) {
+    const int k = tid & 255;
+    double t = 0.0;
+    for (int v = 0; v < 4; ++v) t += red[b][v][k];
+    a.partials[(f * nb + b) * nq + k] = t;
+  }
+  __syncthreads();
+  // ---- k_readout ----
+  const double* partials = a.partials + f * nb * nq;
+  double* readout = a.readout + f * (C + d + 1);
+  for (int k0 = 0; k0 < nq; k0 += 8) {
+    double sv[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) sv[kk] = 0.0;
+    for (long long bb = tid; bb < nb; bb += 1024)
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+        if (k0 + kk < nq) sv[kk] += partials[bb * nq + k0 + kk];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) {
+      const double v = wave_sum(sv[kk]);
+      if (lane == 0) rred[kk][w] = v;
+    }
+    __syncthreads();
+    if (tid < 8 && k0 + tid < nq) {
+      double t = 0.0;
+      for (int v = 0; v < 16; ++v) t += rred[tid][v];
+      tot[k0 + tid] = t;
+    }
+    __syncthreads();
+  }
+  const int nro = C + d + 1;
+  if (tid < nro) {
+    double v;
+    if (tid < C) {
+      double cl = 0.0;
+      for (int c = 0; c < C; ++c) cl += tot[c];
+      v = tot[tid] / cl;
+    } else if (tid < C + d) {
+      v = tot[tid + 1];
+    } else {
+      v = tot[C];
+    }
+    readout[tid] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(kB) void k_pack(PackArgs a) {
   const long long r = (long long)blockIdx.x * kB + threadIdx.x;
@@ -831,6 +1143,24 @@ void launch_group(const GroupArgs& a, hipStream_t s) {
   else
     hipLaunchKernelGGL(k_group<false>, dim3(nblk(a.n > 0 ? a.n : 1, kB)), dim3(kB), 0, s, a);
 }
+// switch + class scan + grouping (+ leader compaction with `la`): one launch for a small
+// single-shard filter (k_small_switch, the same tables), the multi-kernel path otherwise.
+// The owner preset of the leader election is part of either path.
+void launch_switch_group(const SwitchArgs& sa, const ScanArgs& sc, const GroupArgs& ga, const LeadArgs* la,
+                         hipStream_t s) {
+  static const bool no_small = std::getenv("GPMDM_NO_SMALL_PATH") != nullptr;
+  if (!no_small && sa.P <= kSmallSwitchP && sa.n == sa.P && sa.base == 0 && !sa.own && sa.n > 0 &&
+      (la == nullptr) == (sa.owner == nullptr) && (la == nullptr || la->npos == sa.P)) {
+    LeadArgs l = la ? *la : LeadArgs{};
+    hipLaunchKernelGGL(k_small_switch, dim3(1), dim3(1024), 0, s, sa, sc, ga, l, la ? 1 : 0);
+    return;
+  }
+  if (la) (void)hipMemsetAsync(sa.owner, 0xff, sizeof(unsigned) * (size_t)sa.C * sa.P, s);
+  launch_switch(sa, s);
+  launch_scan_counts(sc, s);
+  launch_group(ga, s);
+  if (la) launch_lead(*la, s);
+}
 void launch_lead(const LeadArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_lead_flags, dim3((unsigned)a.nb), dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_lead_tables, dim3(1), dim3(1024), 0, s, a);
@@ -864,6 +1194,17 @@ void launch_resample(const ResampleArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_guide, dim3(nblk(a.GB + 3, kB), (unsigned)a.F), dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_resample, dim3(nblk(a.P, kB), (unsigned)a.F), dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_readout, dim3((unsigned)a.F), dim3(1024), 0, s, a);
+}
+// normalise + resample + read-out: one launch for small filters (k_small_resample, bitwise
+// the multi-kernel path), the multi-kernel path otherwise (GPMDM_NO_SMALL_PATH=1 forces it)
+void launch_normalise_resample(const NormArgs& na, const ResampleArgs& ra, hipStream_t s) {
+  static const bool no_small = std::getenv("GPMDM_NO_SMALL_PATH") != nullptr;
+  if (!no_small && na.P <= kSmallP && ra.GB == 0) {
+    hipLaunchKernelGGL(k_small_resample, dim3((unsigned)na.F), dim3(1024), 0, s, na, ra);
+    return;
+  }
+  launch_normalise(na, s);
+  launch_resample(ra, s);
 }
 void launch_pack(const PackArgs& a, hipStream_t s) {
   if (a.n > 0) hipLaunchKernelGGL(k_pack, dim3(nblk(a.n, kB)), dim3(kB), 0, s, a);

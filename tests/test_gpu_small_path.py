@@ -1,0 +1,69 @@
+"""GPU: the one-launch paths of small filters (pf_kernels.hip: k_small_switch -- switch, class
+scan, grouping, leader compaction -- for P <= 1024 particles on one shard, k_small_resample
+-- normalise, resample, read-out -- for P <= 1024 per filter) are bitwise the multi-kernel
+path (GPMDM_NO_SMALL_PATH=1): replay and Philox draws, multinomial and systematic
+resampling, with and without ancestor de-duplication, a bank of filters, several frames.  The environment switch is read once per process, so
+each path runs in its own child process (one at a time)."""
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+CHILD = r'''
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[2]); sys.path.insert(0, sys.argv[2] + "/tests")
+from conftest import load_fixture, product_model
+from gpmdm_amd import GPMDM_PF, GPMDM_PF_Bank
+f = load_fixture("config2_n2000_p1000")
+m = product_model(f)
+T = torch.tensor(np.asarray(f["T"], dtype=np.float64))
+Y = m.get_Y()
+out = {}
+for name, P, rng, res, dd in (("replay100", 100, "torch", "multinomial", True),
+                              ("philox1000", 1000, "philox", "multinomial", True),
+                              ("nodedup1000", 1000, "philox", "multinomial", False),
+                              ("sys777", 777, "philox", "systematic", True),
+                              ("one", 1, "philox", "multinomial", True),
+                              ("big1500", 1500, "philox", "multinomial", True)):
+    torch.manual_seed(3)
+    pf = GPMDM_PF(m, T, P, rng=rng, seed=9 if rng == "philox" else None, resample=res, dedup=dd)
+    for k in range(4):
+        pf.update(Y[50 + 9 * k] + 0.01)
+        out[f"{name}_{k}_post"] = pf.class_probabilities().numpy()
+        out[f"{name}_{k}_mean"] = pf.current_state_mean().numpy()
+        out[f"{name}_{k}_lik"] = np.array([pf.log_likelihood()])
+        out[f"{name}_{k}_rows"] = np.array([pf.dynamics_rows()])
+    st = pf.export_state()
+    for key in ("states", "classes", "ll", "w", "resample_idx"):
+        out[f"{name}_{key}"] = st[key]
+bank = GPMDM_PF_Bank(m, T, 3, 300, seed=5)
+for k in range(3):
+    bank.update(np.stack([Y[10 * i + k] for i in range(3)]))
+out["bank_post"] = bank.class_probabilities().numpy()
+out["bank_states"] = bank.export_state()["states"]
+np.savez(sys.argv[1], **out)
+'''
+
+
+def _run(tmp_path, tag, env_extra):
+    env = dict(os.environ, **env_extra)
+    path = tmp_path / f"{tag}.npz"
+    r = subprocess.run([sys.executable, "-c", CHILD, str(path), str(ROOT)], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return dict(np.load(path))
+
+
+@pytest.mark.timeout(600)
+def test_small_path_is_bitwise_the_multi_kernel_path(tmp_path):
+    fused = _run(tmp_path, "fused", {})
+    multi = _run(tmp_path, "multi", {"GPMDM_NO_SMALL_PATH": "1"})
+    assert fused.keys() == multi.keys()
+    for k in fused:
+        assert np.array_equal(fused[k], multi[k]), k
