@@ -286,33 +286,50 @@ __global__ __launch_bounds__(kB) void k_lead_compact(LeadArgs a) {
 // ownership order): one 1024-thread workgroup runs the switch, the class scan, the grouping
 // and the leader compaction in one launch instead of seven (with the owner preset).  Every
 // step is integer and deterministic (the leader of a key is its smallest particle index,
-// whatever the order of the atomics), the 256-thread blocks of k_switch / k_group /
-// k_lead_* are the workgroup's quarters and the one-workgroup kernels run as they are, so
-// every table is the multi-kernel path's exactly (tests/test_gpu_small_path.py).
+// whatever the order of the atomics; integer sums in any order are equal), the 256-thread
+// blocks of k_switch / k_group / k_lead_* are the workgroup's quarters, and what the
+// multi-kernel path reads back from its buffers is kept in LDS (the buffers are still
+// written for the later stages), so every table is the multi-kernel path's exactly
+// (tests/test_gpu_small_path.py).  The scans over at most four blocks are one thread per
+// class (or one thread) instead of 1024-wide Hillis-Steele passes.
 constexpr long long kSmallSwitchP = 1024;
 
 __global__ __launch_bounds__(1024) void k_small_switch(SwitchArgs sa, ScanArgs sc, GroupArgs ga, LeadArgs la,
                                                        int dedup) {
-  __shared__ int hist[4][kMaxClasses];
+  __shared__ int hist[4][kMaxClasses];        // block counts (blockcounts)
+  __shared__ int boff[4][kMaxClasses];        // block offsets (blockoff)
+  __shared__ int cstart[kMaxClasses];         // class_start
+  __shared__ int lo_cnt[kMaxClasses], hi_cnt[kMaxClasses];
+  __shared__ int segb[kMaxClasses], sege[kMaxClasses], sego[kMaxClasses], segt[kMaxClasses + 1];
+  __shared__ int ctot[kMaxClasses];
+  __shared__ int lsegb[kMaxClasses], lsege[kMaxClasses], lsegt[kMaxClasses + 1];
   __shared__ int wcount[4][4][kMaxClasses];
   __shared__ int wc[4][4];
+  __shared__ int lblk[4];
+  __shared__ int cls_s[kSmallSwitchP];        // cls_new
+  __shared__ int anc_s[kSmallSwitchP];        // anc
+  __shared__ int perm_s[kSmallSwitchP];       // perm
+  __shared__ int lflag_s[kSmallSwitchP];      // lflag_scan
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, b = tid >> 8, wq = w & 3;
   const long long P = sa.P;
   const int C = sa.C;
-  const int nbs = (int)((P + kB - 1) / kB);
+  const int nb = (int)((P + kB - 1) / kB);
   if (dedup)
     for (long long i = tid; i < (long long)C * P; i += 1024) sa.owner[i] = 0xffffffffu;
   if (tid < 4 * kMaxClasses) hist[tid / kMaxClasses][tid % kMaxClasses] = 0;
+  if (tid < kMaxClasses) { lo_cnt[tid] = 0; hi_cnt[tid] = 0; }
   if (sa.gmax_reset && tid < sa.F) sa.gmax_reset[tid] = ord_enc(-INFINITY);
+  __threadfence();                            // the owner preset lands before the atomics
   __syncthreads();
   // ---- k_switch ----
   const long long p = tid;
+  int best = -1;
   if (p < P) {
     const int c0 = sa.cls[p];
     const long long f = p / sa.Pf;
     const uint2 key = filter_key(sa.seed_lo, sa.seed_hi, f);
     const unsigned pl = (unsigned)(p - f * sa.Pf);
-    int best = 0;
+    best = 0;
     double bestv = -INFINITY;
     for (int j = 0; j < C; j += 2) {
       double e0, e1 = 1.0;
@@ -332,18 +349,71 @@ __global__ __launch_bounds__(1024) void k_small_switch(SwitchArgs sa, ScanArgs s
       }
     }
     sa.cls_new[p] = best;
+    cls_s[p] = best;
     atomicAdd(&hist[b][best], 1);
-    if (dedup && p >= sa.lo && p < sa.hi) atomicMin(&sa.owner[(long long)best * P + f * sa.Pf + sa.anc[p]], (unsigned)p);
+    if (dedup) {
+      const int an = sa.anc[p];
+      anc_s[p] = an;
+      if (p >= sa.lo && p < sa.hi) atomicMin(&sa.owner[(long long)best * P + f * sa.Pf + an], (unsigned)p);
+    }
   }
   __syncthreads();
-  if (tid < nbs * C) sa.blockcounts[tid] = hist[tid / C][tid % C];   // block bb, class c: bb * C + c
-  __syncthreads();
   // ---- k_scan_counts ----
-  scan_counts_body(sc);
+  if (tid < nb * C) sa.blockcounts[tid] = hist[tid / C][tid % C];   // block bb, class c: bb * C + c
+  if (tid < C) {
+    int run = 0;
+    for (int bb = 0; bb < nb; ++bb) {
+      boff[bb][tid] = run;
+      sc.blockoff[(long long)bb * C + tid] = run;
+      run += hist[bb][tid];
+    }
+    cstart[tid] = run;                         // class total, until the table pass
+  }
+  // class counts among positions [0, lo) and [0, hi): the partial block by atomics
+  for (int which = 0; which < 2; ++which) {
+    const long long bound = which ? sc.hi : sc.lo;
+    const long long start = (bound / kB) * kB;
+    if (tid < kB && start + tid < bound) atomicAdd(which ? &hi_cnt[cls_s[start + tid]] : &lo_cnt[cls_s[start + tid]], 1);
+  }
   __syncthreads();
+  if (tid == 0) {
+    int cs = 0, ob = 0, ts = 0;
+    for (int c = 0; c < C; ++c) {
+      const int tot = cstart[c];
+      const long long blo = sc.lo / kB, bhi = sc.hi / kB;
+      const int lo = lo_cnt[c] + (blo < nb ? boff[blo][c] : tot);
+      const int hi = hi_cnt[c] + (bhi < nb ? boff[bhi][c] : tot);
+      cstart[c] = cs;
+      ctot[c] = tot;
+      const int b0 = cs + lo, e0 = cs + hi;
+      segb[c] = b0;
+      sege[c] = e0;
+      sego[c] = ob;
+      segt[c] = ts;
+      ob += e0 - b0;
+      ts += (e0 - b0 + sc.pt - 1) / sc.pt;
+      cs += tot;
+    }
+    segt[C] = ts;
+    hist[0][0] = cs;                           // (class_start[C]; hist is not read again)
+  }
+  __syncthreads();
+  // the tables, one entry per lane (a one-thread loop of stores is vectorised into wide
+  // stores, which tests/test_isa_guard.py rejects)
+  if (tid < C) {
+    sc.class_start[tid] = cstart[tid];
+    sc.counts[tid] = ctot[tid];
+    sc.seg_pos_begin[tid] = segb[tid];
+    sc.seg_pos_end[tid] = sege[tid];
+    sc.seg_out_base[tid] = sego[tid];
+    sc.seg_tile_start[tid] = segt[tid];
+  } else if (tid == C) {
+    sc.class_start[C] = hist[0][0];
+    sc.seg_tile_start[C] = segt[C];
+  }
   // ---- k_group ----
   {
-    const int c = p < P ? sa.cls_new[p] : -1;
+    const int c = best;
     int rank = 0;
     for (int k = 0; k < C; ++k) {
       const unsigned long long m = __ballot(c == k);
@@ -352,9 +422,10 @@ __global__ __launch_bounds__(1024) void k_small_switch(SwitchArgs sa, ScanArgs s
     }
     __syncthreads();
     if (c >= 0) {
-      int off = ga.class_start[c] + ga.blockoff[(long long)b * C + c];
+      int off = cstart[c] + boff[b][c];
       for (int v = 0; v < wq; ++v) off += wcount[b][v][c];
       ga.perm[off + rank] = (int)p;
+      perm_s[off + rank] = (int)p;
     }
   }
   __syncthreads();
@@ -362,33 +433,69 @@ __global__ __launch_bounds__(1024) void k_small_switch(SwitchArgs sa, ScanArgs s
   // ---- k_lead_flags ----
   {
     const long long pos = p;
-    const int lf = lead_flag(la, pos);
+    int lf = 0;
+    if (pos < la.npos) {
+      const long long q = perm_s[pos];
+      const long long f = q / la.Pf;
+      // the owners were set by this launch's atomics (at L2): read them past the L1
+      lf = __hip_atomic_load(&la.owner[(long long)cls_s[q] * la.P + f * la.Pf + anc_s[q]], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT) == (unsigned)q;
+    }
     const unsigned long long m = __ballot(lf);
     const int excl = __popcll(m & ((1ull << lane) - 1ull));
     if (lane == 0) wc[b][wq] = __popcll(m);
     __syncthreads();
     int base = 0;
     for (int v = 0; v < wq; ++v) base += wc[b][v];
-    if (pos < la.npos) la.lflag_scan[pos] = ((base + excl) << 1) | lf;
-    if ((tid & (kB - 1)) == 0 && b < la.nb) {
-      int t = 0;
-      for (int v = 0; v < kB / 64; ++v) t += wc[b][v];
-      la.lblock[b] = t;
+    if (pos < la.npos) {
+      la.lflag_scan[pos] = ((base + excl) << 1) | lf;
+      lflag_s[pos] = ((base + excl) << 1) | lf;
+    }
+    if (tid == 0) {                            // ---- k_lead_tables (one thread) ----
+      int run = 0;
+      for (int bb = 0; bb < nb; ++bb) {
+        int t = 0;
+        for (int v = 0; v < kB / 64; ++v) t += wc[bb][v];
+        lblk[bb] = run;
+        run += t;
+      }
     }
   }
   __syncthreads();
-  // ---- k_lead_tables ----
-  lead_tables_body(la);
+  if (tid == 0) {
+    int total = 0;
+    for (int bb = 0; bb < nb; ++bb)
+      for (int v = 0; v < kB / 64; ++v) total += wc[bb][v];
+    auto row = [&](long long x) { return x >= la.npos ? total : lblk[x / kB] + (lflag_s[x] >> 1); };
+    int ts = 0;
+    for (int c = 0; c < C; ++c) {
+      const int b0 = row(segb[c]), e0 = row(sege[c]);
+      lsegb[c] = b0;
+      lsege[c] = e0;
+      lsegt[c] = ts;
+      ts += (e0 - b0 + la.pt - 1) / la.pt;
+    }
+    lsegt[C] = ts;
+  }
   __syncthreads();
+  if (tid < C) {
+    la.lseg_pos_begin[tid] = lsegb[tid];
+    la.lseg_pos_end[tid] = lsege[tid];
+    la.lseg_out_base[tid] = lsegb[tid];
+    la.lseg_tile_start[tid] = lsegt[tid];
+  } else if (tid == C) {
+    la.lseg_tile_start[C] = lsegt[C];
+  }
   // ---- k_lead_compact ----
+  if (tid < nb) la.lblock[tid] = lblk[tid];
   if (p < la.npos) {
-    const int v = la.lflag_scan[p];
+    const int v = lflag_s[p];
     if (v & 1) {
-      const long long q = la.perm[p];
-      const int r = la.lblock[b] + (v >> 1);
+      const long long q = perm_s[p];
+      const int r = lblk[b] + (v >> 1);
       const long long f = q / la.Pf;
       la.lperm[r] = (int)q;
-      la.slot[(long long)la.cls_new[q] * la.P + f * la.Pf + la.anc[q]] = r;
+      la.slot[(long long)cls_s[q] * la.P + f * la.Pf + anc_s[q]] = r;
     }
   }
 }
@@ -855,7 +962,11 @@ constexpr long long kSmallP = 1024;
 __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleArgs a) {
   __shared__ double mx[16];
   __shared__ double wsum[4][4];
-  __shared__ double part[1024];
+  // the values the multi-kernel path reads back from its buffers, kept here as written
+  // (the buffers are still written for their other readers): M, block sums / offsets, S,
+  // the read-out partials
+  __shared__ double Msh, Ssh, bsum[4], boff[4];
+  __shared__ double psh[4][kMaxReadout];
   __shared__ double cum_s[kSmallP];
   __shared__ double red[4][4][kMaxReadout];
   __shared__ double rred[8][16];
@@ -867,9 +978,10 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
   const int nb = na.nb;
   const long long p = tid;                            // = b * 256 + (tid & 255)
   const long long g0 = f * P;
+  const double llp = p < P ? na.ll[g0 + p] : 0.0;
   // ---- k_norm_max: the largest ll (NaN ignored, as fmax does) ----
   {
-    double v = p < P ? na.ll[g0 + p] : -INFINITY;
+    double v = p < P ? llp : -INFINITY;
     v = fmax(-INFINITY, v);
     v = wave_max(v);
     if (lane == 0) mx[w] = v;
@@ -878,13 +990,15 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
       double m = mx[0];
       for (int i = 1; i < 16; ++i) m = fmax(m, mx[i]);
       na.gmax[f] = ord_enc(m);
+      Msh = ord_dec(ord_enc(m));
     }
     __syncthreads();
   }
-  const double M = ord_dec(na.gmax[f]);
+  const double M = Msh;
   // ---- k_norm_exp_scan ----
-  const double e = p < P ? exp(na.ll[g0 + p] - M) : 0.0;
+  const double e = p < P ? exp(llp - M) : 0.0;
   if (p < P) na.e[g0 + p] = e;
+  double e_incl;
   {
     double x = e;
 #pragma unroll
@@ -897,41 +1011,34 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
     double base = 0.0;
     for (int v = 0; v < wq; ++v) base += wsum[b][v];
     x += base;
+    e_incl = x;
     if (p < P) na.local[g0 + p] = x;
-    if ((tid & 255) == 255 && b < nb) na.blocksum[f * nb + b] = x;
+    if ((tid & 255) == 255 && b < nb) {
+      na.blocksum[f * nb + b] = x;
+      bsum[b] = x;
+    }
   }
   __syncthreads();
   // ---- k_norm_total ----
-  {
-    const int chunk = (nb + 1023) / 1024;
-    double sv = 0.0;
-    for (int i = 0; i < chunk; ++i) {
-      const int bb = tid * chunk + i;
-      if (bb < nb) sv += na.blocksum[f * nb + bb];
-    }
-    part[tid] = sv;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-      const double v = tid >= off ? part[tid - off] : 0.0;
-      __syncthreads();
-      part[tid] += v;
-      __syncthreads();
-    }
-    double run = tid ? part[tid - 1] : 0.0;
-    for (int i = 0; i < chunk; ++i) {
-      const int bb = tid * chunk + i;
-      if (bb < nb) {
-        na.blockoff[f * nb + bb] = run;
-        run += na.blocksum[f * nb + bb];
-      }
-    }
-    if (tid == 1023) na.total[f] = part[1023];
+  // k_norm_total's 1024-wide Hillis-Steele scan over the nb <= 4 block sums (zeros
+  // beyond): every addition past the first four slots adds an exact +0, so its values are
+  // those of the same scan over four slots, computed here by one thread with the same
+  // operand order (part[i] = part[i] + part[i - off]).
+  if (tid == 0) {
+    double h[4];
+    for (int i = 0; i < 4; ++i) h[i] = i < nb ? bsum[i] : 0.0;
+    for (int off = 1; off < 4; off <<= 1)
+      for (int i = 3; i >= off; --i) h[i] = h[i] + h[i - off];
+    for (int bb = 0; bb < 4; ++bb) boff[bb] = bb ? h[bb - 1] : 0.0;
+    Ssh = h[3];
   }
   __syncthreads();
-  const double S = na.total[f];
+  const double S = Ssh;
+  if (tid < nb) na.blockoff[f * nb + tid] = boff[tid];      // one 8-byte store per lane
+  if (tid == 0) na.total[f] = S;
   // ---- k_cdf ----
   if (p < P) {
-    const double c = p == P - 1 ? 1.0 : (na.blockoff[f * nb + b] + na.local[g0 + p]) / S;
+    const double c = p == P - 1 ? 1.0 : (boff[b] + e_incl) / S;
     na.cum[g0 + p] = c;
     cum_s[p] = c;
   }
@@ -969,7 +1076,7 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
       a.cls_dst[g0 + p] = cnew;
       for (int j = 0; j < d; ++j) a.X_dst[(g0 + p) * d + j] = a.X_src[(g0 + idx) * d + j];
     }
-    const double llv = a.ll[g0 + p];
+    const double llv = llp;
     const double lw = llv - M;
     e2 = exp((llv + lw) - M);
     wv = e / S;
@@ -990,19 +1097,19 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
     double t = 0.0;
     for (int v = 0; v < 4; ++v) t += red[b][v][k];
     a.partials[(f * nb + b) * nq + k] = t;
+    psh[b][k] = t;
   }
   __syncthreads();
   // ---- k_readout ----
-  const double* partials = a.partials + f * nb * nq;
   double* readout = a.readout + f * (C + d + 1);
   for (int k0 = 0; k0 < nq; k0 += 8) {
     double sv[8];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) sv[kk] = 0.0;
-    for (long long bb = tid; bb < nb; bb += 1024)
+    if (tid < nb)
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
-        if (k0 + kk < nq) sv[kk] += partials[bb * nq + k0 + kk];
+        if (k0 + kk < nq) sv[kk] += psh[tid][k0 + kk];
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       const double v = wave_sum(sv[kk]);

@@ -180,7 +180,8 @@ class GPMDM(torch.nn.Module):
             setattr(self, name, torch.nn.Parameter(t.clone(), requires_grad=grad))
 
     def _param_versions(self):
-        return tuple((n, p.data_ptr(), p._version) for n, p in self.named_parameters())
+        # (this module has no submodules: its own parameter table is named_parameters())
+        return tuple((n, p.data_ptr(), p._version) for n, p in self._parameters.items() if p is not None)
 
     def _refresh(self) -> None:
         """Rebuild the device model when the parameters changed since it was built (an

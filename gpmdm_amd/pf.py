@@ -76,6 +76,7 @@ class GPMDM_PF:
         if resample not in ("multinomial", "systematic"):
             raise ValueError("resample must be 'multinomial' or 'systematic'")
         self._rng = rng
+        self._draws = None                      # replay.FrameDraws (rng='torch'), made on first use
         self._resample_mode = resample
         self._group = process_group
         self._exchange_fn = exchange
@@ -187,13 +188,13 @@ class GPMDM_PF:
         lib, h, s = _lib.load(), self._h, self._stream()
         P, C, d = self._num_particles, self.num_classes, self.latent_dim
         if self._rng == "torch":
-            E = np.ascontiguousarray(replay.switch_draws(P, C))
-            counts = np.zeros(C, dtype=np.int64)
-            _lib.check(lib.gpmdm_pf_switch(h, _lib.dptr(E), _lib.i64ptr(counts), s), "switch")
-            normals = np.ascontiguousarray(replay.dynamics_draws(counts, d))
-            self._propagate(z, normals, s)
-            U = replay.resample_draws(P if self._resample_mode == "multinomial" else 1)
-            _lib.check(lib.gpmdm_pf_resample(h, _lib.dptr(np.ascontiguousarray(U)), s), "resample")
+            if self._draws is None:
+                self._draws = replay.FrameDraws(P, C, d, P if self._resample_mode == "multinomial" else 1)
+                self._counts = np.zeros(C, dtype=np.int64)
+            dr, counts = self._draws, self._counts
+            _lib.check(lib.gpmdm_pf_switch(h, _lib.dptr(dr.switch()), _lib.i64ptr(counts), s), "switch")
+            self._propagate(z, dr.dynamics(counts), s)
+            _lib.check(lib.gpmdm_pf_resample(h, _lib.dptr(dr.resample()), s), "resample")
         else:
             _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
             self._propagate(z, None, s)

@@ -61,3 +61,39 @@ def dynamics_draws(counts, d: int, generator: Optional[torch.Generator] = None) 
 def resample_draws(P: int, generator: Optional[torch.Generator] = None) -> np.ndarray:
     """Uniforms of ``torch.multinomial(w, P, replacement=True)`` (P float64)."""
     return torch.rand((P,), dtype=torch.float64, generator=generator).numpy()
+
+
+class FrameDraws:
+    """The per-frame streams of ``switch_draws`` / ``dynamics_draws`` /
+    ``resample_draws`` drawn in place into buffers allocated once (the notebook's
+    per-frame host cost is mostly torch's per-call overhead, not the draws).  A
+    contiguous block of rows draws exactly what a fresh tensor of its shape draws, so
+    the streams are unchanged (tests/test_abi_and_replay.py).  The returned arrays are
+    overwritten by the next frame's draws."""
+
+    def __init__(self, P: int, C: int, d: int, n_uniform: int,
+                 generator: Optional[torch.Generator] = None):
+        self._gen = generator
+        self._E = torch.empty((P, C), dtype=torch.float64)
+        self._N = torch.empty((P, d), dtype=torch.float64)
+        self._U = torch.empty((n_uniform,), dtype=torch.float64)
+        self.E, self.N, self.U = self._E.numpy(), self._N.numpy(), self._U.numpy()
+
+    def switch(self) -> np.ndarray:
+        self._E.exponential_(1, generator=self._gen)
+        return self.E
+
+    def dynamics(self, counts) -> np.ndarray:
+        off = 0
+        for p_c in counts:
+            p_c = int(p_c)
+            if p_c:
+                self._N[off:off + p_c].normal_(0, 1, generator=self._gen)
+                off += p_c
+        if off != self._N.shape[0]:
+            raise ValueError(f"class counts sum to {off}, not {self._N.shape[0]}")
+        return self.N
+
+    def resample(self) -> np.ndarray:
+        self._U.uniform_(0, 1, generator=self._gen)
+        return self.U

@@ -6,6 +6,7 @@ import re
 from pathlib import Path
 
 import numpy as np
+import pytest
 import torch
 
 from conftest import ROOT
@@ -110,3 +111,25 @@ def test_c_host_builds_and_links():
     exe = build.build_c_host()
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "usage" in r.stderr
+
+
+def test_frame_draws_are_the_replay_streams():
+    """replay.FrameDraws (in-place, preallocated) draws the streams of switch_draws /
+    dynamics_draws / resample_draws: class blocks below and above torch's 16-value
+    vectorised threshold, empty classes, several frames."""
+    from gpmdm_amd import replay
+    P, C, d = 37, 3, 3
+    frames = [[20, 0, 17], [1, 30, 6], [37, 0, 0], [5, 5, 27]]
+    torch.manual_seed(11)
+    want = []
+    for counts in frames:
+        want.append((replay.switch_draws(P, C).copy(), replay.dynamics_draws(counts, d).copy(),
+                     replay.resample_draws(P).copy()))
+    torch.manual_seed(11)
+    fd = replay.FrameDraws(P, C, d, P)
+    for counts, (E, N, U) in zip(frames, want):
+        assert np.array_equal(fd.switch(), E)
+        assert np.array_equal(fd.dynamics(counts), N)
+        assert np.array_equal(fd.resample(), U)
+    with pytest.raises(ValueError):
+        fd.dynamics([1, 2, 3])
