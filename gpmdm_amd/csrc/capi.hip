@@ -139,6 +139,23 @@ static void model_release(gpmdm_model* m) {
   if (m && m->refs.fetch_sub(1) == 1) delete m;
 }
 
+// The observation launch's shape for a filter shard of n particles.  With fewer 32-row tiles
+// than one per CU per column block (the notebook's 100 particles: 8 workgroups, a
+// 32-K-step chain of full 32 x 512 MFMA steps on 8 CUs), 16-row tiles over the same image
+// (the 32 x 512 image's fragment layout depends on the waves and column tiles only) halve
+// each workgroup's MFMA chain and double the CUs working.  Each output is accumulated and
+// reduced in the same order whatever the tile height, so results are bitwise those of the
+// default shape (tests/test_gpu_small_path.py).  GPMDM_OBS_SMALL_TILES=0 / 1 forces it
+// off / on (A/B).
+static TileGeo obs_run_geo(const GpImage& obs, long long n, int d) {
+  const TileGeo g = obs.geo;
+  if (!(g.nw == 4 && g.mt == 2 && g.ntw == 8) || d > 12) return g;
+  static const char* env = std::getenv("GPMDM_OBS_SMALL_TILES");
+  bool small = (long long)obs.n_j * cdiv(n, g.pt()) <= 256;
+  if (env) small = env[0] == '1';
+  return small ? TileGeo{4, 1, 8} : g;
+}
+
 struct gpmdm_pf {
   gpmdm_model* m = nullptr;
   // P = all particles = F filters x Pf (a single filter: F = 1, Pf = P)
@@ -156,6 +173,7 @@ struct gpmdm_pf {
   int *cls = nullptr, *cls_new = nullptr, *perm = nullptr, *ridx = nullptr;
   int *blockcounts = nullptr, *blockoff = nullptr, *small = nullptr;   // small: class tables
   int *obs_tab = nullptr;
+  TileGeo obs_geo{};                  // the observation launch's shape (obs_run_geo)
   int* guide = nullptr;             // F x (GB + 3) inverse-CDF guide table
   int *sys_mark = nullptr, *sys_block = nullptr;   // systematic resampling by scan (pf_kernels.hip)
   // ancestor de-duplication: owner/slot are C x P keyed by (class, ancestor)
@@ -628,7 +646,8 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
         return fail(GPMDM_E_NOMEM, "pinned replay-draw buffer");
       }
   }
-  const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, m->obs.tiles(pf->nloc)};
+  pf->obs_geo = obs_run_geo(m->obs, pf->nloc, m->d);
+  const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, pf->obs_geo.pt())};
   if (hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(pf->T, T, sizeof(double) * C * C, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(pf->health, 0, sizeof(unsigned) * kHealthN) != hipSuccess) {
@@ -966,8 +985,8 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     TileParams tp{};
     tp.seg[0] = m->obs.seg();
     tp.n_seg = 1;
-    tp.geo = m->obs.geo;
-    tp.tiles_ub = m->obs.tiles(nl);
+    tp.geo = pf->obs_geo;
+    tp.tiles_ub = (int)cdiv(nl, pf->obs_geo.pt());
     tp.n_j_max = m->obs.n_j;
     tp.seg_pos_begin = pf->obs_tab + 0;
     tp.seg_pos_end = pf->obs_tab + 1;
@@ -1410,7 +1429,8 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
   int rc = dalloc(&qdyn, (size_t)maxparts * nl);
   if (!rc) rc = dalloc(&qobs, (size_t)m->obs.n_parts() * nl);
   if (!rc) rc = dalloc(&sobs, (size_t)m->obs.n_j * nl);
-  const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, m->obs.tiles(pf->nloc)};
+  const TileGeo og = obs_run_geo(m->obs, pf->nloc, m->d);
+  const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, og.pt())};
   if (!rc && hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess)
     rc = fail(GPMDM_E_HIP, "upload of the observation tile table");
   if (rc) {
@@ -1429,6 +1449,7 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
   pf->qobs = qobs;
   pf->sobs = sobs;
   pf->nparts_dyn_max = maxparts;
+  pf->obs_geo = og;
   m->refs.fetch_add(1);
   pf->m = m;
   model_release(old);

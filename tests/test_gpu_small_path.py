@@ -1,9 +1,11 @@
 """GPU: the one-launch paths of small filters (pf_kernels.hip: k_small_switch -- switch, class
 scan, grouping, leader compaction -- for P <= 1024 particles on one shard, k_small_resample
 -- normalise, resample, read-out -- for P <= 1024 per filter) are bitwise the multi-kernel
-path (GPMDM_NO_SMALL_PATH=1): replay and Philox draws, multinomial and systematic
-resampling, with and without ancestor de-duplication, a bank of filters, several frames.  The environment switch is read once per process, so
-each path runs in its own child process (one at a time)."""
+path (GPMDM_NO_SMALL_PATH=1), and the observation GP's 16-row tiles (capi.hip obs_run_geo)
+are bitwise its 32-row tiles: replay and Philox draws, multinomial and systematic
+resampling, with and without ancestor de-duplication, a bank of filters, several frames.
+The environment switches are read once per process, so each configuration runs in its own
+child process (one at a time)."""
 import os
 import subprocess
 import sys
@@ -30,7 +32,8 @@ for name, P, rng, res, dd in (("replay100", 100, "torch", "multinomial", True),
                               ("nodedup1000", 1000, "philox", "multinomial", False),
                               ("sys777", 777, "philox", "systematic", True),
                               ("one", 1, "philox", "multinomial", True),
-                              ("big1500", 1500, "philox", "multinomial", True)):
+                              ("big1500", 1500, "philox", "multinomial", True),
+                              ("philox20k", 20000, "philox", "multinomial", True)):
     torch.manual_seed(3)
     pf = GPMDM_PF(m, T, P, rng=rng, seed=9 if rng == "philox" else None, resample=res, dedup=dd)
     for k in range(4):
@@ -62,8 +65,12 @@ def _run(tmp_path, tag, env_extra):
 
 @pytest.mark.timeout(600)
 def test_small_path_is_bitwise_the_multi_kernel_path(tmp_path):
+    """Default (fused small-filter kernels, 16-row observation tiles for small shards) vs
+    neither, vs 16-row observation tiles for every filter size."""
     fused = _run(tmp_path, "fused", {})
-    multi = _run(tmp_path, "multi", {"GPMDM_NO_SMALL_PATH": "1"})
-    assert fused.keys() == multi.keys()
+    multi = _run(tmp_path, "multi", {"GPMDM_NO_SMALL_PATH": "1", "GPMDM_OBS_SMALL_TILES": "0"})
+    tiles16 = _run(tmp_path, "tiles16", {"GPMDM_OBS_SMALL_TILES": "1"})
+    assert fused.keys() == multi.keys() == tiles16.keys()
     for k in fused:
         assert np.array_equal(fused[k], multi[k]), k
+        assert np.array_equal(fused[k], tiles16[k]), k

@@ -9,7 +9,7 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
   || { echo "pytest failed rc=$?"; tail -40 $out/pytest.log; exit 1; }
 tail -2 $out/pytest.log
 timeout -k 10 300 python bench.py --config 1 > $out/c1_fused.json 2> $out/c1_fused.err || { echo "bench fused failed"; tail -20 $out/c1_fused.err; exit 1; }
-GPMDM_NO_SMALL_PATH=1 timeout -k 10 300 python bench.py --config 1 > $out/c1_multi.json 2> $out/c1_multi.err || { echo "bench multi failed"; tail -20 $out/c1_multi.err; exit 1; }
+GPMDM_NO_SMALL_PATH=1 GPMDM_OBS_SMALL_TILES=0 timeout -k 10 300 python bench.py --config 1 > $out/c1_multi.json 2> $out/c1_multi.err || { echo "bench multi failed"; tail -20 $out/c1_multi.err; exit 1; }
 python -c "
 import json
 for t in ('fused','multi'):
