@@ -190,19 +190,38 @@ struct gpmdm_pf {
   // observation upload through two pinned slots (a pageable hipMemcpyAsync is staged by the
   // runtime and stalls the launching thread); each slot's event guards its reuse
   double* zpin[2] = {nullptr, nullptr};
+  const double* zdev[2] = {nullptr, nullptr};   // device views of zpin (small z read in place)
   double* rpin = nullptr;             // pinned read-out landing buffer (F x (C + d + 1))
   // replay-mode draws (E, normals, U) staged through pinned buffers: the caller's arrays are
   // free for reuse when the call returns, whatever the runtime does with pageable copies;
   // each buffer's event guards its reuse
+  // Small draws (<= kZeroCopyBytes: the notebook's P = 100) are not copied at all: the
+  // kernels read them from the mapped pinned buffer (a copy is a launch of its own, ~4 us
+  // on the frame's critical path).  rep_src[k] is what the kernels read this frame; the
+  // event, recorded after the consuming launches (draws_used), guards the buffer's reuse.
   double* rep_pin[3] = {nullptr, nullptr, nullptr};
+  const double* rep_dev[3] = {nullptr, nullptr, nullptr};   // device view of rep_pin
+  const double* rep_src[3] = {nullptr, nullptr, nullptr};
   hipEvent_t rep_ev[3] = {nullptr, nullptr, nullptr};
+  static constexpr size_t kZeroCopyBytes = 32768;
   hipError_t upload_draws(int k, double* dst, const double* src, size_t n, hipStream_t s) {
-    hipError_t e = hipEventSynchronize(rep_ev[k]);   // the buffer's previous upload has run
+    hipError_t e = hipEventSynchronize(rep_ev[k]);   // the buffer's previous readers have run
     if (e != hipSuccess) return e;
     std::memcpy(rep_pin[k], src, sizeof(double) * n);
-    e = hipMemcpyAsync(dst, rep_pin[k], sizeof(double) * n, hipMemcpyHostToDevice, s);
-    return e != hipSuccess ? e : hipEventRecord(rep_ev[k], s);
+    if (sizeof(double) * n <= kZeroCopyBytes && rep_dev[k]) {
+      rep_src[k] = rep_dev[k];
+      return hipSuccess;
+    }
+    rep_src[k] = dst;
+    return hipMemcpyAsync(dst, rep_pin[k], sizeof(double) * n, hipMemcpyHostToDevice, s);
   }
+  hipError_t draws_used(int k, hipStream_t s) { return hipEventRecord(rep_ev[k], s); }
+  int* cnt_pin = nullptr;             // class counts landing buffer (mapped; replay mode)
+  // read-outs written by the resampling kernels straight into mapped host memory as well
+  // (small read-out tables): gpmdm_pf_read then needs no copy launch, only the stream sync
+  double* ro_pin = nullptr;
+  double* ro_dev = nullptr;
+  int* cnt_dev = nullptr;
   hipEvent_t zev[2] = {nullptr, nullptr};
   int zslot = 0;
   double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *sobs = nullptr;
@@ -280,6 +299,8 @@ struct gpmdm_pf {
     for (auto& r : recs) { pool.push_back(r.a); pool.push_back(r.b); }
     for (auto ev : pool) (void)hipEventDestroy(ev);
     if (rpin) (void)hipHostFree(rpin);
+    if (cnt_pin) (void)hipHostFree(cnt_pin);
+    if (ro_pin) (void)hipHostFree(ro_pin);
     for (int k = 0; k < 2; ++k) {
       if (zpin[k]) (void)hipHostFree(zpin[k]);
       if (zev[k]) (void)hipEventDestroy(zev[k]);
@@ -627,24 +648,51 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   }
 #undef ALLOC
   for (int k = 0; k < 2; ++k) {
-    if (hipHostMalloc((void**)&pf->zpin[k], sizeof(double) * F * D) != hipSuccess ||
-        hipEventCreateWithFlags(&pf->zev[k], hipEventDisableTiming) != hipSuccess) {
+    void* zv = nullptr;
+    if (hipHostMalloc((void**)&pf->zpin[k], sizeof(double) * F * D, hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipEventCreateWithFlags(&pf->zev[k], hipEventDisableTiming) != hipSuccess ||
+        hipHostGetDevicePointer(&zv, pf->zpin[k], 0) != hipSuccess) {
       delete pf;
       return fail(GPMDM_E_NOMEM, "pinned observation buffer");
     }
+    pf->zdev[k] = (const double*)zv;
   }
   if (hipHostMalloc((void**)&pf->rpin, sizeof(double) * F * (C + d + 1)) != hipSuccess) {
     delete pf;
     return fail(GPMDM_E_NOMEM, "pinned read-out buffer");
   }
+  if (sizeof(double) * F * (C + d + 1) <= 32768) {
+    void* rv = nullptr;
+    if (hipHostMalloc((void**)&pf->ro_pin, sizeof(double) * F * (C + d + 1),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(&rv, pf->ro_pin, 0) != hipSuccess) {
+      delete pf;
+      return fail(GPMDM_E_NOMEM, "mapped read-out buffer");
+    }
+    pf->ro_dev = (double*)rv;
+  }
   if (rng_mode == GPMDM_RNG_REPLAY) {
     const long long n[3] = {P * C, P * d, P};      // E, normals, U
-    for (int k = 0; k < 3; ++k)
-      if (hipHostMalloc((void**)&pf->rep_pin[k], sizeof(double) * n[k]) != hipSuccess ||
-          hipEventCreateWithFlags(&pf->rep_ev[k], hipEventDisableTiming) != hipSuccess) {
+    // mapped, coherent (fine-grained): kernels may read the small draws in place
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    for (int k = 0; k < 3; ++k) {
+      void* dv = nullptr;
+      if (hipHostMalloc((void**)&pf->rep_pin[k], sizeof(double) * n[k], fl) != hipSuccess ||
+          hipEventCreateWithFlags(&pf->rep_ev[k], hipEventDisableTiming) != hipSuccess ||
+          hipHostGetDevicePointer(&dv, pf->rep_pin[k], 0) != hipSuccess) {
         delete pf;
         return fail(GPMDM_E_NOMEM, "pinned replay-draw buffer");
       }
+      pf->rep_dev[k] = (const double*)dv;
+    }
+    void* cv = nullptr;
+    if (hipHostMalloc((void**)&pf->cnt_pin, sizeof(int) * kMaxClasses, fl) != hipSuccess ||
+        hipHostGetDevicePointer(&cv, pf->cnt_pin, 0) != hipSuccess) {
+      delete pf;
+      return fail(GPMDM_E_NOMEM, "pinned class-count buffer");
+    }
+    pf->cnt_dev = (int*)cv;
   }
   pf->obs_geo = obs_run_geo(m->obs, pf->nloc, m->d);
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, pf->obs_geo.pt())};
@@ -704,6 +752,7 @@ static ResampleArgs resample_args(gpmdm_pf* pf) {
   ra.ridx = pf->ridx;
   ra.partials = pf->partials;
   ra.readout = pf->readout;
+  ra.readout_host = pf->ro_dev;
   ra.guide = pf->guide;
   ra.GB = guide_buckets_used(pf->Pf);   // 0: plain search
   ra.sys_mark = pf->sys_mark;           // systematic: by scan, no search
@@ -791,7 +840,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   sa.cls = pf->cls;
   sa.cls_new = pf->cls_new;
   sa.T = pf->T;
-  sa.E = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->E : nullptr;
+  sa.E = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->rep_src[0] : nullptr;
   sa.blockcounts = pf->blockcounts;
   sa.gmax_reset = pf->gmax;
   if (pf->dedup && pf->nloc > 0) {
@@ -853,14 +902,20 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
     la.lperm = pf->lperm;
     la.slot = pf->slot;
   }
+  sc.counts_host = class_counts ? pf->cnt_dev : nullptr;   // the counts straight to the host
   launch_switch_group(sa, sc, ga, sa.owner ? &la : nullptr, s);
   pf->mark_end(s, GPMDM_STAGE_SWITCH, t0);
   HIPCHK(hipGetLastError());
+  if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(0, s));
   if (class_counts) {
     int tmp[kMaxClasses];
-    HIPCHK(hipMemcpyAsync(tmp, pf->counts(), sizeof(int) * C, hipMemcpyDeviceToHost, s));
+    const int* src = pf->cnt_pin;
+    if (!sc.counts_host) {
+      HIPCHK(hipMemcpyAsync(tmp, pf->counts(), sizeof(int) * C, hipMemcpyDeviceToHost, s));
+      src = tmp;
+    }
     HIPCHK(hipStreamSynchronize(s));
-    for (int c = 0; c < C; ++c) class_counts[c] = tmp[c];
+    for (int c = 0; c < C; ++c) class_counts[c] = src[c];
   }
   pf->switched = true;
   return GPMDM_OK;
@@ -946,7 +1001,7 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
     fa.X = pf->X;
     for (int j = 0; j <= d; ++j) fa.lin_c2[j] = m->x_lin_c2[j];
     for (int j = 0; j < d; ++j) fa.il2[j] = m->x_il2[j];
-    fa.normals = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->normals : nullptr;
+    fa.normals = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->rep_src[1] : nullptr;
     fa.X_out = pf->X_prop;
     if (pf->dedup) {
       fa.slot = pf->slot;
@@ -956,9 +1011,9 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
     fa.health = pf->health;
     launch_dyn_finish(fa, s);
     pf->mark_end(s, GPMDM_STAGE_DYN_FINISH, t0);
-
   }
   HIPCHK(hipGetLastError());
+  if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(1, s));
   pf->dyn_done = true;
   pf->switched = false;
   return GPMDM_OK;
@@ -970,12 +1025,18 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
   gpmdm_model* m = pf->m;
   const int d = m->d, D = m->D;
   hipEvent_t t0;
+  // z: a small shard's tiles read it in place from the mapped staging slot (no copy launch);
+  // otherwise it is copied once (every tile holding mean columns reads it)
+  const int zk = pf->zslot;
+  const bool zmap = pf->nloc <= 4096 && sizeof(double) * D * pf->F <= 32768;
+  const double* zsrc = pf->z;
   {
-    const int k = pf->zslot;
-    HIPCHK(hipEventSynchronize(pf->zev[k]));      // the slot's previous upload has run
-    std::memcpy(pf->zpin[k], zh, sizeof(double) * D * pf->F);
-    HIPCHK(hipMemcpyAsync(pf->z, pf->zpin[k], sizeof(double) * D * pf->F, hipMemcpyHostToDevice, s));
-    HIPCHK(hipEventRecord(pf->zev[k], s));
+    HIPCHK(hipEventSynchronize(pf->zev[zk]));     // the slot's previous readers have run
+    std::memcpy(pf->zpin[zk], zh, sizeof(double) * D * pf->F);
+    if (zmap)
+      zsrc = pf->zdev[zk];
+    else
+      HIPCHK(hipMemcpyAsync(pf->z, pf->zpin[zk], sizeof(double) * D * pf->F, hipMemcpyHostToDevice, s));
     pf->zslot ^= 1;
   }
   const long long nl = pf->nloc;
@@ -998,7 +1059,7 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     tp.qpart = pf->qobs;
     tp.ld_q = nl;
     tp.spart = pf->sobs;
-    tp.z = pf->z;
+    tp.z = zsrc;
     tp.lam2 = m->y_lam2_dev;
     tp.Pf = pf->Pf;
     launch_gp_tile(tp, d, false, s);
@@ -1014,7 +1075,7 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     oa.jm0 = (m->obs.n_rows + m->obs.coff) / m->obs.geo.nb();   // first block with mean columns
     oa.n_j = m->obs.n_j;
     oa.sum_log_il2 = m->sum_log_il2;
-    oa.z = pf->z;
+    oa.z = zsrc;
     oa.Pf = pf->Pf;
     oa.il2 = m->y_il2_dev;
     oa.ll_const = (double)((float)(0.5 * D) * (float)1.8378770351409912);
@@ -1025,6 +1086,7 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     launch_obs_finish(oa, s);
     pf->mark_end(s, GPMDM_STAGE_OBS_FINISH, t0);
   }
+  HIPCHK(hipEventRecord(pf->zev[zk], s));
   HIPCHK(hipGetLastError());
   pf->propagated = true;
   pf->dyn_done = false;
@@ -1253,8 +1315,9 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   hipEvent_t t0;
   pf->mark_begin(s, GPMDM_STAGE_RESAMPLE, t0);
   ResampleArgs ra = resample_args(pf);
-  ra.U = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->U : nullptr;
+  ra.U = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->rep_src[2] : nullptr;
   launch_normalise_resample(norm_args(pf), ra, s);
+  if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(2, s));
   // next frame's ownership order (identical on every rank: same replicated ancestors)
   pf->own_valid = false;
   if (pf->own && pf->dedup && pf->shard_order) {
@@ -1287,10 +1350,14 @@ int gpmdm_pf_read(gpmdm_pf_t pf, double* post, double* mean, double* lik, void* 
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;
   const int nr = m->C + m->d + 1;
-  HIPCHK(hipMemcpyAsync(pf->rpin, pf->readout, sizeof(double) * pf->F * nr, hipMemcpyDeviceToHost, s));
+  const double* src = pf->ro_pin;      // written by the read-out kernels themselves
+  if (!src) {
+    HIPCHK(hipMemcpyAsync(pf->rpin, pf->readout, sizeof(double) * pf->F * nr, hipMemcpyDeviceToHost, s));
+    src = pf->rpin;
+  }
   HIPCHK(hipStreamSynchronize(s));
   for (int f = 0; f < pf->F; ++f) {
-    const double* b = pf->rpin + (size_t)f * nr;
+    const double* b = src + (size_t)f * nr;
     if (post) std::memcpy(post + (size_t)f * m->C, b, sizeof(double) * m->C);
     if (mean) std::memcpy(mean + (size_t)f * m->d, b + m->C, sizeof(double) * m->d);
     if (lik) lik[f] = b[m->C + m->d];

@@ -64,6 +64,7 @@ struct ScanArgs {
   int* blockoff;                  // nb x C
   int* class_start;               // C + 1
   int* counts;                    // C
+  int* counts_host;               // C, or nullptr: the counts also into mapped host memory
   int* seg_pos_begin;             // C
   int* seg_pos_end;               // C
   int* seg_out_base;              // C
@@ -182,6 +183,7 @@ struct ResampleArgs {
   int* ridx;                      // in-filter source index of each slot
   double* partials;               // F x nb x (C + 1 + d)
   double* readout;                // per filter: C posterior, d mean, 1 likelihood sum
+  double* readout_host;           // the same into mapped host memory (small filters), or nullptr
   int* guide;                     // F x (GB + 3): guide[b] = first i with cum[i] >= b / GB
   long long GB;                   // guide buckets per filter
   // systematic resampling by scan (no per-slot search): run starts of each particle's

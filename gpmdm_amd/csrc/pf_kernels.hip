@@ -146,6 +146,7 @@ __device__ __forceinline__ void scan_counts_body(const ScanArgs& a) {
     for (int c = 0; c < a.C; ++c) {
       a.class_start[c] = cs;
       a.counts[c] = tot[c];
+      if (a.counts_host) a.counts_host[c] = tot[c];
       const int b0 = cs + lo_cnt[c], e0 = cs + hi_cnt[c];
       a.seg_pos_begin[c] = b0;
       a.seg_pos_end[c] = e0;
@@ -403,6 +404,7 @@ __global__ __launch_bounds__(1024) void k_small_switch(SwitchArgs sa, ScanArgs s
   if (tid < C) {
     sc.class_start[tid] = cstart[tid];
     sc.counts[tid] = ctot[tid];
+    if (sc.counts_host) sc.counts_host[tid] = ctot[tid];
     sc.seg_pos_begin[tid] = segb[tid];
     sc.seg_pos_end[tid] = sege[tid];
     sc.seg_out_base[tid] = sego[tid];
@@ -942,6 +944,7 @@ __global__ __launch_bounds__(1024) void k_readout(ResampleArgs a) {
       v = tot[a.C];                                      // log_likelihood()
     }
     readout[tid] = v;
+    if (a.readout_host) a.readout_host[f * nro + tid] = v;
   }
 }
 
@@ -1136,6 +1139,7 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
       v = tot[C];
     }
     readout[tid] = v;
+    if (a.readout_host) a.readout_host[f * nro + tid] = v;
   }
 }
 

@@ -40,7 +40,12 @@ def _obs(m):
 
 
 def _worker(rank, world, port, rng, seeds, out_q):
+    import faulthandler
+    import sys
     import torch.distributed as dist
+    # a rank that hangs dumps its stacks and exits (the parent's queue wait then fails with
+    # the dump in the captured stderr) instead of holding the run until an outer watchdog
+    faulthandler.dump_traceback_later(100, exit=True, file=sys.stderr)
     from conftest import load_fixture
     from gpmdm_amd import GPMDM_PF
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -77,7 +82,7 @@ def _run(rng, seeds):
     for p in procs:
         p.start()
     try:
-        res = dict((r, (kind, payload)) for r, kind, payload in (q.get(timeout=240) for _ in range(world)))
+        res = dict((r, (kind, payload)) for r, kind, payload in (q.get(timeout=130) for _ in range(world)))
     finally:
         for p in procs:
             p.join(timeout=120)
@@ -164,7 +169,7 @@ def test_rccl_async_allgather_world1():
     p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
     p.start()
     try:
-        kind, payload = q.get(timeout=240)
+        kind, payload = q.get(timeout=130)
     finally:
         p.join(timeout=60)
         if p.is_alive():
