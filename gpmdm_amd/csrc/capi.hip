@@ -173,6 +173,11 @@ struct gpmdm_pf {
   int *cls = nullptr, *cls_new = nullptr, *perm = nullptr, *ridx = nullptr;
   int *blockcounts = nullptr, *blockoff = nullptr, *small = nullptr;   // small: class tables
   int *obs_tab = nullptr;
+  // likelihood finish deferred into the resampling launch (single-shard small filters:
+  // k_small_resample computes ll first, one launch less per frame); flush_ll runs it for
+  // any reader of ll that comes first
+  bool ll_pending = false;
+  ObsFinishArgs oa_pending{};
   TileGeo obs_geo{};                  // the observation launch's shape (obs_run_geo)
   int* guide = nullptr;             // F x (GB + 3) inverse-CDF guide table
   int *sys_mark = nullptr, *sys_block = nullptr;   // systematic resampling by scan (pf_kernels.hip)
@@ -773,7 +778,19 @@ static NormArgs norm_args(gpmdm_pf* pf) {
   na.blockoff = pf->blockoffw;
   na.total = pf->total;
   na.cum = pf->cum;
+  if (pf->ll_pending) {
+    na.obs = pf->oa_pending;
+    na.obs_pending = 1;
+  }
   return na;
+}
+
+static int flush_ll(gpmdm_pf* pf, hipStream_t s) {
+  if (!pf->ll_pending) return GPMDM_OK;
+  launch_obs_finish(pf->oa_pending, s);
+  pf->ll_pending = false;
+  HIPCHK(hipGetLastError());
+  return GPMDM_OK;
 }
 
 int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
@@ -803,7 +820,7 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   HIPCHK(hipDeviceSynchronize());
   pf->initialised = true;
   pf->own_valid = false;               // no ancestors yet: identity ownership
-  pf->switched = pf->propagated = pf->dyn_done = false;
+  pf->switched = pf->propagated = pf->dyn_done = pf->ll_pending = false;
   return GPMDM_OK;
 }
 
@@ -1083,7 +1100,13 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     oa.ll_offset = pf->lo;
     oa.own = pf->own_order();
     oa.health = pf->health;
-    launch_obs_finish(oa, s);
+    pf->ll_pending = false;
+    if (pf->n_ranks == 1 && !oa.own && oa.ll_offset == 0 && small_resample_ok(norm_args(pf), resample_args(pf))) {
+      pf->oa_pending = oa;             // computed by the resampling launch (or flush_ll)
+      pf->ll_pending = true;
+    } else {
+      launch_obs_finish(oa, s);
+    }
     pf->mark_end(s, GPMDM_STAGE_OBS_FINISH, t0);
   }
   HIPCHK(hipEventRecord(pf->zev[zk], s));
@@ -1262,6 +1285,7 @@ int gpmdm_pf_pack_part(gpmdm_pf_t pf, double* send, int part, void* stream) {
 }
 
 static int pack_part(gpmdm_pf* pf, double* send, int part, hipStream_t s) {
+  TRY(flush_ll(pf, s));
   PackArgs a{};
   a.n = pf->nloc;
   a.lo = pf->lo;
@@ -1317,6 +1341,7 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   ResampleArgs ra = resample_args(pf);
   ra.U = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->rep_src[2] : nullptr;
   launch_normalise_resample(norm_args(pf), ra, s);
+  pf->ll_pending = false;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(2, s));
   // next frame's ownership order (identical on every rank: same replicated ancestors)
   pf->own_valid = false;
@@ -1371,6 +1396,7 @@ int gpmdm_pf_export(gpmdm_pf_t pf, double* states, int64_t* classes, double* ll,
   const gpmdm_model* m = pf->m;
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;
+  TRY(flush_ll(pf, s));
   HIPCHK(hipStreamSynchronize(s));
   const long long P = pf->P;
   if (states) HIPCHK(hipMemcpy(states, pf->X, sizeof(double) * P * m->d, hipMemcpyDeviceToHost));
@@ -1527,6 +1553,7 @@ int gpmdm_pf_health(gpmdm_pf_t pf, int64_t* counts, int reset, void* stream) {
   CHECK(pf, "null handle");
   HIPCHK(hipSetDevice(pf->m->device));
   hipStream_t s = (hipStream_t)stream;
+  TRY(flush_ll(pf, s));
   unsigned h[kHealthN];
   HIPCHK(hipMemcpyAsync(h, pf->health, sizeof(h), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));

@@ -164,6 +164,10 @@ struct NormArgs {
   double* blockoff;               // F x nb
   double* total;                  // F: sum of e
   double* cum;                    // normalised CDF, F x P
+  // a deferred likelihood finish (k_obs_ll) of a single-shard filter: the small-filter
+  // kernel computes ll itself first, the multi-kernel path launches k_obs_ll first
+  ObsFinishArgs obs;
+  int obs_pending;
 };
 
 struct ResampleArgs {
@@ -231,6 +235,7 @@ void launch_obs_finish(const ObsFinishArgs& a, hipStream_t s);
 void launch_normalise(const NormArgs& a, hipStream_t s);
 void launch_resample(const ResampleArgs& a, hipStream_t s);
 void launch_normalise_resample(const NormArgs& na, const ResampleArgs& ra, hipStream_t s);
+bool small_resample_ok(const NormArgs& na, const ResampleArgs& ra);
 void launch_switch_group(const SwitchArgs& sa, const ScanArgs& sc, const GroupArgs& ga, const LeadArgs* la,
                          hipStream_t s);
 void launch_pack(const PackArgs& a, hipStream_t s);

@@ -614,15 +614,21 @@ __global__ __launch_bounds__(kB) void k_obs_finish(ObsFinishArgs a) {
 //   ll = -1/2 sum_j[(z_j - mu_j)^2 / var_j + log var_j] + sum_j(-log sqrt var_j) - D/2 ln(2pi)_f32
 //      = -1/2 S / vc - D log vc - sum_j log il2_j - D/2 ln(2pi)_f32
 // (the reference's double count of log var kept, gpmdm_pf.py:188-192).
-__global__ __launch_bounds__(kB) void k_obs_ll(ObsFinishArgs a) {
-  const long long o = (long long)blockIdx.x * kB + threadIdx.x;
-  if (o >= a.n_out) return;
+// (a device function: k_small_resample computes a deferred finish with the same code)
+__device__ __forceinline__ double obs_ll_value(const ObsFinishArgs& a, long long o, double& vc) {
   double q = 0.0;
   for (int k = 0; k < a.n_parts; ++k) q += a.qpart[(long long)k * a.ld_q + o];
   double S = 0.0;
   for (int k = a.jm0; k < a.n_j; ++k) S += a.spart[(long long)k * a.ld_q + o];
-  const double vc = 1.0 - q;                           // k(x*,x*) = 1 (gpmdm.py:991)
-  const double llv = -0.5 * S / vc - a.D * log(vc) - a.sum_log_il2 - a.ll_const;
+  vc = 1.0 - q;                                        // k(x*,x*) = 1 (gpmdm.py:991)
+  return -0.5 * S / vc - a.D * log(vc) - a.sum_log_il2 - a.ll_const;
+}
+
+__global__ __launch_bounds__(kB) void k_obs_ll(ObsFinishArgs a) {
+  const long long o = (long long)blockIdx.x * kB + threadIdx.x;
+  if (o >= a.n_out) return;
+  double vc;
+  const double llv = obs_ll_value(a, o, vc);
   a.ll[a.own ? a.own[a.ll_offset + o] : a.ll_offset + o] = llv;
   if (a.health) {
     count_event(a.health + kHealthObsVar, !(vc > 0.0));
@@ -981,7 +987,22 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
   const int nb = na.nb;
   const long long p = tid;                            // = b * 256 + (tid & 255)
   const long long g0 = f * P;
-  const double llp = p < P ? na.ll[g0 + p] : 0.0;
+  double llp;
+  if (na.obs_pending) {
+    // ---- k_obs_ll (deferred by the single-shard filter's weigh step): out index g0 + p ----
+    double vc = 1.0, llv = 0.0;
+    if (p < P) {
+      llv = obs_ll_value(na.obs, g0 + p, vc);
+      na.obs.ll[g0 + p] = llv;
+    }
+    if (na.obs.health) {
+      count_event(na.obs.health + kHealthObsVar, p < P && !(vc > 0.0));
+      count_event(na.obs.health + kHealthObsLL, p < P && !isfinite(llv));
+    }
+    llp = llv;
+  } else {
+    llp = p < P ? na.ll[g0 + p] : 0.0;
+  }
   // ---- k_norm_max: the largest ll (NaN ignored, as fmax does) ----
   {
     double v = p < P ? llp : -INFINITY;
@@ -1308,12 +1329,17 @@ void launch_resample(const ResampleArgs& a, hipStream_t s) {
 }
 // normalise + resample + read-out: one launch for small filters (k_small_resample, bitwise
 // the multi-kernel path), the multi-kernel path otherwise (GPMDM_NO_SMALL_PATH=1 forces it)
-void launch_normalise_resample(const NormArgs& na, const ResampleArgs& ra, hipStream_t s) {
+bool small_resample_ok(const NormArgs& na, const ResampleArgs& ra) {
   static const bool no_small = std::getenv("GPMDM_NO_SMALL_PATH") != nullptr;
-  if (!no_small && na.P <= kSmallP && ra.GB == 0) {
+  return !no_small && na.P <= kSmallP && ra.GB == 0;
+}
+
+void launch_normalise_resample(const NormArgs& na, const ResampleArgs& ra, hipStream_t s) {
+  if (small_resample_ok(na, ra)) {
     hipLaunchKernelGGL(k_small_resample, dim3((unsigned)na.F), dim3(1024), 0, s, na, ra);
     return;
   }
+  if (na.obs_pending) launch_obs_finish(na.obs, s);
   launch_normalise(na, s);
   launch_resample(ra, s);
 }
