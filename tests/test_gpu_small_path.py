@@ -74,3 +74,36 @@ def test_small_path_is_bitwise_the_multi_kernel_path(tmp_path):
     for k in fused:
         assert np.array_equal(fused[k], multi[k]), k
         assert np.array_equal(fused[k], tiles16[k]), k
+
+
+def test_deferred_likelihood_is_flushed_for_an_early_reader():
+    """A single-shard small filter defers its likelihood finish into the resampling launch
+    (capi.hip weigh / flush_ll): an export between propagate and resample must still see
+    the finished ll, and the frame must end bitwise as an uninterrupted update."""
+    import torch
+    from conftest import load_fixture, product_model
+    from gpmdm_amd import GPMDM_PF, _lib
+    f = load_fixture("config2_n2000_p1000")
+    m = product_model(f)
+    T = torch.tensor(np.asarray(f["T"], dtype=np.float64))
+    Y = m.get_Y()
+    torch.manual_seed(5)                      # the initial particles come from torch's generator
+    a = GPMDM_PF(m, T, 300, rng="philox", seed=4)
+    torch.manual_seed(5)
+    b = GPMDM_PF(m, T, 300, rng="philox", seed=4)
+    lib = _lib.load()
+    for k in range(3):
+        z = np.ascontiguousarray(np.asarray(Y[70 + 11 * k], dtype=np.float64) + 0.02)
+        a.update(z)
+        s = b._stream()
+        _lib.check(lib.gpmdm_pf_switch(b._h, None, None, s), "switch")
+        _lib.check(lib.gpmdm_pf_propagate(b._h, _lib.dptr(z), None, s), "propagate")
+        mid = b.export_state()                # reads ll before the resampling launch
+        _lib.check(lib.gpmdm_pf_resample(b._h, None, s), "resample")
+        b._readout = None
+        ea, eb = a.export_state(), b.export_state()
+        assert np.array_equal(mid["ll"], ea["ll"])
+        for key in ("states", "classes", "ll", "w", "resample_idx"):
+            assert np.array_equal(ea[key], eb[key]), key
+        assert np.array_equal(a.class_probabilities().numpy(), b.class_probabilities().numpy())
+        assert np.array_equal(a.current_state_mean().numpy(), b.current_state_mean().numpy())
