@@ -112,6 +112,10 @@ struct gpmdm_model {
   std::vector<double> X;              // host copy, N x d
   std::vector<double> y_ls, x_ls, x_lin_c2, x_il2, y_il2;
   GpImage obs;
+  // the observation GP in 16 x 256 tiles for small models and filters (obs_pick): at the
+  // notebook's N = 500 and P = 100 the 512-column blocks leave a 32-K-step chain of wide
+  // MFMA steps on a handful of CUs; 256-column blocks halve each chain (empty: not built)
+  GpImage obs_small;
   std::vector<GpImage> dyn;           // narrow tiles (16x256): de-duplicated rows, small maps
   std::vector<GpImage> dynw;          // wide tiles (the observation GP's shape): every particle
                                       // (dedup off, predict), large maps; empty = same as dyn
@@ -128,6 +132,7 @@ struct gpmdm_model {
 
   ~gpmdm_model() {
     obs.release();
+    obs_small.release();
     for (auto& g : dyn) g.release();
     for (auto& g : dynw) g.release();
     dfree(y_il2_dev);
@@ -139,21 +144,40 @@ static void model_release(gpmdm_model* m) {
   if (m && m->refs.fetch_sub(1) == 1) delete m;
 }
 
-// The observation launch's shape for a filter shard of n particles.  With fewer 32-row tiles
-// than one per CU per column block (the notebook's 100 particles: 8 workgroups, a
-// 32-K-step chain of full 32 x 512 MFMA steps on 8 CUs), 16-row tiles over the same image
-// (the 32 x 512 image's fragment layout depends on the waves and column tiles only) halve
-// each workgroup's MFMA chain and double the CUs working.  Each output is accumulated and
-// reduced in the same order whatever the tile height, so results are bitwise those of the
-// default shape (tests/test_gpu_small_path.py).  GPMDM_OBS_SMALL_TILES=0 / 1 forces it
-// off / on (A/B).
-static TileGeo obs_run_geo(const GpImage& obs, long long n, int d) {
-  const TileGeo g = obs.geo;
-  if (!(g.nw == 4 && g.mt == 2 && g.ntw == 8) || d > 12) return g;
-  static const char* env = std::getenv("GPMDM_OBS_SMALL_TILES");
-  bool small = (long long)obs.n_j * cdiv(n, g.pt()) <= 256;
-  if (env) small = env[0] == '1';
-  return small ? TileGeo{4, 1, 8} : g;
+// The observation launch's image and shape for filters of P particles each (all ranks;
+// a bank: per filter) whose shard holds n rows.
+// * Small models (N <= kSmallObsN, d <= 12) and filters (P <= kSmallObsP): the 16 x 256
+//   image (model.obs_small).  Its column blocks differ from the default image's, so the
+//   per-block partial sums combine in another order: results agree to rounding, not bit
+//   for bit, and the choice depends on the per-filter P only (every rank of a sharded
+//   filter, and a bank and its filters run alone, make the same one).
+//   GPMDM_OBS_IMAGE16=0 does not build the image.
+// * Otherwise, with fewer 32-row tiles than one per CU per column block, 16-row tiles over
+//   the same 32 x 512 image (the image's fragment layout depends on the waves and column
+//   tiles only): each workgroup's MFMA chain halves and twice the CUs work; every output is
+//   accumulated and reduced in the same order whatever the tile height, so results are
+//   bitwise those of the default shape (tests/test_gpu_small_path.py).
+//   GPMDM_OBS_SMALL_TILES=0 / 1 forces these 16-row tiles off / on (A/B).
+constexpr long long kSmallObsN = 1024, kSmallObsP = 1024;
+
+static int obs_parts_max(const gpmdm_model* m) {
+  return std::max(m->obs.n_parts(), m->obs_small.Bf ? m->obs_small.n_parts() : 0);
+}
+static int obs_blocks_max(const gpmdm_model* m) { return std::max(m->obs.n_j, m->obs_small.n_j); }
+static const GpImage& obs_pick(const gpmdm_model* m, long long P, long long n, TileGeo& geo) {
+  if (m->obs_small.Bf && P <= kSmallObsP) {
+    geo = m->obs_small.geo;
+    return m->obs_small;
+  }
+  const TileGeo g = m->obs.geo;
+  geo = g;
+  if (g.nw == 4 && g.mt == 2 && g.ntw == 8 && m->d <= 12) {
+    static const char* env = std::getenv("GPMDM_OBS_SMALL_TILES");
+    bool small = (long long)m->obs.n_j * cdiv(n, g.pt()) <= 256;
+    if (env) small = env[0] == '1';
+    if (small) geo = TileGeo{4, 1, 8};
+  }
+  return m->obs;
 }
 
 struct gpmdm_pf {
@@ -178,7 +202,8 @@ struct gpmdm_pf {
   // any reader of ll that comes first
   bool ll_pending = false;
   ObsFinishArgs oa_pending{};
-  TileGeo obs_geo{};                  // the observation launch's shape (obs_run_geo)
+  const GpImage* obs_img = nullptr;   // the observation launch's image and shape (obs_pick)
+  TileGeo obs_geo{};
   int* guide = nullptr;             // F x (GB + 3) inverse-CDF guide table
   int *sys_mark = nullptr, *sys_block = nullptr;   // systematic resampling by scan (pf_kernels.hip)
   // ancestor de-duplication: owner/slot are C x P keyed by (class, ancestor)
@@ -413,6 +438,15 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
   int rc = build_image(m->obs, (int)m->N, d, m->D, desc->X, desc->y_lengthscales, nullptr,
                        desc->obs_R, desc->obs_beta, obs_geo);
   if (rc) { delete m; return rc; }
+  {
+    const char* e = std::getenv("GPMDM_OBS_IMAGE16");       // "0": not built (A/B, tests)
+    if (m->N <= kSmallObsN && d <= 12 && obs_geo.nw == kGeo32x512.nw && obs_geo.mt == kGeo32x512.mt &&
+        obs_geo.ntw == kGeo32x512.ntw && !(e && e[0] == '0')) {
+      rc = build_image(m->obs_small, (int)m->N, d, m->D, desc->X, desc->y_lengthscales, nullptr,
+                       desc->obs_R, desc->obs_beta, kGeo16x256);
+      if (rc) { delete m; return rc; }
+    }
+  }
   m->dyn.resize(m->C);
   const bool two = dynw_geo.nw != dyn_geo.nw || dynw_geo.mt != dyn_geo.mt || dynw_geo.ntw != dyn_geo.ntw;
   if (two) m->dynw.resize(m->C);
@@ -622,8 +656,8 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   ALLOC(lperm, P);
   ALLOC(qdyn, (long long)maxparts * nl);
   ALLOC(mudyn, nl * d);
-  ALLOC(qobs, (long long)m->obs.n_parts() * nl);
-  ALLOC(sobs, (long long)m->obs.n_j * nl);   // fused likelihood partials (no mean stored)
+  ALLOC(qobs, (long long)obs_parts_max(m) * nl);
+  ALLOC(sobs, (long long)obs_blocks_max(m) * nl);   // fused likelihood partials (no mean stored)
   ALLOC(z, F * D);
   if (rng_mode == GPMDM_RNG_REPLAY) {
     ALLOC(E, P * C);
@@ -699,7 +733,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
     }
     pf->cnt_dev = (int*)cv;
   }
-  pf->obs_geo = obs_run_geo(m->obs, pf->nloc, m->d);
+  pf->obs_img = &obs_pick(m, pf->Pf, pf->nloc, pf->obs_geo);
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, pf->obs_geo.pt())};
   if (hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(pf->T, T, sizeof(double) * C * C, hipMemcpyHostToDevice) != hipSuccess ||
@@ -1061,11 +1095,12 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     // ---- observation GP + likelihood over particles [lo, hi) ----
     pf->mark_begin(s, GPMDM_STAGE_OBS_GEMM, t0);
     TileParams tp{};
-    tp.seg[0] = m->obs.seg();
+    const GpImage& oi = *pf->obs_img;
+    tp.seg[0] = oi.seg();
     tp.n_seg = 1;
     tp.geo = pf->obs_geo;
     tp.tiles_ub = (int)cdiv(nl, pf->obs_geo.pt());
-    tp.n_j_max = m->obs.n_j;
+    tp.n_j_max = oi.n_j;
     tp.seg_pos_begin = pf->obs_tab + 0;
     tp.seg_pos_end = pf->obs_tab + 1;
     tp.seg_out_base = pf->obs_tab + 2;
@@ -1084,13 +1119,13 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     pf->mark_begin(s, GPMDM_STAGE_OBS_FINISH, t0);
     ObsFinishArgs oa{};
     oa.n_out = nl;
-    oa.n_parts = m->obs.n_parts();
+    oa.n_parts = oi.n_parts();
     oa.D = D;
     oa.qpart = pf->qobs;
     oa.ld_q = nl;
     oa.spart = pf->sobs;
-    oa.jm0 = (m->obs.n_rows + m->obs.coff) / m->obs.geo.nb();   // first block with mean columns
-    oa.n_j = m->obs.n_j;
+    oa.jm0 = (oi.n_rows + oi.coff) / oi.geo.nb();   // first block with mean columns
+    oa.n_j = oi.n_j;
     oa.sum_log_il2 = m->sum_log_il2;
     oa.z = zsrc;
     oa.Pf = pf->Pf;
@@ -1520,9 +1555,10 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
   const long long nl = std::max(pf->nloc, 1ll);
   double *qdyn = nullptr, *qobs = nullptr, *sobs = nullptr;
   int rc = dalloc(&qdyn, (size_t)maxparts * nl);
-  if (!rc) rc = dalloc(&qobs, (size_t)m->obs.n_parts() * nl);
-  if (!rc) rc = dalloc(&sobs, (size_t)m->obs.n_j * nl);
-  const TileGeo og = obs_run_geo(m->obs, pf->nloc, m->d);
+  if (!rc) rc = dalloc(&qobs, (size_t)obs_parts_max(m) * nl);
+  if (!rc) rc = dalloc(&sobs, (size_t)obs_blocks_max(m) * nl);
+  TileGeo og{};
+  const GpImage* oimg = &obs_pick(m, pf->Pf, pf->nloc, og);
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, og.pt())};
   if (!rc && hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess)
     rc = fail(GPMDM_E_HIP, "upload of the observation tile table");
@@ -1543,6 +1579,7 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
   pf->sobs = sobs;
   pf->nparts_dyn_max = maxparts;
   pf->obs_geo = og;
+  pf->obs_img = oimg;
   m->refs.fetch_add(1);
   pf->m = m;
   model_release(old);

@@ -107,3 +107,57 @@ def test_deferred_likelihood_is_flushed_for_an_early_reader():
             assert np.array_equal(ea[key], eb[key]), key
         assert np.array_equal(a.class_probabilities().numpy(), b.class_probabilities().numpy())
         assert np.array_equal(a.current_state_mean().numpy(), b.current_state_mean().numpy())
+
+
+CHILD_IMAGE16 = r'''
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[2]); sys.path.insert(0, sys.argv[2] + "/tests")
+from conftest import load_fixture, product_model
+from gpmdm_amd import GPMDM_PF, GPMDM_PF_Bank
+f = load_fixture("config1_n500_p100_f200")
+m = product_model(f)
+T = torch.tensor(np.asarray(f["T"], dtype=np.float64))
+Y = m.get_Y()
+out = {}
+for name, P, rng in (("replay100", 100, "torch"), ("philox1000", 1000, "philox")):
+    torch.manual_seed(3)
+    pf = GPMDM_PF(m, T, P, rng=rng, seed=9 if rng == "philox" else None)
+    for k in range(6):
+        pf.update(Y[40 + 7 * k] + 0.01)
+        out[f"{name}_{k}_post"] = pf.class_probabilities().numpy()
+        out[f"{name}_{k}_mean"] = pf.current_state_mean().numpy()
+    st = pf.export_state()
+    for key in ("states", "classes", "ll", "resample_idx"):
+        out[f"{name}_{key}"] = st[key]
+bank = GPMDM_PF_Bank(m, T, 5, 100, seed=5)
+for k in range(4):
+    bank.update(np.stack([Y[10 * i + k] for i in range(5)]))
+out["bank_post"] = bank.class_probabilities().numpy()
+out["bank_states"] = bank.export_state()["states"]
+np.savez(sys.argv[1], **out)
+'''
+
+
+@pytest.mark.timeout(600)
+def test_small_observation_image_matches_the_default_image(tmp_path):
+    """Small models and filters run the observation GP over a 16 x 256 image (capi.hip
+    obs_pick): its column blocks partition the sums differently, so the filter agrees with
+    the 32 x 512 image to rounding (not bit for bit) -- same classes and resampling
+    indices, states and read-outs to 1e-9 -- on the config-1 model (N = 500)."""
+    def run(tag, env_extra):
+        env = dict(os.environ, **env_extra)
+        path = tmp_path / f"{tag}.npz"
+        r = subprocess.run([sys.executable, "-c", CHILD_IMAGE16, str(path), str(ROOT)], env=env,
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return dict(np.load(path))
+    small = run("image16", {})
+    default = run("image32", {"GPMDM_OBS_IMAGE16": "0"})
+    assert small.keys() == default.keys()
+    for k in small:
+        if k.endswith(("classes", "resample_idx")):
+            assert np.array_equal(small[k], default[k]), k
+        elif k.endswith("_ll"):
+            np.testing.assert_allclose(small[k], default[k], rtol=1e-9, atol=1e-9, err_msg=k)
+        else:
+            np.testing.assert_allclose(small[k], default[k], rtol=1e-9, atol=1e-12, err_msg=k)
