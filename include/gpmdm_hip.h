@@ -140,7 +140,12 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* exp_draws, int64_t* class_count
 
 /* _propogate_dynamics + _update_weights' likelihoods for this rank's particles
  * (gpmdm_pf.py:153-192).  z: D host.  normals: (sum_c P_c) x d host in the reference's
- * per-class order (replay) or NULL (philox). */
+ * per-class order (replay) or NULL (philox).  A single-shard filter of <= 1024 particles
+ * per filter leaves the last step of the likelihoods (the per-particle finish) to the
+ * next gpmdm_pf_resample launch; gpmdm_pf_export, gpmdm_pf_pack(_part) and
+ * gpmdm_pf_health run it first if it is still pending, so every reader sees the same ll.
+ * The host arrays (draws, z) are copied before the call returns; small ones are read by
+ * the kernels from the library's mapped pinned buffers instead of a copy launch. */
 int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* z, const double* normals, void* stream);
 
 /* gpmdm_pf_propagate in two halves, so a multi-rank caller can exchange the new states
