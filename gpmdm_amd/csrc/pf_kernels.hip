@@ -987,6 +987,9 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
   const int nb = na.nb;
   const long long p = tid;                            // = b * 256 + (tid & 255)
   const long long g0 = f * P;
+  // the replay uniforms (host-mapped for small filters: a PCIe round trip) are loaded
+  // here, ahead of the phases before the search, so their latency overlaps them
+  const double u_pre = (a.U && !a.identity && p < P) ? a.U[a.systematic ? 0 : p] : 0.0;
   double llp;
   if (na.obs_pending) {
     // ---- k_obs_ll (deferred by the single-shard filter's weigh step): out index g0 + p ----
@@ -1080,9 +1083,9 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
     } else {
       double u;
       if (a.systematic) {
-        u = sys_u(p, sys_u0(a, f), P);
+        u = sys_u(p, a.U ? u_pre : sys_u0(a, f), P);
       } else if (a.U) {
-        u = a.U[p];
+        u = u_pre;
       } else {
         const uint4 r = philox4x32_10(make_uint4((unsigned)p, a.frame, kStreamResample, 0u), key);
         u = u01_co(r.x, r.y);
