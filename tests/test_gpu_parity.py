@@ -246,11 +246,14 @@ def test_two_rank_sharding_on_one_gpu(m2):
         assert np.array_equal(ref.current_state_mean().numpy(), r1.current_state_mean().numpy())
 
 
-@pytest.mark.parametrize("C,d,D,L", [(5, 8, 24, 41), (8, 16, 40, 23), (1, 1, 5, 70)])
+@pytest.mark.parametrize("C,d,D,L", [(5, 8, 24, 41), (8, 16, 40, 23), (1, 1, 5, 70), (2, 2, 700, 30),
+                                     (3, 4, 600, 120)])
 def test_config3_and_config5_shapes_vs_oracle(C, d, D, L):
     """The d / C instantiations of the BASELINE configs 3 (d=8, C=5) and 5 (d=16, C=8) at
-    small N, plus the degenerate C=1, d=1: predictive maps and one full resynced filter
-    step against the oracle."""
+    small N, plus the degenerate C=1, d=1, and wide observations whose mean columns span
+    several column blocks (D = 700 at N = 180: the small-model 16 x 256 image, 3 blocks of
+    mean columns; D = 600 at N = 1080: the default image, 2 blocks): predictive maps and one
+    full resynced filter step against the oracle."""
     from gpmdm_amd import GPMDM, GPMDM_PF, synthetic, replay
     from oracle import gpmdm_oracle as O
     data = synthetic.make_sequences(C=C, S=3, L=L, D=D, d=d, seed=9)
