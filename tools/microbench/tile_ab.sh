@@ -1,18 +1,25 @@
 #!/bin/bash
 # Build tile_ab.hip against gp_tile.h as of several commits (WT = the working tree), here:
-#   bash tools/microbench/tile_ab.sh build <commit>...
+#   bash tools/microbench/tile_ab.sh build <commit>[:MACRO,...]...
 # and run them alternately on the GPU box:  bash tools/microbench/tile_ab.sh run
 set -e
 cd "$(dirname "$0")/../.."
 out=tools/microbench/ab
 if [ "$1" = build ]; then
   shift; rm -rf $out; mkdir -p $out
-  for c in "$@"; do
+  # a build spec is <commit|WT>[:MACRO[,MACRO...]] -- the macros are defined for that build
+  # (A/B candidates kept behind #ifdef in the working tree), e.g. WT:GPMDM_EXP_SHIFT
+  for spec in "$@"; do
+    c=${spec%%:*}; defs=""; name=$c
+    if [ "$spec" != "$c" ]; then
+      for m in $(echo ${spec#*:} | tr ',' ' '); do defs="$defs -D$m"; done
+      name=${c}_$(echo ${spec#*:} | tr ',' '_')
+    fi
     src=/tmp/tile_ab_src/$c; rm -rf $src; mkdir -p $src
     if [ $c = WT ]; then cp -r gpmdm_amd include $src/; else git archive $c gpmdm_amd/csrc include | tar -x -C $src; fi
     for d in 3 8 16; do
-      /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I $src/include -DTB_D=$d \
-        "-DGP_TILE_H=\"$src/gpmdm_amd/csrc/gp_tile.h\"" tools/microbench/tile_ab.hip -o $out/tile_ab_d${d}_$c &
+      /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I $src/include -DTB_D=$d $defs \
+        "-DGP_TILE_H=\"$src/gpmdm_amd/csrc/gp_tile.h\"" tools/microbench/tile_ab.hip -o $out/tile_ab_d${d}_$name &
     done
   done
   wait; ls $out
