@@ -35,6 +35,11 @@ namespace {
 // problem; below, the narrow tiles' shorter K loops win)
 constexpr long long kWideRows = 4096;
 
+// Single replay filters up to this size count their switched classes on the host
+// (gpmdm_pf::cls_pin; the one-workgroup resampling kernel k_small_resample provides the
+// classes).  The host loop is P x C fp64 divisions: ~1 us at the notebook's P = 100.
+constexpr long long kHostCountsMaxP = 1024;
+
 // One GP's device image: scaled inputs (+ squared norms) and B = [R | M] (+ H for the
 // dynamics GPs) in MFMA-fragment order -- layout and packing in host_image.h.
 struct GpImage {
@@ -247,6 +252,23 @@ struct gpmdm_pf {
   }
   hipError_t draws_used(int k, hipStream_t s) { return hipEventRecord(rep_ev[k], s); }
   int* cnt_pin = nullptr;             // class counts landing buffer (mapped; replay mode)
+  // Host-side class counts (single small replay filters).  The per-class normals are drawn
+  // on the host with shapes P_c x d after the switch, so the switch's class counts used to
+  // cost a mid-frame stream synchronisation.  The switch is argmax_j T[c_p, j] / E[p, j]
+  // (k_switch), and every input is on the host once the previous resample's classes are:
+  // k_small_resample also writes them into mapped memory (cls_pin), so the host computes the
+  // same counts with the same fp64 divisions and comparisons while the kernels run.  The
+  // device's own counts still land in cnt_pin and are compared at the next synchronisation
+  // (a mismatch is an error, never a silent divergence).
+  int* cls_pin = nullptr;             // mapped: the current classes (valid when cls_host_ok)
+  int* cls_pdev = nullptr;
+  bool cls_host_ok = false;           // cls_pin holds the classes the next switch reads
+  bool cls_ev_pending = false;        // ... once cls_ev (after the resample that wrote them) is done
+  hipEvent_t cls_ev = nullptr;
+  hipEvent_t cnt_ev = nullptr;        // after the switch whose device counts cnt_expect awaits
+  std::vector<double> T_host;         // C x C
+  int cnt_expect[kMaxClasses] = {0};
+  bool cnt_check = false;             // compare cnt_pin with cnt_expect at the next sync
   // read-outs written by the resampling kernels straight into mapped host memory as well
   // (small read-out tables): gpmdm_pf_read then needs no copy launch, only the stream sync
   double* ro_pin = nullptr;
@@ -330,6 +352,9 @@ struct gpmdm_pf {
     for (auto ev : pool) (void)hipEventDestroy(ev);
     if (rpin) (void)hipHostFree(rpin);
     if (cnt_pin) (void)hipHostFree(cnt_pin);
+    if (cls_pin) (void)hipHostFree(cls_pin);
+    if (cls_ev) (void)hipEventDestroy(cls_ev);
+    if (cnt_ev) (void)hipEventDestroy(cnt_ev);
     if (ro_pin) (void)hipHostFree(ro_pin);
     for (int k = 0; k < 2; ++k) {
       if (zpin[k]) (void)hipHostFree(zpin[k]);
@@ -732,6 +757,18 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
       return fail(GPMDM_E_NOMEM, "pinned class-count buffer");
     }
     pf->cnt_dev = (int*)cv;
+    if (F == 1 && n_ranks == 1 && P <= kHostCountsMaxP) {
+      void* lv = nullptr;
+      if (hipHostMalloc((void**)&pf->cls_pin, sizeof(int) * P, fl) != hipSuccess ||
+          hipHostGetDevicePointer(&lv, pf->cls_pin, 0) != hipSuccess ||
+          hipEventCreateWithFlags(&pf->cls_ev, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&pf->cnt_ev, hipEventDisableTiming) != hipSuccess) {
+        delete pf;
+        return fail(GPMDM_E_NOMEM, "pinned class buffer");
+      }
+      pf->cls_pdev = (int*)lv;
+      pf->T_host.assign(T, T + (size_t)C * C);
+    }
   }
   pf->obs_img = &obs_pick(m, pf->Pf, pf->nloc, pf->obs_geo);
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, pf->obs_geo.pt())};
@@ -827,6 +864,19 @@ static int flush_ll(gpmdm_pf* pf, hipStream_t s) {
   return GPMDM_OK;
 }
 
+// The device's class counts of the last host-counted switch (checked by the next one, after
+// the resample that followed it): they must equal the host's (same inputs, same fp64
+// operations); a difference is reported as an error, never used.
+static int check_counts(gpmdm_pf* pf) {
+  if (!pf->cnt_check) return GPMDM_OK;
+  HIPCHK(hipEventSynchronize(pf->cnt_ev));   // done: it precedes the resample already waited for
+  pf->cnt_check = false;
+  for (int c = 0; c < pf->m->C; ++c)
+    if (pf->cnt_pin[c] != pf->cnt_expect[c])
+      return fail(GPMDM_E_STATE, "host and device class counts of the switch differ");
+  return GPMDM_OK;
+}
+
 int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   CHECK(pf && states && classes, "null argument");
   gpmdm_model* m = pf->m;
@@ -839,6 +889,11 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   }
   HIPCHK(hipMemcpy(pf->X, states, sizeof(double) * P * m->d, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(pf->cls, c32.data(), sizeof(int) * P, hipMemcpyHostToDevice));
+  if (pf->cls_pin) {
+    std::memcpy(pf->cls_pin, c32.data(), sizeof(int) * P);
+    pf->cls_host_ok = true;
+    pf->cls_ev_pending = false;
+  }
   for (long long i = 0; i < P; ++i) c32[i] = (int)(i % pf->Pf);   // no shared ancestors yet
   HIPCHK(hipMemcpy(pf->ridx, c32.data(), sizeof(int) * P, hipMemcpyHostToDevice));
   HIPCHK(hipMemset(pf->ll, 0, sizeof(double) * P));
@@ -954,11 +1009,40 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
     la.slot = pf->slot;
   }
   sc.counts_host = class_counts ? pf->cnt_dev : nullptr;   // the counts straight to the host
+  // the counts on the host (cls_pin): no wait for this switch
+  // (GPMDM_NO_HOST_COUNTS=1: the device counts and the synchronisation, for A/B tests)
+  static const bool no_host_counts = std::getenv("GPMDM_NO_HOST_COUNTS") != nullptr;
+  const bool host_counts =
+      class_counts && pf->rng_mode == GPMDM_RNG_REPLAY && pf->cls_host_ok && !sl && !no_host_counts;
+  if (host_counts) {
+    if (pf->cls_ev_pending) {          // the resample that wrote cls_pin (normally done: read)
+      HIPCHK(hipEventSynchronize(pf->cls_ev));
+      pf->cls_ev_pending = false;
+    }
+    TRY(check_counts(pf));
+    int cnt[kMaxClasses] = {0};
+    for (long long p = 0; p < pf->P; ++p) {  // k_switch's argmax, the same fp64 operations
+      const double* Tr = pf->T_host.data() + (size_t)pf->cls_pin[p] * C;
+      const double* Ep = E + p * C;
+      int best = 0;
+      double bestv = -INFINITY;
+      for (int j = 0; j < C; ++j) {
+        const double v = Tr[j] / Ep[j];
+        if (v > bestv) { bestv = v; best = j; }
+      }
+      ++cnt[best];
+    }
+    for (int c = 0; c < C; ++c) pf->cnt_expect[c] = cnt[c];
+  }
   launch_switch_group(sa, sc, ga, sa.owner ? &la : nullptr, s);
   pf->mark_end(s, GPMDM_STAGE_SWITCH, t0);
   HIPCHK(hipGetLastError());
   if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(0, s));
-  if (class_counts) {
+  if (host_counts) {
+    HIPCHK(hipEventRecord(pf->cnt_ev, s));
+    pf->cnt_check = true;
+    for (int c = 0; c < C; ++c) class_counts[c] = pf->cnt_expect[c];
+  } else if (class_counts) {
     int tmp[kMaxClasses];
     const int* src = pf->cnt_pin;
     if (!sc.counts_host) {
@@ -1375,7 +1459,14 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   pf->mark_begin(s, GPMDM_STAGE_RESAMPLE, t0);
   ResampleArgs ra = resample_args(pf);
   ra.U = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->rep_src[2] : nullptr;
+  const bool cls_host = pf->cls_pin && small_resample_ok(norm_args(pf), ra);
+  if (cls_host) ra.cls_host = pf->cls_pdev;
   launch_normalise_resample(norm_args(pf), ra, s);
+  pf->cls_host_ok = cls_host;
+  if (cls_host) {
+    HIPCHK(hipEventRecord(pf->cls_ev, s));
+    pf->cls_ev_pending = true;
+  }
   pf->ll_pending = false;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(2, s));
   // next frame's ownership order (identical on every rank: same replicated ancestors)

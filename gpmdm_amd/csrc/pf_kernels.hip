@@ -1101,6 +1101,7 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
     if (!a.identity) {
       a.ridx[g0 + p] = (int)idx;
       a.cls_dst[g0 + p] = cnew;
+      if (a.cls_host) a.cls_host[g0 + p] = cnew;
       for (int j = 0; j < d; ++j) a.X_dst[(g0 + p) * d + j] = a.X_src[(g0 + idx) * d + j];
     }
     const double llv = llp;

@@ -1,8 +1,9 @@
 """GPU: the one-launch paths of small filters (pf_kernels.hip: k_small_switch -- switch, class
 scan, grouping, leader compaction -- for P <= 1024 particles on one shard, k_small_resample
 -- normalise, resample, read-out -- for P <= 1024 per filter) are bitwise the multi-kernel
-path (GPMDM_NO_SMALL_PATH=1), and the observation GP's 16-row tiles (capi.hip obs_run_geo)
-are bitwise its 32-row tiles: replay and Philox draws, multinomial and systematic
+path (GPMDM_NO_SMALL_PATH=1), the observation GP's 16-row tiles (capi.hip obs_run_geo)
+are bitwise its 32-row tiles, and a small replay filter's class counts computed on the host
+(no mid-frame sync) are the device's (GPMDM_NO_HOST_COUNTS=1): replay and Philox draws, multinomial and systematic
 resampling, with and without ancestor de-duplication, a bank of filters, several frames.
 The environment switches are read once per process, so each configuration runs in its own
 child process (one at a time)."""
@@ -33,7 +34,9 @@ for name, P, rng, res, dd in (("replay100", 100, "torch", "multinomial", True),
                               ("sys777", 777, "philox", "systematic", True),
                               ("one", 1, "philox", "multinomial", True),
                               ("big1500", 1500, "philox", "multinomial", True),
-                              ("philox20k", 20000, "philox", "multinomial", True)):
+                              ("philox20k", 20000, "philox", "multinomial", True),
+                              ("replay1024sys", 1024, "torch", "systematic", True),
+                              ("replay1025", 1025, "torch", "multinomial", True)):
     torch.manual_seed(3)
     pf = GPMDM_PF(m, T, P, rng=rng, seed=9 if rng == "philox" else None, resample=res, dedup=dd)
     for k in range(4):
@@ -45,6 +48,14 @@ for name, P, rng, res, dd in (("replay100", 100, "torch", "multinomial", True),
     st = pf.export_state()
     for key in ("states", "classes", "ll", "w", "resample_idx"):
         out[f"{name}_{key}"] = st[key]
+# replay updates with no read-out between them: the host class counts wait for the
+# previous resample themselves (capi.hip gpmdm_pf::cls_ev)
+torch.manual_seed(4)
+pf = GPMDM_PF(m, T, 300, rng="torch")
+for k in range(5):
+    pf.update(Y[70 + 3 * k] + 0.01)
+out["unread_post"] = pf.class_probabilities().numpy()
+out["unread_states"] = pf.export_state()["states"]
 bank = GPMDM_PF_Bank(m, T, 3, 300, seed=5)
 for k in range(3):
     bank.update(np.stack([Y[10 * i + k] for i in range(3)]))
@@ -70,10 +81,13 @@ def test_small_path_is_bitwise_the_multi_kernel_path(tmp_path):
     fused = _run(tmp_path, "fused", {})
     multi = _run(tmp_path, "multi", {"GPMDM_NO_SMALL_PATH": "1", "GPMDM_OBS_SMALL_TILES": "0"})
     tiles16 = _run(tmp_path, "tiles16", {"GPMDM_OBS_SMALL_TILES": "1"})
-    assert fused.keys() == multi.keys() == tiles16.keys()
+    # replay filters' class counts from the device with a mid-frame sync, not the host
+    devcounts = _run(tmp_path, "devcounts", {"GPMDM_NO_HOST_COUNTS": "1"})
+    assert fused.keys() == multi.keys() == tiles16.keys() == devcounts.keys()
     for k in fused:
         assert np.array_equal(fused[k], multi[k]), k
         assert np.array_equal(fused[k], tiles16[k]), k
+        assert np.array_equal(fused[k], devcounts[k]), k
 
 
 def test_deferred_likelihood_is_flushed_for_an_early_reader():
