@@ -312,6 +312,22 @@ struct gpmdm_pf {
     cstream = nullptr;
     comm = nullptr;                    // the caller owns the communicator
   }
+  // Pre-switch (Philox filters): the next frame's class switch needs no host input (its
+  // draws are keyed by the frame counter), so the resample launches it right behind the
+  // read-out; it runs while the host takes the frame's outputs, and gpmdm_pf_switch then
+  // only consumes it.  Every later call that reads or rewrites the switch's tables, or must
+  // see the filter between frames (predict, set_*, init), drops it first, and the next
+  // gpmdm_pf_switch launches it again -- the same draws, bitwise the same tables.  The
+  // normaliser-maximum reset and the dynamics row count moved out of the switch into
+  // k_dyn_finish, so nothing a between-frames reader sees changes.  GPMDM_NO_PRESWITCH=1
+  // turns it off (A/B).
+  bool preswitch = true;
+  bool preswitched = false;           // launched, not yet consumed by gpmdm_pf_switch
+  hipEvent_t sw_ev = nullptr;         // after the pre-switch
+  hipStream_t sw_stream = nullptr;
+  hipEvent_t ro_ev = nullptr;         // after the last read-out (gpmdm_pf_read waits on it)
+  bool ro_ev_ok = false;
+  int* rows_last() const { return small + 504; }   // rows of the last dynamics pass
   // timing
   bool timing = false;
   std::vector<hipEvent_t> pool;
@@ -336,6 +352,7 @@ struct gpmdm_pf {
   const int* own_order() const { return own_valid ? own : nullptr; }
 
   ~gpmdm_pf() {
+    if (sw_ev) (void)hipEventSynchronize(sw_ev);   // a pre-switch may still use the buffers
     release_comm();
     double* ds[] = {T, X, X_prop, ll, qdyn, mudyn, qobs, sobs, z, E, normals, U,
                     e, local, blocksum, blockoffw, total, cum, partials, readout,
@@ -355,6 +372,8 @@ struct gpmdm_pf {
     if (cls_pin) (void)hipHostFree(cls_pin);
     if (cls_ev) (void)hipEventDestroy(cls_ev);
     if (cnt_ev) (void)hipEventDestroy(cnt_ev);
+    if (sw_ev) (void)hipEventDestroy(sw_ev);
+    if (ro_ev) (void)hipEventDestroy(ro_ev);
     if (ro_pin) (void)hipHostFree(ro_pin);
     for (int k = 0; k < 2; ++k) {
       if (zpin[k]) (void)hipHostFree(zpin[k]);
@@ -770,11 +789,18 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
       pf->T_host.assign(T, T + (size_t)C * C);
     }
   }
+  if (hipEventCreateWithFlags(&pf->sw_ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&pf->ro_ev, hipEventDisableTiming) != hipSuccess) {
+    delete pf;
+    return fail(GPMDM_E_HIP, "filter events");
+  }
+  pf->preswitch = rng_mode == GPMDM_RNG_PHILOX && std::getenv("GPMDM_NO_PRESWITCH") == nullptr;
   pf->obs_img = &obs_pick(m, pf->Pf, pf->nloc, pf->obs_geo);
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, pf->obs_geo.pt())};
   if (hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(pf->T, T, sizeof(double) * C * C, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(pf->health, 0, sizeof(unsigned) * kHealthN) != hipSuccess) {
+      hipMemset(pf->health, 0, sizeof(unsigned) * kHealthN) != hipSuccess ||
+      hipMemset(pf->small, 0, sizeof(int) * 512) != hipSuccess) {
     delete pf;
     return fail(GPMDM_E_HIP, "upload of particle-filter tables failed");
   }
@@ -864,6 +890,20 @@ static int flush_ll(gpmdm_pf* pf, hipStream_t s) {
   return GPMDM_OK;
 }
 
+// Undo a pre-switch before a call that reads or rewrites the switch's tables or needs the
+// filter between frames: the caller's stream (or, with none, the host) waits for it, and
+// the next gpmdm_pf_switch launches the switch again (same draws: the same tables).
+static int drop_preswitch(gpmdm_pf* pf, hipStream_t s, bool host_wait) {
+  if (!pf->preswitched) return GPMDM_OK;
+  if (host_wait)
+    HIPCHK(hipEventSynchronize(pf->sw_ev));
+  else if (s != pf->sw_stream)
+    HIPCHK(hipStreamWaitEvent(s, pf->sw_ev, 0));
+  pf->preswitched = false;
+  pf->switched = false;
+  return GPMDM_OK;
+}
+
 // The device's class counts of the last host-counted switch (checked by the next one, after
 // the resample that followed it): they must equal the host's (same inputs, same fp64
 // operations); a difference is reported as an error, never used.
@@ -881,6 +921,7 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   CHECK(pf && states && classes, "null argument");
   gpmdm_model* m = pf->m;
   HIPCHK(hipSetDevice(m->device));
+  TRY(drop_preswitch(pf, nullptr, true));
   const long long P = pf->P;
   std::vector<int> c32(P);
   for (long long i = 0; i < P; ++i) {
@@ -906,19 +947,17 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   ra.X_src = pf->X;
   launch_normalise_resample(norm_args(pf), ra, nullptr);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(pf->ro_ev, nullptr));
   HIPCHK(hipDeviceSynchronize());
+  pf->ro_ev_ok = true;
   pf->initialised = true;
   pf->own_valid = false;               // no ancestors yet: identity ownership
   pf->switched = pf->propagated = pf->dyn_done = pf->ll_pending = false;
   return GPMDM_OK;
 }
 
-int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void* stream) {
-  CHECK(pf, "null handle");
-  if (!pf->initialised) return fail(GPMDM_E_STATE, "particle filter not initialised");
+static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipStream_t s) {
   gpmdm_model* m = pf->m;
-  hipStream_t s = (hipStream_t)stream;
-  HIPCHK(hipSetDevice(m->device));
   const int C = m->C;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
     CHECK(E, "replay mode needs the Exp(1) switch draws");
@@ -948,7 +987,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   sa.T = pf->T;
   sa.E = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->rep_src[0] : nullptr;
   sa.blockcounts = pf->blockcounts;
-  sa.gmax_reset = pf->gmax;
+  sa.gmax_reset = nullptr;             // k_dyn_finish resets the maxima (the switch may run ahead)
   if (pf->dedup && pf->nloc > 0) {
     sa.anc = pf->ridx;
     sa.owner = pf->owner;
@@ -1056,6 +1095,25 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   return GPMDM_OK;
 }
 
+int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void* stream) {
+  CHECK(pf, "null handle");
+  if (!pf->initialised) return fail(GPMDM_E_STATE, "particle filter not initialised");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(pf->m->device));
+  if (pf->preswitched) {               // launched by the last resample: consume it
+    if (s != pf->sw_stream) HIPCHK(hipStreamWaitEvent(s, pf->sw_ev, 0));
+    pf->preswitched = false;
+    if (class_counts) {
+      int tmp[kMaxClasses];
+      HIPCHK(hipMemcpyAsync(tmp, pf->counts(), sizeof(int) * pf->m->C, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      for (int c = 0; c < pf->m->C; ++c) class_counts[c] = tmp[c];
+    }
+    return GPMDM_OK;
+  }
+  return do_switch(pf, E, class_counts, s);
+}
+
 // _propogate_dynamics for this rank's particles (gpmdm_pf.py:153-168): the dynamics GP per
 // class (de-duplicated rows or every particle) and the new states X_prop.
 static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s) {
@@ -1144,8 +1202,20 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
       fa.P = pf->P;
     }
     fa.health = pf->health;
+    fa.gmax_reset = pf->gmax;
+    fa.F = pf->F;
+    fa.rows_b = pf->dedup ? pf->lseg_begin() : pf->seg_begin();
+    fa.rows_e = pf->dedup ? pf->lseg_end() : pf->seg_end();
+    fa.n_rows_seg = C;
+    fa.rows_out = pf->rows_last();
     launch_dyn_finish(fa, s);
     pf->mark_end(s, GPMDM_STAGE_DYN_FINISH, t0);
+  } else {
+    // no particles on this rank: the maxima reset and row count k_dyn_finish would do
+    static const unsigned long long kNegInf[1] = {0x000fffffffffffffull};   // ord_enc(-inf)
+    for (int f = 0; f < pf->F; ++f)
+      HIPCHK(hipMemcpyAsync(pf->gmax + f, kNegInf, sizeof(kNegInf), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(pf->rows_last(), 0, sizeof(int), s));
   }
   HIPCHK(hipGetLastError());
   if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(1, s));
@@ -1285,7 +1355,7 @@ static int propagate_exchange(gpmdm_pf* pf, const double* zh, const double* norm
 
 int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, void* stream) {
   CHECK(pf && zh, "null argument");
-  if (!pf->switched) return fail(GPMDM_E_STATE, "propagate called before switch");
+  if (!pf->switched || pf->preswitched) return fail(GPMDM_E_STATE, "propagate called before switch");
   if (pf->rng_mode == GPMDM_RNG_REPLAY) CHECK(normals, "replay mode needs the dynamics normals");
   HIPCHK(hipSetDevice(pf->m->device));
   if (pf->comm) return propagate_exchange(pf, zh, normals, (hipStream_t)stream);
@@ -1296,6 +1366,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
 int gpmdm_pf_set_comm(gpmdm_pf_t pf, void* rccl_comm, int flags) {
   CHECK(pf, "null handle");
   CHECK((flags & ~GPMDM_COMM_PAD_ROWS) == 0, "bad flags");
+  TRY(drop_preswitch(pf, nullptr, true));
   CHECK(!pf->switched && !pf->propagated, "set_comm between switch and resample");
   HIPCHK(hipSetDevice(pf->m->device));
   pf->release_comm();
@@ -1367,7 +1438,8 @@ int gpmdm_comm_destroy(void* comm) {
 
 int gpmdm_pf_propagate_dynamics(gpmdm_pf_t pf, const double* normals, void* stream) {
   CHECK(pf, "null handle");
-  if (!pf->switched) return fail(GPMDM_E_STATE, "propagate_dynamics called before switch");
+  if (!pf->switched || pf->preswitched)
+    return fail(GPMDM_E_STATE, "propagate_dynamics called before switch");
   if (pf->rng_mode == GPMDM_RNG_REPLAY) CHECK(normals, "replay mode needs the dynamics normals");
   HIPCHK(hipSetDevice(pf->m->device));
   return propagate_dynamics(pf, normals, (hipStream_t)stream);
@@ -1478,8 +1550,16 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   }
   pf->mark_end(s, GPMDM_STAGE_RESAMPLE, t0);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(pf->ro_ev, s));
+  pf->ro_ev_ok = true;
   pf->frame += 1;
   pf->propagated = false;
+  if (pf->preswitch) {                 // the next frame's switch, behind the read-out
+    TRY(do_switch(pf, nullptr, nullptr, s));
+    HIPCHK(hipEventRecord(pf->sw_ev, s));
+    pf->sw_stream = s;
+    pf->preswitched = true;
+  }
   return GPMDM_OK;
 }
 
@@ -1505,8 +1585,12 @@ int gpmdm_pf_read(gpmdm_pf_t pf, double* post, double* mean, double* lik, void* 
   if (!src) {
     HIPCHK(hipMemcpyAsync(pf->rpin, pf->readout, sizeof(double) * pf->F * nr, hipMemcpyDeviceToHost, s));
     src = pf->rpin;
+    HIPCHK(hipStreamSynchronize(s));
+  } else if (pf->ro_ev_ok) {
+    HIPCHK(hipEventSynchronize(pf->ro_ev));   // not the stream: a pre-switch may follow
+  } else {
+    HIPCHK(hipStreamSynchronize(s));
   }
-  HIPCHK(hipStreamSynchronize(s));
   for (int f = 0; f < pf->F; ++f) {
     const double* b = src + (size_t)f * nr;
     if (post) std::memcpy(post + (size_t)f * m->C, b, sizeof(double) * m->C);
@@ -1557,6 +1641,7 @@ int gpmdm_pf_export(gpmdm_pf_t pf, double* states, int64_t* classes, double* ll,
 
 int gpmdm_pf_set_dedup(gpmdm_pf_t pf, int enable) {
   CHECK(pf, "null handle");
+  TRY(drop_preswitch(pf, nullptr, true));
   if (pf->switched || pf->dyn_done) return fail(GPMDM_E_STATE, "set_dedup between switch and propagate");
   pf->dedup = enable != 0;
   return GPMDM_OK;
@@ -1566,6 +1651,7 @@ int gpmdm_pf_set_dyn_tiles(gpmdm_pf_t pf, int mode) {
   CHECK(pf, "null handle");
   CHECK(mode == GPMDM_DYN_TILES_AUTO || mode == GPMDM_DYN_TILES_NARROW || mode == GPMDM_DYN_TILES_WIDE,
         "mode must be GPMDM_DYN_TILES_*");
+  TRY(drop_preswitch(pf, nullptr, true));
   if (pf->switched || pf->dyn_done) return fail(GPMDM_E_STATE, "set_dyn_tiles between switch and propagate");
   pf->dyn_tiles = mode;
   return GPMDM_OK;
@@ -1573,6 +1659,7 @@ int gpmdm_pf_set_dyn_tiles(gpmdm_pf_t pf, int mode) {
 
 int gpmdm_pf_set_shard_order(gpmdm_pf_t pf, int enable) {
   CHECK(pf, "null handle");
+  TRY(drop_preswitch(pf, nullptr, true));
   if (pf->switched || pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "set_shard_order inside a step");
   pf->shard_order = enable != 0;
   if (!pf->shard_order) pf->own_valid = false;
@@ -1582,14 +1669,10 @@ int gpmdm_pf_set_shard_order(gpmdm_pf_t pf, int enable) {
 int gpmdm_pf_dyn_rows(gpmdm_pf_t pf, int64_t* rows, void* stream) {
   CHECK(pf && rows, "null argument");
   HIPCHK(hipSetDevice(pf->m->device));
-  const int C = pf->m->C;
-  int b[kMaxClasses], e[kMaxClasses];
   hipStream_t s = (hipStream_t)stream;
-  HIPCHK(hipMemcpyAsync(b, pf->dedup ? pf->lseg_begin() : pf->seg_begin(), sizeof(int) * C, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(e, pf->dedup ? pf->lseg_end() : pf->seg_end(), sizeof(int) * C, hipMemcpyDeviceToHost, s));
+  int r = 0;                           // k_dyn_finish's count of the last pass's rows
+  HIPCHK(hipMemcpyAsync(&r, pf->rows_last(), sizeof(int), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  long long r = 0;
-  for (int c = 0; c < C; ++c) r += e[c] - b[c];
   *rows = r;
   return GPMDM_OK;
 }
@@ -1634,6 +1717,7 @@ int gpmdm_pf_frame(gpmdm_pf_t pf, int64_t* frame) {
 
 int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
   CHECK(pf && m, "null argument");
+  TRY(drop_preswitch(pf, nullptr, true));
   if (pf->switched || pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "set_model inside a step");
   gpmdm_model* old = pf->m;
   if (m == old) return GPMDM_OK;
@@ -1694,6 +1778,8 @@ int gpmdm_pf_health(gpmdm_pf_t pf, int64_t* counts, int reset, void* stream) {
 int gpmdm_pf_predict(gpmdm_pf_t pf, double* mean, void* stream) {
   CHECK(pf && mean, "null argument");
   if (!pf->initialised) return fail(GPMDM_E_STATE, "particle filter not initialised");
+  HIPCHK(hipSetDevice(pf->m->device));
+  TRY(drop_preswitch(pf, (hipStream_t)stream, false));   // predict rewrites the grouping scratch
   if (pf->switched || pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "predict inside a step");
   gpmdm_model* m = pf->m;
   HIPCHK(hipSetDevice(m->device));

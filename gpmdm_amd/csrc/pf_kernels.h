@@ -128,6 +128,15 @@ struct DynFinishArgs {
   const int* anc;
   long long P;
   unsigned* health;               // kHealth* counters (PF) or nullptr
+  // PF bookkeeping done by output 0 / outputs < F (not by the switch, which may run ahead:
+  // capi.hip pre-switch): the normaliser maxima reset, and the row count of this dynamics
+  // pass (sum over n_rows_seg segments of rows_e - rows_b) for gpmdm_pf_dyn_rows
+  unsigned long long* gmax_reset; // F maxima, or nullptr
+  int F;
+  const int* rows_b;
+  const int* rows_e;
+  int n_rows_seg;
+  int* rows_out;                  // or nullptr
 };
 
 struct ObsFinishArgs {

@@ -522,6 +522,12 @@ __device__ __forceinline__ int seg_of(const int* seg_out_base, int n_seg, int to
 
 __global__ __launch_bounds__(kB) void k_dyn_finish(DynFinishArgs a) {
   const long long o = (long long)blockIdx.x * kB + threadIdx.x;
+  if (a.gmax_reset && o < a.F) a.gmax_reset[o] = ord_enc(-INFINITY);
+  if (a.rows_out && o == 0) {
+    int r = 0;
+    for (int c = 0; c < a.n_rows_seg; ++c) r += a.rows_e[c] - a.rows_b[c];
+    a.rows_out[0] = r;
+  }
   if (o >= a.n_out) return;
   const int c = a.seg_out_base ? seg_of(a.seg_out_base, a.n_seg, (int)a.n_out, (int)o) : 0;
   const long long pos = (a.seg_pos_begin ? a.seg_pos_begin[c] : 0) + (o - (a.seg_out_base ? a.seg_out_base[c] : 0));

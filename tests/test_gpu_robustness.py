@@ -135,3 +135,14 @@ def test_step_call_order_is_enforced(fx_config1):
     a, b = pfs[0].export_state(), pfs[1].export_state()
     for key in ("states", "classes", "ll", "resample_idx"):
         assert np.array_equal(a[key], b[key]), key
+    # after a resample the next switch is already launched (pre-switch), but the order still
+    # holds: propagate before gpmdm_pf_switch is refused, and the step completes after it
+    assert lib.gpmdm_pf_propagate_dynamics(h, None, s) == _lib.GPMDM_E_STATE
+    assert lib.gpmdm_pf_propagate(h, _lib.dptr(z), None, s) == _lib.GPMDM_E_STATE
+    _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
+    _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), None, s), "propagate")
+    _lib.check(lib.gpmdm_pf_resample(h, None, s), "resample")
+    pfs[1].update(z)
+    a, b = pfs[0].export_state(), pfs[1].export_state()
+    for key in ("states", "classes", "ll", "resample_idx"):
+        assert np.array_equal(a[key], b[key]), key

@@ -3,7 +3,9 @@ scan, grouping, leader compaction -- for P <= 1024 particles on one shard, k_sma
 -- normalise, resample, read-out -- for P <= 1024 per filter) are bitwise the multi-kernel
 path (GPMDM_NO_SMALL_PATH=1), the observation GP's 16-row tiles (capi.hip obs_run_geo)
 are bitwise its 32-row tiles, and a small replay filter's class counts computed on the host
-(no mid-frame sync) are the device's (GPMDM_NO_HOST_COUNTS=1): replay and Philox draws, multinomial and systematic
+(no mid-frame sync) are the device's (GPMDM_NO_HOST_COUNTS=1), and a Philox filter whose
+next switch the resample launches ahead (pre-switch) is bitwise one that switches in the next
+update (GPMDM_NO_PRESWITCH=1), with predict / dynamics_rows / export between frames: replay and Philox draws, multinomial and systematic
 resampling, with and without ancestor de-duplication, a bank of filters, several frames.
 The environment switches are read once per process, so each configuration runs in its own
 child process (one at a time)."""
@@ -41,6 +43,8 @@ for name, P, rng, res, dd in (("replay100", 100, "torch", "multinomial", True),
     pf = GPMDM_PF(m, T, P, rng=rng, seed=9 if rng == "philox" else None, resample=res, dedup=dd)
     for k in range(4):
         pf.update(Y[50 + 9 * k] + 0.01)
+        if k == 1:                           # between frames: drops a pre-switch (capi.hip)
+            out[f"{name}_{k}_pred"] = pf.predict().numpy()
         out[f"{name}_{k}_post"] = pf.class_probabilities().numpy()
         out[f"{name}_{k}_mean"] = pf.current_state_mean().numpy()
         out[f"{name}_{k}_lik"] = np.array([pf.log_likelihood()])
@@ -83,11 +87,14 @@ def test_small_path_is_bitwise_the_multi_kernel_path(tmp_path):
     tiles16 = _run(tmp_path, "tiles16", {"GPMDM_OBS_SMALL_TILES": "1"})
     # replay filters' class counts from the device with a mid-frame sync, not the host
     devcounts = _run(tmp_path, "devcounts", {"GPMDM_NO_HOST_COUNTS": "1"})
-    assert fused.keys() == multi.keys() == tiles16.keys() == devcounts.keys()
+    # Philox filters' next switch launched by the resample (pre-switch) or by the next update
+    nopre = _run(tmp_path, "nopre", {"GPMDM_NO_PRESWITCH": "1"})
+    assert fused.keys() == multi.keys() == tiles16.keys() == devcounts.keys() == nopre.keys()
     for k in fused:
         assert np.array_equal(fused[k], multi[k]), k
         assert np.array_equal(fused[k], tiles16[k]), k
         assert np.array_equal(fused[k], devcounts[k]), k
+        assert np.array_equal(fused[k], nopre[k]), k
 
 
 def test_deferred_likelihood_is_flushed_for_an_early_reader():
