@@ -285,6 +285,12 @@ struct gpmdm_pf {
   size_t pred_q_cap = 0;
   double *z = nullptr, *E = nullptr, *normals = nullptr, *U = nullptr;
   unsigned long long* gmax = nullptr;
+  // single filters: k_obs_ll's per-block maxima of ll, read by the normaliser in place of
+  // k_norm_max (bmax_ready: produced by this frame's weigh, not yet consumed)
+  unsigned long long* bmax = nullptr;
+  bool bmax_ready = false;
+  // the leader election's owner table is all 0xffffffff (the last compaction restored it)
+  bool owner_clean = false;
   double *e = nullptr, *local = nullptr, *blocksum = nullptr, *blockoffw = nullptr, *total = nullptr,
          *cum = nullptr, *partials = nullptr, *readout = nullptr;
   // library-driven exchange (gpmdm_pf_set_comm): an RCCL communicator of n_ranks ranks, a
@@ -363,6 +369,7 @@ struct gpmdm_pf {
     for (int* p : is) dfree(p);
     dfree(own_tmp);
     dfree(gmax);
+    dfree(bmax);
     dfree(owner);
     dfree(health);
     for (auto& r : recs) { pool.push_back(r.a); pool.push_back(r.b); }
@@ -709,6 +716,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
     ALLOC(U, P);
   }
   ALLOC(gmax, F);
+  if (F == 1 && n_ranks == 1) ALLOC(bmax, pf->nb);
   ALLOC(e, P);
   ALLOC(local, P);
   ALLOC(blocksum, F * pf->nbf);
@@ -879,6 +887,7 @@ static NormArgs norm_args(gpmdm_pf* pf) {
     na.obs = pf->oa_pending;
     na.obs_pending = 1;
   }
+  if (pf->bmax_ready) na.bmax = pf->bmax;
   return na;
 }
 
@@ -922,6 +931,7 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   gpmdm_model* m = pf->m;
   HIPCHK(hipSetDevice(m->device));
   TRY(drop_preswitch(pf, nullptr, true));
+  pf->bmax_ready = false;
   const long long P = pf->P;
   std::vector<int> c32(P);
   for (long long i = 0; i < P; ++i) {
@@ -1046,6 +1056,7 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
     la.lseg_tile_start = pf->lseg_tiles();
     la.lperm = pf->lperm;
     la.slot = pf->slot;
+    la.owner_reset = pf->owner;        // restores the preset for the next election
   }
   sc.counts_host = class_counts ? pf->cnt_dev : nullptr;   // the counts straight to the host
   // the counts on the host (cls_pin): no wait for this switch
@@ -1073,7 +1084,8 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
     }
     for (int c = 0; c < C; ++c) pf->cnt_expect[c] = cnt[c];
   }
-  launch_switch_group(sa, sc, ga, sa.owner ? &la : nullptr, s);
+  const bool small_path = launch_switch_group(sa, sc, ga, sa.owner ? &la : nullptr, !pf->owner_clean, s);
+  if (sa.owner) pf->owner_clean = !small_path;   // the small path presets in-kernel, leaves it dirty
   pf->mark_end(s, GPMDM_STAGE_SWITCH, t0);
   HIPCHK(hipGetLastError());
   if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(0, s));
@@ -1290,10 +1302,15 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     oa.own = pf->own_order();
     oa.health = pf->health;
     pf->ll_pending = false;
+    pf->bmax_ready = false;
     if (pf->n_ranks == 1 && !oa.own && oa.ll_offset == 0 && small_resample_ok(norm_args(pf), resample_args(pf))) {
       pf->oa_pending = oa;             // computed by the resampling launch (or flush_ll)
       pf->ll_pending = true;
     } else {
+      if (pf->bmax && !oa.own && oa.ll_offset == 0) {   // single filter: the maxima for k_norm_exp_scan
+        oa.bmax = pf->bmax;
+        pf->bmax_ready = true;
+      }
       launch_obs_finish(oa, s);
     }
     pf->mark_end(s, GPMDM_STAGE_OBS_FINISH, t0);
@@ -1534,6 +1551,7 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   const bool cls_host = pf->cls_pin && small_resample_ok(norm_args(pf), ra);
   if (cls_host) ra.cls_host = pf->cls_pdev;
   launch_normalise_resample(norm_args(pf), ra, s);
+  pf->bmax_ready = false;
   pf->cls_host_ok = cls_host;
   if (cls_host) {
     HIPCHK(hipEventRecord(pf->cls_ev, s));

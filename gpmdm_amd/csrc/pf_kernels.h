@@ -102,6 +102,8 @@ struct LeadArgs {
   int* lseg_tile_start;           // [C + 1]
   int* lperm;                     // leader row -> particle
   int* slot;                      // C x P: key -> leader row
+  unsigned* owner_reset;          // owner table to restore to 0xffffffff at each leader's key
+                                  // (every registered key has one leader), or nullptr
 };
 
 struct DynFinishArgs {
@@ -159,6 +161,9 @@ struct ObsFinishArgs {
   int jm0, n_j;
   double sum_log_il2;             // sum_j log il2_j
   unsigned* health;               // kHealth* counters (PF) or nullptr
+  // single filters: the maximum of each block's ll (ord_enc keys), which the normaliser
+  // reads instead of running k_norm_max (nullptr: not produced)
+  unsigned long long* bmax;
 };
 
 // Normalisation and resampling run per filter: grid (nb, F), nb blocks of 256 per filter.
@@ -177,6 +182,8 @@ struct NormArgs {
   // kernel computes ll itself first, the multi-kernel path launches k_obs_ll first
   ObsFinishArgs obs;
   int obs_pending;
+  // k_obs_ll's block maxima of ll (single filters, nb keys): the maximum without k_norm_max
+  const unsigned long long* bmax;
 };
 
 struct ResampleArgs {
@@ -247,8 +254,11 @@ void launch_normalise(const NormArgs& a, hipStream_t s);
 void launch_resample(const ResampleArgs& a, hipStream_t s);
 void launch_normalise_resample(const NormArgs& na, const ResampleArgs& ra, hipStream_t s);
 bool small_resample_ok(const NormArgs& na, const ResampleArgs& ra);
-void launch_switch_group(const SwitchArgs& sa, const ScanArgs& sc, const GroupArgs& ga, const LeadArgs* la,
-                         hipStream_t s);
+// returns true when the one-workgroup small path ran (its owner preset leaves the table
+// dirty); owner_preset = false skips the multi-kernel path's preset of a table that the last
+// leader compaction restored (LeadArgs::owner_reset)
+bool launch_switch_group(const SwitchArgs& sa, const ScanArgs& sc, const GroupArgs& ga, const LeadArgs* la,
+                         bool owner_preset, hipStream_t s);
 void launch_pack(const PackArgs& a, hipStream_t s);
 // predict(): per-block class histogram of `cls` (blockcounts nb x C, nb = ceil(P / 256))
 // single-segment tile table {0, n, 0, 0, tiles} at t[0..4] (predictive maps)

@@ -87,11 +87,39 @@ __global__ __launch_bounds__(kB) void k_switch(SwitchArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
+// Exclusive scan of one int per thread over a 1024-thread workgroup: wave shuffles, the 16
+// wave totals scanned by wave 0 -- two barriers instead of a 1024-wide Hillis-Steele's
+// twenty (integer sums: any association gives the same result).  Returns the exclusive
+// prefix of x; *total = the sum over the workgroup.  wtot / wpre: 16 ints of LDS each.
+__device__ __forceinline__ int block1024_exclusive_scan(int x, int* wtot, int* wpre, int* total) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int v = x;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(v, off);
+    if (lane >= off) v += y;
+  }
+  if (lane == 63) wtot[w] = v;
+  __syncthreads();
+  if (w == 0) {
+    int t = lane < 16 ? wtot[lane] : 0;
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) {
+      const int y = __shfl_up(t, off);
+      if (lane >= off) t += y;
+    }
+    if (lane < 16) wpre[lane] = t;
+  }
+  __syncthreads();
+  *total = wpre[15];
+  return v - x + (w ? wpre[w - 1] : 0);
+}
+
 // One workgroup: exclusive scans of the per-block class counts, class starts, and the
 // segments (grouped position ranges) of this rank's particle slice [lo, hi).
 // (a device function: k_small_switch runs the same body inside its workgroup)
 __device__ __forceinline__ void scan_counts_body(const ScanArgs& a) {
-  __shared__ int part[1024];
+  __shared__ int wtot[16], wpre[16];
   __shared__ int tot[kMaxClasses];
   __shared__ int lo_cnt[kMaxClasses], hi_cnt[kMaxClasses];
   const int tid = threadIdx.x;
@@ -103,15 +131,8 @@ __device__ __forceinline__ void scan_counts_body(const ScanArgs& a) {
       const int b = tid * chunk + i;
       if (b < nb) s += a.blockcounts[(long long)b * a.C + c];
     }
-    part[tid] = s;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {        // Hillis-Steele inclusive scan
-      const int v = tid >= off ? part[tid - off] : 0;
-      __syncthreads();
-      part[tid] += v;
-      __syncthreads();
-    }
-    int run = tid ? part[tid - 1] : 0;
+    int total;
+    int run = block1024_exclusive_scan(s, wtot, wpre, &total);
     for (int i = 0; i < chunk; ++i) {
       const int b = tid * chunk + i;
       if (b < nb) {
@@ -119,9 +140,9 @@ __device__ __forceinline__ void scan_counts_body(const ScanArgs& a) {
         run += a.blockcounts[(long long)b * a.C + c];
       }
     }
-    if (tid == 1023) tot[c] = part[1023];
-    __syncthreads();
+    if (tid == 0) tot[c] = total;
   }
+  __syncthreads();
   // counts of each class among particles [0, lo) and [0, hi)
   if (tid < a.C) { lo_cnt[tid] = 0; hi_cnt[tid] = 0; }
   __syncthreads();
@@ -224,7 +245,7 @@ __global__ __launch_bounds__(kB) void k_lead_flags(LeadArgs a) {
 
 // One workgroup: lblock -> exclusive offsets (in place), then the leader segment tables.
 __device__ __forceinline__ void lead_tables_body(const LeadArgs& a) {
-  __shared__ int part[1024];
+  __shared__ int wtot[16], wpre[16];
   __shared__ int total;
   const int tid = threadIdx.x;
   const int nb = a.nb;
@@ -234,15 +255,8 @@ __device__ __forceinline__ void lead_tables_body(const LeadArgs& a) {
     const int b = tid * chunk + i;
     if (b < nb) s += a.lblock[b];
   }
-  part[tid] = s;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const int v = tid >= off ? part[tid - off] : 0;
-    __syncthreads();
-    part[tid] += v;
-    __syncthreads();
-  }
-  int run = tid ? part[tid - 1] : 0;
+  int tsum;
+  int run = block1024_exclusive_scan(s, wtot, wpre, &tsum);
   for (int i = 0; i < chunk; ++i) {
     const int b = tid * chunk + i;
     if (b < nb) {
@@ -251,7 +265,7 @@ __device__ __forceinline__ void lead_tables_body(const LeadArgs& a) {
       run += cnt;
     }
   }
-  if (tid == 1023) total = part[1023];
+  if (tid == 0) total = tsum;
   __syncthreads();
   if (tid == 0) {
     auto row = [&](long long x) { return x >= a.npos ? total : a.lblock[x / kB] + (a.lflag_scan[x] >> 1); };
@@ -278,7 +292,9 @@ __global__ __launch_bounds__(kB) void k_lead_compact(LeadArgs a) {
   const int r = a.lblock[blockIdx.x] + (v >> 1);
   const long long f = p / a.Pf;
   a.lperm[r] = (int)p;
-  a.slot[(long long)a.cls_new[p] * a.P + f * a.Pf + a.anc[p]] = r;
+  const long long key = (long long)a.cls_new[p] * a.P + f * a.Pf + a.anc[p];
+  a.slot[key] = r;
+  if (a.owner_reset) a.owner_reset[key] = 0xffffffffu;   // the next election's preset
 }
 
 
@@ -632,13 +648,34 @@ __device__ __forceinline__ double obs_ll_value(const ObsFinishArgs& a, long long
 
 __global__ __launch_bounds__(kB) void k_obs_ll(ObsFinishArgs a) {
   const long long o = (long long)blockIdx.x * kB + threadIdx.x;
-  if (o >= a.n_out) return;
-  double vc;
-  const double llv = obs_ll_value(a, o, vc);
-  a.ll[a.own ? a.own[a.ll_offset + o] : a.ll_offset + o] = llv;
-  if (a.health) {
-    count_event(a.health + kHealthObsVar, !(vc > 0.0));
-    count_event(a.health + kHealthObsLL, !isfinite(llv));
+  unsigned long long key = 0;            // below ord_enc of any double
+  if (o < a.n_out) {
+    double vc;
+    const double llv = obs_ll_value(a, o, vc);
+    a.ll[a.own ? a.own[a.ll_offset + o] : a.ll_offset + o] = llv;
+    if (a.health) {
+      count_event(a.health + kHealthObsVar, !(vc > 0.0));
+      count_event(a.health + kHealthObsLL, !isfinite(llv));
+    }
+    key = ord_enc(fmax(-INFINITY, llv));  // k_norm_max's value set: NaN ignored
+  }
+  if (a.bmax) {
+    // the block's maximum as an integer key: the max of a set in ord_enc's total order
+    // does not depend on how the set is split, so k_norm_exp_scan's max over the block
+    // maxima is k_norm_max's atomicMax result exactly
+    __shared__ unsigned long long wk[kB / 64];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned long long y = __shfl_xor(key, off);
+      key = y > key ? y : key;
+    }
+    if ((threadIdx.x & 63) == 0) wk[threadIdx.x >> 6] = key;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long m = wk[0];
+      for (int i = 1; i < kB / 64; ++i) m = wk[i] > m ? wk[i] : m;
+      a.bmax[blockIdx.x] = m;
+    }
   }
 }
 
@@ -664,10 +701,30 @@ __global__ __launch_bounds__(kB) void k_norm_max(NormArgs a) {
 // e = exp(ll - max); block-local inclusive scan of e; block sums.
 __global__ __launch_bounds__(kB) void k_norm_exp_scan(NormArgs a) {
   __shared__ double wsum[kB / 64];
+  __shared__ unsigned long long wk[kB / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const long long f = blockIdx.y;
   const long long p = (long long)blockIdx.x * kB + tid;
-  const double M = ord_dec(a.gmax[f]);
+  double M;
+  if (a.bmax) {
+    // single filter: the maximum over k_obs_ll's block maxima (no k_norm_max launch); every
+    // block computes it, block 0 publishes it for the resample and export
+    unsigned long long key = 0;
+    for (int i = tid; i < a.nb; i += kB) key = a.bmax[i] > key ? a.bmax[i] : key;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const unsigned long long y = __shfl_xor(key, off);
+      key = y > key ? y : key;
+    }
+    if (lane == 0) wk[w] = key;
+    __syncthreads();
+    key = wk[0];
+    for (int i = 1; i < kB / 64; ++i) key = wk[i] > key ? wk[i] : key;
+    if (blockIdx.x == 0 && tid == 0) a.gmax[f] = key;
+    M = ord_dec(key);
+  } else {
+    M = ord_dec(a.gmax[f]);
+  }
   const double e = p < a.P ? exp(a.ll[f * a.P + p] - M) : 0.0;
   if (p < a.P) a.e[f * a.P + p] = e;
   double x = e;                               // wave inclusive scan
@@ -1288,20 +1345,21 @@ void launch_group(const GroupArgs& a, hipStream_t s) {
 // switch + class scan + grouping (+ leader compaction with `la`): one launch for a small
 // single-shard filter (k_small_switch, the same tables), the multi-kernel path otherwise.
 // The owner preset of the leader election is part of either path.
-void launch_switch_group(const SwitchArgs& sa, const ScanArgs& sc, const GroupArgs& ga, const LeadArgs* la,
-                         hipStream_t s) {
+bool launch_switch_group(const SwitchArgs& sa, const ScanArgs& sc, const GroupArgs& ga, const LeadArgs* la,
+                         bool owner_preset, hipStream_t s) {
   static const bool no_small = std::getenv("GPMDM_NO_SMALL_PATH") != nullptr;
   if (!no_small && sa.P <= kSmallSwitchP && sa.n == sa.P && sa.base == 0 && !sa.own && sa.n > 0 &&
       (la == nullptr) == (sa.owner == nullptr) && (la == nullptr || la->npos == sa.P)) {
     LeadArgs l = la ? *la : LeadArgs{};
     hipLaunchKernelGGL(k_small_switch, dim3(1), dim3(1024), 0, s, sa, sc, ga, l, la ? 1 : 0);
-    return;
+    return true;
   }
-  if (la) (void)hipMemsetAsync(sa.owner, 0xff, sizeof(unsigned) * (size_t)sa.C * sa.P, s);
+  if (la && owner_preset) (void)hipMemsetAsync(sa.owner, 0xff, sizeof(unsigned) * (size_t)sa.C * sa.P, s);
   launch_switch(sa, s);
   launch_scan_counts(sc, s);
   launch_group(ga, s);
   if (la) launch_lead(*la, s);
+  return false;
 }
 void launch_lead(const LeadArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_lead_flags, dim3((unsigned)a.nb), dim3(kB), 0, s, a);
@@ -1321,7 +1379,7 @@ void launch_obs_finish(const ObsFinishArgs& a, hipStream_t s) {
 void launch_normalise(const NormArgs& a, hipStream_t s) {
   const dim3 g(nblk(a.P, kB), (unsigned)a.F);
   const unsigned nbm = nblk(a.P, kB) < kMaxNormBlocks ? nblk(a.P, kB) : kMaxNormBlocks;
-  hipLaunchKernelGGL(k_norm_max, dim3(nbm, (unsigned)a.F), dim3(kB), 0, s, a);
+  if (!a.bmax) hipLaunchKernelGGL(k_norm_max, dim3(nbm, (unsigned)a.F), dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_norm_exp_scan, g, dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_norm_total, dim3((unsigned)a.F), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(k_cdf, g, dim3(kB), 0, s, a);
