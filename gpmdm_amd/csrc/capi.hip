@@ -276,6 +276,7 @@ struct gpmdm_pf {
   int* cnt_dev = nullptr;
   hipEvent_t zev[2] = {nullptr, nullptr};
   int zslot = 0;
+  bool z_staged = false;              // zpin[zslot] holds the frame's z, k_dyn_finish copies it
   double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *sobs = nullptr;
   int nparts_dyn_max = 0;
   // failure detection: kHealth* counters, device, zeroed at create
@@ -1128,7 +1129,9 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
 
 // _propogate_dynamics for this rank's particles (gpmdm_pf.py:153-168): the dynamics GP per
 // class (de-duplicated rows or every particle) and the new states X_prop.
-static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s) {
+// zstage: the frame's observation, already in the mapped staging slot zpin[zslot] (the
+// one-call propagate): k_dyn_finish copies it to pf->z, and weigh skips its copy launch.
+static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s, bool zstage = false) {
   gpmdm_model* m = pf->m;
   const int C = m->C, d = m->d;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
@@ -1220,6 +1223,12 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
     fa.rows_e = pf->dedup ? pf->lseg_end() : pf->seg_end();
     fa.n_rows_seg = C;
     fa.rows_out = pf->rows_last();
+    if (zstage) {
+      fa.z_src = pf->zdev[pf->zslot];
+      fa.z_dst = pf->z;
+      fa.z_n = (long long)m->D * pf->F;
+      pf->z_staged = true;
+    }
     launch_dyn_finish(fa, s);
     pf->mark_end(s, GPMDM_STAGE_DYN_FINISH, t0);
   } else {
@@ -1247,7 +1256,10 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
   const int zk = pf->zslot;
   const bool zmap = pf->nloc <= 4096 && sizeof(double) * D * pf->F <= 32768;
   const double* zsrc = pf->z;
-  {
+  if (pf->z_staged) {                  // staged by gpmdm_pf_propagate, copied by k_dyn_finish
+    pf->z_staged = false;
+    pf->zslot ^= 1;
+  } else {
     HIPCHK(hipEventSynchronize(pf->zev[zk]));     // the slot's previous readers have run
     std::memcpy(pf->zpin[zk], zh, sizeof(double) * D * pf->F);
     if (zmap)
@@ -1376,8 +1388,19 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
   if (pf->rng_mode == GPMDM_RNG_REPLAY) CHECK(normals, "replay mode needs the dynamics normals");
   HIPCHK(hipSetDevice(pf->m->device));
   if (pf->comm) return propagate_exchange(pf, zh, normals, (hipStream_t)stream);
-  const int rc = propagate_dynamics(pf, normals, (hipStream_t)stream);
-  return rc ? rc : weigh(pf, zh, (hipStream_t)stream);
+  // a large shard's z goes through k_dyn_finish (no copy launch before the observation GP)
+  const int D = pf->m->D;
+  const bool zstage = pf->nloc > 4096 && pf->nloc >= (long long)D * pf->F;
+  if (zstage) {
+    HIPCHK(hipEventSynchronize(pf->zev[pf->zslot]));   // the slot's previous readers have run
+    std::memcpy(pf->zpin[pf->zslot], zh, sizeof(double) * D * pf->F);
+  }
+  const int rc = propagate_dynamics(pf, normals, (hipStream_t)stream, zstage);
+  if (rc) {
+    pf->z_staged = false;
+    return rc;
+  }
+  return weigh(pf, zh, (hipStream_t)stream);
 }
 
 int gpmdm_pf_set_comm(gpmdm_pf_t pf, void* rccl_comm, int flags) {

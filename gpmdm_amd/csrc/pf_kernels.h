@@ -139,6 +139,11 @@ struct DynFinishArgs {
   const int* rows_e;
   int n_rows_seg;
   int* rows_out;                  // or nullptr
+  // the frame's observation copied by outputs < z_n from host-mapped memory to the device
+  // buffer the observation GP reads (no copy launch on the critical path), or z_n = 0
+  const double* z_src;
+  double* z_dst;
+  long long z_n;
 };
 
 struct ObsFinishArgs {

@@ -539,6 +539,7 @@ __device__ __forceinline__ int seg_of(const int* seg_out_base, int n_seg, int to
 __global__ __launch_bounds__(kB) void k_dyn_finish(DynFinishArgs a) {
   const long long o = (long long)blockIdx.x * kB + threadIdx.x;
   if (a.gmax_reset && o < a.F) a.gmax_reset[o] = ord_enc(-INFINITY);
+  if (o < a.z_n) a.z_dst[o] = a.z_src[o];
   if (a.rows_out && o == 0) {
     int r = 0;
     for (int c = 0; c < a.n_rows_seg; ++c) r += a.rows_e[c] - a.rows_b[c];
