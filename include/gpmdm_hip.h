@@ -133,8 +133,13 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes);
 
 /* _propogate_markov_switching  (gpmdm_pf.py:137-151).  exp_draws: P x C host (replay)
  * or NULL (philox).  class_counts: C host, or NULL; when given, the post-switch class
- * counts are copied back synchronously (the replay caller needs them to draw the
- * per-class normals of the next stage). */
+ * counts are returned (the replay caller needs them to draw the per-class normals of the
+ * next stage): a single replay filter of <= 1024 particles counts them on the host from
+ * exp_draws and the classes its last resample left in mapped memory (no stream wait; the
+ * device's counts are checked at the next switch), others copy them back synchronously.
+ * Philox filters: gpmdm_pf_resample already launched the next frame's switch behind its
+ * read-out (its draws need no host input), and this call then only consumes it (the
+ * caller's stream waits on it if it is another stream); the call order is still required. */
 int gpmdm_pf_switch(gpmdm_pf_t pf, const double* exp_draws, int64_t* class_counts,
                     void* stream);
 
@@ -192,7 +197,10 @@ int gpmdm_comm_init(int n_ranks, int rank, const void* id, int device, void** co
 int gpmdm_comm_destroy(void* comm);
 
 /* _update_weights' normalisation + _resample + the read-outs  (gpmdm_pf.py:194-262,
- * 302-312).  uniforms: P host (replay, multinomial), 1 host (replay, systematic) or NULL. */
+ * 302-312).  uniforms: P host (replay, multinomial), 1 host (replay, systematic) or NULL.
+ * Philox filters then launch the next frame's switch on the same stream (see
+ * gpmdm_pf_switch); gpmdm_pf_predict, gpmdm_pf_init and the gpmdm_pf_set_* calls drop it,
+ * and the next gpmdm_pf_switch launches it again (the same draws, the same result). */
 int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream);
 
 /* update(z) in one call  (gpmdm_pf.py:117-135): switch + propagate + resample.
@@ -202,7 +210,9 @@ int gpmdm_pf_step(gpmdm_pf_t pf, const double* z, const double* exp_draws,
                   const double* normals, const double* uniforms, void* stream);
 
 /* class_probabilities() / current_state_mean() / log_likelihood()
- * (gpmdm_pf.py:224-262, 215-222).  Synchronises `stream`; any pointer may be NULL. */
+ * (gpmdm_pf.py:224-262, 215-222).  Waits for the last read-out (an event recorded after it,
+ * so not for a pre-launched switch behind it), or synchronises `stream` when the read-outs
+ * need a copy (banks of more than ~800 filters); any pointer may be NULL. */
 int gpmdm_pf_read(gpmdm_pf_t pf, double* posterior, double* mean, double* lik, void* stream);
 
 /* Export the full particle state to host (any pointer may be NULL): states P x d,

@@ -19,6 +19,6 @@ for r in $(seq "$rounds"); do
   for v in new prev; do
     dir=.; [ $v = prev ] && dir=tools/ab_prev
     (cd $dir && timeout -k 10 240 python -u bench.py $args) > "$out/${v}_$r.json" 2> "$out/${v}_$r.err" || { echo "$v failed"; tail -5 "$out/${v}_$r.err"; exit 1; }
-    python -c "import json,sys;d=json.load(open(sys.argv[1]));st=d['stages_ms_per_step'];print(sys.argv[2], round(d['ms_per_step'],4), '%.4g'%d['value'], 'obs', round(d['roofline']['launch_ms'],4), 'switch', round(st['switch'],4), 'resample', round(st['resample'],4))" "$out/${v}_$r.json" "$v"
+    python -c "import json,sys;d=json.load(open(sys.argv[1]));st=d['stages_ms_per_step'];print(sys.argv[2], round(d['ms_per_step'],4), '%.4g'%d['value'], 'obs', round(d['roofline']['launch_ms'],4), 'switch', round(st['switch'],4), 'dyn', round(st['dyn_gemm'],4), 'resample', round(st['resample'],4))" "$out/${v}_$r.json" "$v"
   done
 done
