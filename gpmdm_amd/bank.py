@@ -90,7 +90,9 @@ class GPMDM_PF_Bank:
             pass
 
     def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        dev = self.device
+        return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(dev.index if dev.index is not None
+                                                                   else torch.cuda.current_device()))
 
     def _sync_model(self):
         """Rebind to the GPMDM's current device image (see GPMDM_PF._sync_model)."""

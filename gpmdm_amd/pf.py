@@ -119,6 +119,11 @@ class GPMDM_PF:
         _lib.check(lib.gpmdm_pf_set_dyn_tiles(h, _lib.DYN_TILES[dyn_tiles]), "dyn_tiles")
         self._readout = None
         self._comm = None
+        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        # read-out landing buffers and their pointers, made once (read per frame)
+        C, d = self.num_classes, self.latent_dim
+        self._ro = (np.zeros(C), np.zeros(d), np.zeros(1))
+        self._ro_ptr = tuple(_lib.dptr(a) for a in self._ro)
         if self._world > 1:
             w, lo, hi = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
             lib.gpmdm_pf_exchange_width(h, ctypes.byref(w), ctypes.byref(lo), ctypes.byref(hi))
@@ -143,7 +148,9 @@ class GPMDM_PF:
 
     # ---- helpers --------------------------------------------------------------
     def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        # the raw handle of the device's current stream (torch.cuda.current_stream builds a
+        # Stream object per call: ~5 us, a visible share of a 0.12 ms notebook frame)
+        return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(self._dev_index))
 
     def _sync_model(self):
         """The reference filter reads its GPMDM's current state on every call
@@ -191,10 +198,16 @@ class GPMDM_PF:
             if self._draws is None:
                 self._draws = replay.FrameDraws(P, C, d, P if self._resample_mode == "multinomial" else 1)
                 self._counts = np.zeros(C, dtype=np.int64)
+                dr = self._draws           # the draws land in place: their pointers are fixed
+                self._draw_ptr = (_lib.dptr(dr.E), _lib.i64ptr(self._counts), _lib.dptr(dr.N), _lib.dptr(dr.U))
             dr, counts = self._draws, self._counts
-            _lib.check(lib.gpmdm_pf_switch(h, _lib.dptr(dr.switch()), _lib.i64ptr(counts), s), "switch")
-            self._propagate(z, dr.dynamics(counts), s)
-            _lib.check(lib.gpmdm_pf_resample(h, _lib.dptr(dr.resample()), s), "resample")
+            pE, pC, pN, pU = self._draw_ptr
+            dr.switch()
+            _lib.check(lib.gpmdm_pf_switch(h, pE, pC, s), "switch")
+            dr.dynamics(counts)
+            self._propagate(z, dr.N, s, pN)
+            dr.resample()
+            _lib.check(lib.gpmdm_pf_resample(h, pU, s), "resample")
         else:
             _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
             self._propagate(z, None, s)
@@ -232,13 +245,13 @@ class GPMDM_PF:
                                                  _lib.GPMDM_COMM_PAD_ROWS if pad_rows else 0), "set_comm")
         self._comm = comm
 
-    def _propagate(self, z, normals, s):
+    def _propagate(self, z, normals, s, normals_ptr=None):
         """gpmdm_pf.py:153-192 for this rank's particles, and on several ranks the exchange:
         the new {class, state} rows are all-gathered while the observation GP runs (they are
         final once the dynamics GP is done), the likelihoods after it -- by the library over
         its communicator (set_comm), or here over the process group / exchange callback."""
         lib, h = _lib.load(), self._h
-        nrm = None if normals is None else _lib.dptr(normals)
+        nrm = normals_ptr if normals_ptr is not None else (None if normals is None else _lib.dptr(normals))
         if self._world == 1 or self._comm is not None:
             _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), nrm, s), "propagate")
             return
@@ -278,10 +291,8 @@ class GPMDM_PF:
 
     def _read(self):
         if self._readout is None:
-            C, d = self.num_classes, self.latent_dim
-            post, mean, lik = np.zeros(C), np.zeros(d), np.zeros(1)
-            _lib.check(_lib.load().gpmdm_pf_read(self._h, _lib.dptr(post), _lib.dptr(mean), _lib.dptr(lik),
-                                                 self._stream()), "read")
+            post, mean, lik = self._ro           # reused buffers: callers get copies
+            _lib.check(_lib.load().gpmdm_pf_read(self._h, *self._ro_ptr, self._stream()), "read")
             self._readout = (post, mean, float(lik[0]))
         return self._readout
 
