@@ -46,6 +46,7 @@ import bench  # noqa: E402
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
     bench.WORKLOAD = bench.workload(2)
+    bench.WORKLOAD["y_lambda"] = 1.0           # the headline (mocap) stream's model
     from gpmdm_amd import GPMDM_PF, synthetic
     dev = torch.device("cuda", 0)
     model, data = bench.build_model(dev)
@@ -88,6 +89,7 @@ def ranks_mode():
     per_rank = next((int(a.split("=")[1]) for a in sys.argv if a.startswith("--per-rank=")), 100_000)
     steps = int(args[0]) if args else 20
     bench.WORKLOAD = bench.workload(2)
+    bench.WORKLOAD["y_lambda"] = 1.0           # the headline (mocap) stream's model
     from gpmdm_amd import GPMDM_PF, synthetic
     dev = torch.device("cuda", 0)
     model, data = bench.build_model(dev)
