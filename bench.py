@@ -74,7 +74,9 @@ WORKLOAD = None
 def workload(cfg):
     from gpmdm_amd import synthetic
     c = synthetic.CONFIGS[cfg]
-    return dict(cfg=cfg, C=c["C"], S=c["S"], L=c["L"], D=c["D"], d=c["d"], P_per_gpu=P_PER_GPU[cfg])
+    # y_lambda: the observation GP's exp(y_log_lambdas) (1.0: the headline's mocap model;
+    # --y-lambda for the spread stream); tools that import bench get the default
+    return dict(cfg=cfg, C=c["C"], S=c["S"], L=c["L"], D=c["D"], d=c["d"], P_per_gpu=P_PER_GPU[cfg], y_lambda=1.0)
 
 
 def log(*a):
