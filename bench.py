@@ -4,6 +4,14 @@
                     [--rng {auto,philox,torch}] [--stream {mocap,predictive}] [--y-lambda L]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
+``--gpus N`` (N > 1) without a launcher around it starts N worker processes itself (one per
+GPU, RANK / LOCAL_RANK / WORLD_SIZE in their environment, before anything touches the GPU)
+and forwards rank 0's line; fewer visible GPUs than N is an error (exit 2) unless
+``--rehearse-gloo`` asks for a time-shared gloo rehearsal.  The line reports the world size
+the backend saw (``world_size_backend``), the backend, the launcher and the exchange; RCCL
+runs add ``library_exchange``: the same filter over the library's own communicator
+(gpmdm_pf_set_comm), timed and checked bit for bit against the process-group filter.
+
 Workload (BASELINE.json configs[1]): N=2000 training latents, D=62, d=3, C=2 classes, 500 frames,
 P=100,000 particles per GPU (weak scaling: P_total = 100k x GPUs), synthetic model and
 observation stream.  One step = ``update(z)`` + ``class_probabilities()``
@@ -186,8 +194,12 @@ def cpu_baseline(data, budget_s=12.0):
     box), once more at that cap (``capped``)."""
     from oracle import gpmdm_oracle as O
     from gpmdm_amd import synthetic
+    import contextlib
     import torch
-    from threadpoolctl import threadpool_limits
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:                 # the BLAS pool stays as the environment set it
+        threadpool_limits = None
     capped, usable, nproc = host_cores()
     w = WORKLOAD
     from sklearn.decomposition import PCA
@@ -211,7 +223,7 @@ def cpu_baseline(data, budget_s=12.0):
         rng = np.random.RandomState(0)
         parts = [rng.randint(0, m.X_for_class(c).shape[0], Ps // w["C"]) for c in range(w["C"])]
         s, c = O.init_particles(m, Ps, parts)
-        with threadpool_limits(threads):
+        with threadpool_limits(threads) if threadpool_limits else contextlib.nullcontext():
             steps, t0 = 0, time.perf_counter()
             while True:
                 r = O.step(m, T, s, c, z[steps % 64], rng.exponential(size=(Ps, w["C"])), rng.randn(Ps, w["d"]),
@@ -224,7 +236,10 @@ def cpu_baseline(data, budget_s=12.0):
         return Ps * steps / el, steps, el
 
     v, steps, el = run(usable)
+    if threadpool_limits is None:       # the pool was not set: report what the environment gave it
+        usable = capped or int(torch.get_num_threads())
     rec = {"value": v, "unit": "particle-steps/s", "cores": int(usable), "kind": "port",
+           "blas_pool": "threadpoolctl" if threadpool_limits else "not set (threadpoolctl missing): environment default",
            "nproc": nproc, "sched_affinity_cores": usable, "cgroup_cpu_quota": cgroup_cpu_quota(), "torch_threads": int(torch.get_num_threads()),
            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
            "sample": f"oracle (numpy fp64 restatement of gpmdm_pf.py's step, BLAS pool set to all {usable} usable "
@@ -232,7 +247,7 @@ def cpu_baseline(data, budget_s=12.0):
                      f"{el:.1f} s (model precompute excluded)",
            "calibration": "port vs the unmodified reference on 8 threads of the build container: "
                           "profiles/r03/cpu_calibration.txt, BASELINE.md §2"}
-    if capped and capped != usable:
+    if capped and capped != usable and threadpool_limits is not None:
         vc, sc, ec = run(capped)
         rec["capped"] = {"value": vc, "cores": capped, "frames": sc, "seconds": ec,
                          "note": "BLAS pool at the environment's OMP_NUM_THREADS cap"}
@@ -400,9 +415,204 @@ def bank_line(model, T, F, P, zs, warmup, steps):
                     "after another with one filter"}
 
 
+def library_comm(world, rank, local, group, device):
+    """An RCCL communicator made by the library (gpmdm_comm_init), rank 0's unique id
+    broadcast over the process group."""
+    from gpmdm_amd import _lib
+    from gpmdm_amd.distributed import RcclComm, broadcast_array
+    uid = RcclComm.unique_id() if rank == 0 else bytes(_lib.GPMDM_COMM_ID_BYTES)
+    uid = broadcast_array(np.frombuffer(uid, dtype=np.uint8).copy(), group, device).tobytes()
+    return RcclComm(world, rank, uid, local)
+
+
+def library_exchange_line(new_filter, zs, steps, dist, device, P_total, warmup=3):
+    """Multi-rank runs over RCCL: the same filter with the library's own exchange
+    (gpmdm_pf_set_comm, both all-gathers on a library stream) timed for ``steps`` frames,
+    then a torch.distributed filter stepped over the same frames; their read-outs and
+    exported states must be bitwise equal (the library path and the process-group path
+    are one filter)."""
+    import torch
+    pf = new_filter(exchange="library")
+    for k in range(warmup):
+        pf.update(zs[k])
+        pf.class_probabilities()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        pf.update(zs[warmup + k])
+        pf.get_most_likely_class()
+        pf.class_probabilities()
+        pf.current_state_mean()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=device)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item())
+    ref = new_filter(exchange="torch")
+    for k in range(warmup + steps):
+        ref.update(zs[k])
+    a, b = pf.export_state(), ref.export_state()
+    same = (np.array_equal(pf.class_probabilities().numpy(), ref.class_probabilities().numpy())
+            and np.array_equal(pf.current_state_mean().numpy(), ref.current_state_mean().numpy())
+            and all(np.array_equal(a[k], b[k]) for k in ("states", "classes", "ll", "resample_idx")))
+    ok = torch.tensor([1 if same else 0], dtype=torch.int64, device=device)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return {"exchange": "gpmdm_pf_set_comm (library-owned RCCL communicator and stream)", "steps": steps,
+            "ms_per_step": el / steps * 1e3, "value": P_total * steps / el,
+            "bitwise_equal_to_process_group_filter": bool(ok.item()),
+            "note": "the headline filter with the library's exchange instead of torch.distributed; read-outs and "
+                    "exported states compared bit for bit with a process-group filter after the same frames, on "
+                    "every rank"}
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_devices():
+    """GPUs this process could use, counted without initialising the GPU runtime
+    (torch.cuda.device_count() does not initialise HIP on this image)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch(args, argv):
+    """``bench.py --gpus N`` without a launcher around it: start N worker processes of this
+    script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment; one process per
+    GPU, as torch.distributed.run would), forward rank 0's JSON line and return the exit
+    status.  The parent never touches the GPU (it only counts devices) and never execs; a
+    worker that fails, or a run past ``--launch-timeout``, ends every worker (by PID) and
+    the launch with a non-zero status.
+
+    Fewer visible GPUs than N is an error (exit 2): nothing would be measured on N GPUs.
+    ``--rehearse-gloo`` is the explicit opt-in to time-share the visible GPU(s) over the gloo
+    backend (RCCL refuses two ranks on one device); ``--plumbing-check`` runs the launcher
+    and the distributed timing harness with no GPU work at all (CPU tests)."""
+    import subprocess
+    N = args.gpus
+    if args.plumbing_check:
+        backend = "gloo"
+    else:
+        ndev = visible_devices()
+        if ndev < N and not args.rehearse_gloo:
+            log(f"[bench] --gpus {N} but {ndev} GPU(s) visible: refusing to report an {N}-GPU number "
+                f"(--rehearse-gloo time-shares the visible GPU(s) over gloo, explicitly)")
+            return 2
+        if ndev == 0:
+            log("[bench] no GPU visible")
+            return 2
+        backend = "gloo" if args.rehearse_gloo else "nccl"
+    port = _free_port()
+    procs = []
+    for r in range(N):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(N), LOCAL_WORLD_SIZE=str(N),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   GPMDM_BENCH_BACKEND=backend, GPMDM_BENCH_LAUNCHER="bench.py")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")    # dmabuf IPC (RCCL between processes)
+        procs.append(subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve()), *argv], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    t0 = time.time()
+    rc = 0
+    out = b""
+    try:
+        live = set(range(N))
+        while live:
+            for r in sorted(live):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                live.discard(r)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    log(f"[bench] worker rank {r} exited with status {code}: stopping the launch")
+            if rc:
+                break
+            if time.time() - t0 > args.launch_timeout:
+                log(f"[bench] launch exceeded {args.launch_timeout} s: stopping the workers")
+                rc = 124
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except Exception:
+                pass
+        if procs[0].stdout is not None:
+            out = procs[0].stdout.read()
+    if rc == 0:
+        lines = [ln for ln in out.decode(errors="replace").splitlines() if ln.startswith("{")]
+        if len(lines) != 1:
+            log(f"[bench] rank 0 printed {len(lines)} JSON lines, expected 1")
+            return 1
+        print(lines[0], flush=True)
+    return rc
+
+
+def plumbing_worker(args):
+    """The distributed timing harness with no GPU work (``--plumbing-check``): process
+    group over gloo, barrier-bracketed timed region of K tiny CPU steps, max over ranks,
+    one JSON line from rank 0 -- the launcher's and the harness's plumbing, testable on a
+    machine without a GPU."""
+    import datetime
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.collective_timeout))
+    if os.environ.get("GPMDM_PLUMBING_FAIL_RANK") == str(rank):   # tests: a worker that dies mid-run
+        os._exit(3)
+    try:
+        x = np.arange(4096, dtype=np.float64)
+        for _ in range(args.warmup):
+            x = np.sqrt(x * x + 1.0)
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            x = np.sqrt(x * x + 1.0)
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": None, "unit": "particle-steps/s", "n_gpus": world,
+                              "steps": args.steps, "warmup": args.warmup,
+                              "ms_per_step": float(el.item()) / max(args.steps, 1) * 1e3,
+                              "world_size_backend": dist.get_world_size(), "backend": dist.get_backend(),
+                              "launcher": os.environ.get("GPMDM_BENCH_LAUNCHER", "external"),
+                              "data": "none: --plumbing-check (launcher and timing harness only, no GPU work)"}),
+                  flush=True)
+    finally:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (one worker process each).  Without WORLD_SIZE in the environment and N > 1, "
+                         "bench.py starts the N workers itself; under torch.distributed.run it must equal WORLD_SIZE")
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="explicit opt-in: run N ranks over gloo on fewer GPUs than N (time-shared; a rehearsal "
+                         "of the multi-rank path, not an N-GPU measurement)")
+    ap.add_argument("--plumbing-check", action="store_true",
+                    help="launcher + distributed timing harness only, no GPU work (CPU tests)")
+    ap.add_argument("--launch-timeout", type=float, default=3000.0,
+                    help="seconds before the self-launch stops its workers")
+    ap.add_argument("--collective-timeout", type=float, default=600.0,
+                    help="seconds a collective may stall before its worker fails")
+    ap.add_argument("--exchange", default="torch", choices=("torch", "library"),
+                    help="multi-rank exchange: torch.distributed (process_group=) or the library's own RCCL "
+                         "communicator (gpmdm_pf_set_comm)")
+    ap.add_argument("--library-steps", type=int, default=20,
+                    help="multi-rank RCCL runs: frames of the library-exchange line (0 = off)")
     ap.add_argument("--steps", type=int, default=None,
                     help="timed frames (default: 500, configs[1]'s 500 frames; 20 for configs 3 and 5)")
     ap.add_argument("--warmup", type=int, default=5)
@@ -419,7 +629,19 @@ def main():
                     help="frames of the spread-cloud line (config 2, one GPU; default 30, 0 = off)")
     ap.add_argument("--dyn-tiles", default="auto", choices=("auto", "narrow", "wide"),
                     help="dynamics tile shape of the headline filter (gpmdm_pf_set_dyn_tiles)")
-    args = ap.parse_args()
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch(args, argv))
+    if env_world is not None and int(env_world) != args.gpus:
+        log(f"[bench] --gpus {args.gpus} but WORLD_SIZE={env_world}: the launcher and the flag disagree")
+        sys.exit(2)
+    if args.plumbing_check:
+        plumbing_worker(args)
+        return
     global WORKLOAD
     WORKLOAD = workload(args.config)
     WORKLOAD["y_lambda"] = args.y_lambda
@@ -434,18 +656,24 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
-    if ndev and local >= ndev:          # rehearsal with more ranks than GPUs (never on a full node)
-        local %= ndev
     backend = os.environ.get("GPMDM_BENCH_BACKEND", "nccl")
+    if world > ndev:
+        if backend != "gloo":
+            log(f"[bench] WORLD_SIZE={world} but {ndev} GPU(s) visible: refusing to time-share GPUs over "
+                f"{backend} (GPMDM_BENCH_BACKEND=gloo / --rehearse-gloo is the explicit rehearsal)")
+            sys.exit(2)
+        local %= max(ndev, 1)           # rehearsal: ranks time-share the visible GPU(s)
     dist = None
     group = None
     if world > 1:
+        import datetime
         import torch.distributed as dist
         torch.cuda.set_device(local)
+        tmo = datetime.timedelta(seconds=args.collective_timeout)   # a stalled collective fails the worker
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
         group = dist.group.WORLD
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
@@ -454,7 +682,7 @@ def main():
     from gpmdm_amd import _lib
     # one builder per node (a no-op when the in-tree library is current); the other ranks
     # wait, so concurrent ranks never write the same objects
-    if local == 0:
+    if int(os.environ.get("LOCAL_RANK", "0")) == 0:
         build.build()
     if dist is not None:
         dist.barrier()
@@ -468,11 +696,22 @@ def main():
     n_frames = args.warmup + args.steps + n_breakdown + 64
     if args.config == 1:
         n_frames += args.steps          # the event-free pass of the notebook line
+    comm = None
+    if world > 1 and args.exchange == "library":
+        if backend != "nccl":
+            log("[bench] --exchange library needs RCCL (one GPU per rank), not a gloo rehearsal")
+            sys.exit(2)
+        comm = library_comm(world, rank, local, group, device)
 
-    def new_filter(**kw):
+    def new_filter(exchange=args.exchange, **kw):
         torch.manual_seed(11)
-        return GPMDM_PF(model, T, P_total, rng=rng, seed=11 if rng == "philox" else None,
-                        process_group=group, dyn_tiles=args.dyn_tiles, **kw)
+        seed = 11 if rng == "philox" else None
+        if world > 1 and exchange == "library":
+            # the library's own exchange: shard=(world, rank) + gpmdm_pf_set_comm
+            pf_ = GPMDM_PF(model, T, P_total, rng=rng, seed=seed, shard=(world, rank), dyn_tiles=args.dyn_tiles, **kw)
+            pf_.set_comm(comm)
+            return pf_
+        return GPMDM_PF(model, T, P_total, rng=rng, seed=seed, process_group=group, dyn_tiles=args.dyn_tiles, **kw)
 
     stream_check = None
     if args.stream == "predictive":
@@ -549,6 +788,11 @@ def main():
     ess = float(1.0 / np.sum(w_last * w_last))
     bank = bank_line(model, T, args.bank, P_total, zs, args.warmup, args.steps) if args.bank and world == 1 else None
     nodedup = None if args.no_nodedup else nodedup_line(model, T, P_total, group, dist, device, zs, args.steps, rng)
+    libx = None
+    if world > 1 and backend == "nccl" and args.library_steps > 0:
+        if comm is None:
+            comm = library_comm(world, rank, local, group, device)
+        libx = library_exchange_line(new_filter, zs, min(args.steps, args.library_steps), dist, device, P_total)
     if args.spread_steps is None:
         args.spread_steps = 30 if (args.config == 2 and args.stream == "mocap" and args.y_lambda == 1.0) else 0
     spread = spread_line(device, args.spread_steps) if args.spread_steps and world == 1 else None
@@ -565,6 +809,15 @@ def main():
         "value": P_total * args.steps / elapsed,
         "unit": "particle-steps/s",
         "n_gpus": world,
+        "world_size_backend": dist.get_world_size() if dist is not None else 1,
+        "backend": backend if dist is not None else None,
+        "launcher": os.environ.get("GPMDM_BENCH_LAUNCHER",
+                                   "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ
+                                   else ("external" if world > 1 else "single process")),
+        "exchange": ("none (one rank)" if world == 1 else
+                     "gpmdm_pf_set_comm (library RCCL communicator)" if args.exchange == "library" else
+                     f"torch.distributed ({backend}) all-gathers over the process group"),
+        "rehearsal": bool(world > ndev),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -614,6 +867,8 @@ def main():
                                   "identical ancestor de-duplication, DESIGN.md §3); breakdown_mean and "
                                   "dyn_gemm_tflops over the stage-breakdown pass"},
     }
+    if libx is not None:
+        rec["library_exchange"] = libx
     if bank is not None:
         rec["bank"] = bank
     if spread is not None:
