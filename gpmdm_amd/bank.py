@@ -122,14 +122,32 @@ class GPMDM_PF_Bank:
         if self._h is not None:
             self._init_particles()
 
-    def load_state(self, states, classes):
-        """states (F_local, P, d), classes (F_local, P)."""
+    def load_state(self, states, classes, *, ll=None, log_w=None, w=None, resample_idx=None, frame=None):
+        """states (F_local, P, d), classes (F_local, P); with ll / log_w / w (F_local, P) the
+        full state of ``export_state`` (GPMDM_PF.load_state; gpmdm_pf_import)."""
         Fl, P, d = self.local_filters, self._num_particles, self.latent_dim
         states = np.ascontiguousarray(states, dtype=np.float64).reshape(Fl * P, d)
         classes = np.ascontiguousarray(classes, dtype=np.int64).reshape(Fl * P)
         self._sync_model()
-        _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "load_state")
+        full = (ll, log_w, w)
+        if all(x is None for x in full) and resample_idx is None and frame is None:
+            _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "load_state")
+        else:
+            if any(x is None for x in full):
+                raise ValueError("a full state import needs ll, log_w and w together")
+            ll, log_w, w = (np.ascontiguousarray(x, dtype=np.float64).reshape(Fl * P) for x in full)
+            ridx = None if resample_idx is None else np.ascontiguousarray(resample_idx, dtype=np.int64).reshape(Fl * P)
+            _lib.check(_lib.load().gpmdm_pf_import(
+                self._h, _lib.dptr(states), _lib.i64ptr(classes), _lib.dptr(ll), _lib.dptr(log_w), _lib.dptr(w),
+                _lib.i64ptr(ridx), -1 if frame is None else int(frame)), "load_state")
         self._readout = None
+
+    def import_state(self, st: dict):
+        """Restore an ``export_state()`` dict (same filters, same seed: checked)."""
+        if "seed" in st and int(st["seed"]) != self._seed:
+            raise ValueError("the state was exported by a bank with another seed")
+        self.load_state(st["states"], st["classes"], ll=st["ll"], log_w=st["log_w"], w=st["w"],
+                        resample_idx=st.get("resample_idx"), frame=st.get("frame"))
 
     def export_state(self) -> dict:
         Fl, P, d = self.local_filters, self._num_particles, self.latent_dim
@@ -143,6 +161,8 @@ class GPMDM_PF_Bank:
         out["states"] = out["states"].reshape(Fl, P, d)
         for k in ("classes", "ll", "log_w", "w", "resample_idx"):
             out[k] = out[k].reshape(Fl, P)
+        out["frame"] = self.frame
+        out["seed"] = self._seed
         return out
 
     # ---- per-frame ------------------------------------------------------------------

@@ -967,6 +967,80 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   return GPMDM_OK;
 }
 
+// Restore an exported state (gpmdm_pf.py:78-82, 100-104): particles, ancestors, ll and the
+// weights, then the read-outs of that state from the restored values themselves -- the
+// identity resampling pass reads ll, max(ll) and e / total, so with e = w and total = 1 it
+// reads w as the exporter's read-out read e / S (export's w is that same division), and
+// the read-outs equal the exporter's bit for bit.  The next frame's normalisation
+// recomputes e and the total from its own ll (weights are not recursive, gpmdm_pf.py:198).
+int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes, const double* ll,
+                    const double* log_w, const double* w, const int64_t* ridx, int64_t frame) {
+  CHECK(pf && states && classes && ll && log_w && w, "null argument");
+  gpmdm_model* m = pf->m;
+  HIPCHK(hipSetDevice(m->device));
+  TRY(drop_preswitch(pf, nullptr, true));
+  if (pf->switched || pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "import between switch and resample");
+  CHECK(frame < (1ll << 32), "frame out of range");
+  const long long P = pf->P, Pf = pf->Pf;
+  const int F = pf->F;
+  std::vector<int> c32(P), r32(P);
+  for (long long i = 0; i < P; ++i) {
+    CHECK(classes[i] >= 0 && classes[i] < m->C, "class id out of range");
+    c32[i] = (int)classes[i];
+    if (ridx) CHECK(ridx[i] >= 0 && ridx[i] < Pf, "resample index out of range");
+    r32[i] = ridx ? (int)ridx[i] : (int)(i % Pf);
+  }
+  // max(ll) per filter as k_norm_max takes it (fmax: NaN ignored), and log_w = ll - max
+  std::vector<unsigned long long> gm(F);
+  for (int f = 0; f < F; ++f) {
+    double M = -INFINITY;
+    for (long long i = f * Pf; i < (f + 1) * Pf; ++i) M = std::fmax(M, ll[i]);
+    for (long long i = f * Pf; i < (f + 1) * Pf; ++i) {
+      const double lw = ll[i] - M;
+      CHECK(std::memcmp(&lw, &log_w[i], sizeof(double)) == 0 || (std::isnan(lw) && std::isnan(log_w[i])),
+            "log_w is not ll - max(ll) of its filter");
+    }
+    unsigned long long u;
+    std::memcpy(&u, &M, sizeof(u));
+    gm[f] = (u >> 63) ? ~u : (u | 0x8000000000000000ull);   // ord_enc (common.h)
+  }
+  const std::vector<double> ones(F, 1.0);
+  HIPCHK(hipMemcpy(pf->X, states, sizeof(double) * P * m->d, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(pf->cls, c32.data(), sizeof(int) * P, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(pf->ridx, r32.data(), sizeof(int) * P, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(pf->ll, ll, sizeof(double) * P, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(pf->e, w, sizeof(double) * P, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(pf->total, ones.data(), sizeof(double) * F, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(pf->gmax, gm.data(), sizeof(unsigned long long) * F, hipMemcpyHostToDevice));
+  if (pf->cls_pin) {
+    std::memcpy(pf->cls_pin, c32.data(), sizeof(int) * P);
+    pf->cls_host_ok = true;
+    pf->cls_ev_pending = false;
+  }
+  pf->bmax_ready = false;
+  pf->ll_pending = false;
+  pf->cnt_check = false;
+  if (frame >= 0) pf->frame = (unsigned)frame;
+  ResampleArgs ra = resample_args(pf);
+  ra.identity = 1;
+  ra.cls_src = pf->cls;
+  ra.X_src = pf->X;
+  launch_resample(ra, nullptr);
+  HIPCHK(hipGetLastError());
+  pf->own_valid = false;
+  if (pf->own && pf->dedup && pf->shard_order) {   // the next frame's shards, as a resample sets them
+    if (launch_ancestor_order(pf->ridx, pf->own, pf->own_inv, pf->P, pf->own_tmp, pf->own_tmp_bytes, nullptr) != 0)
+      return fail(GPMDM_E_HIP, "ancestor-order pass failed");
+    pf->own_valid = true;
+  }
+  HIPCHK(hipEventRecord(pf->ro_ev, nullptr));
+  HIPCHK(hipDeviceSynchronize());
+  pf->ro_ev_ok = true;
+  pf->initialised = true;
+  pf->switched = pf->propagated = pf->dyn_done = false;
+  return GPMDM_OK;
+}
+
 static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipStream_t s) {
   gpmdm_model* m = pf->m;
   const int C = m->C;

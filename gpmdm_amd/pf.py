@@ -348,15 +348,44 @@ class GPMDM_PF:
             self._h, _lib.dptr(out["states"]), _lib.i64ptr(out["classes"]), _lib.dptr(out["ll"]),
             _lib.dptr(out["log_w"]), _lib.dptr(out["w"]), _lib.i64ptr(out["resample_idx"]), self._stream()),
             "export")
+        out["frame"] = self.frame
+        out["seed"] = self._seed
         return out
 
-    def load_state(self, states, classes):
-        """Set the particle states/classes (e.g. a reference pre-step state)."""
+    def load_state(self, states, classes, *, ll=None, log_w=None, w=None, resample_idx=None, frame=None):
+        """Set the particle state.  With ``states``/``classes`` only: those particles with the
+        reference's initial weights (ll = log_w = 0, w = 1/P; gpmdm_pf.py:100-104), e.g. a
+        reference pre-step state.  With ``ll``, ``log_w`` and ``w`` as well (all three): the
+        full filter state of ``export_state`` (gpmdm_pf.py:78-82) -- the read-outs right
+        after are the exporter's, and the next updates continue its trajectory bit for bit
+        (``resample_idx``: the ancestors of the last resample, optional; ``frame``: the
+        Philox counter, optional; a replay filter's torch RNG state is the caller's to
+        restore).  ``gpmdm_pf_import``."""
         self._sync_model()
-        states = np.ascontiguousarray(states, dtype=np.float64).reshape(self._num_particles, self.latent_dim)
-        classes = np.ascontiguousarray(classes, dtype=np.int64).reshape(self._num_particles)
-        _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "load_state")
+        P = self._num_particles
+        states = np.ascontiguousarray(states, dtype=np.float64).reshape(P, self.latent_dim)
+        classes = np.ascontiguousarray(classes, dtype=np.int64).reshape(P)
+        full = (ll, log_w, w)
+        if all(x is None for x in full) and resample_idx is None and frame is None:
+            _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "load_state")
+        else:
+            if any(x is None for x in full):
+                raise ValueError("a full state import needs ll, log_w and w together")
+            ll, log_w, w = (np.ascontiguousarray(x, dtype=np.float64).reshape(P) for x in full)
+            ridx = None if resample_idx is None else np.ascontiguousarray(resample_idx, dtype=np.int64).reshape(P)
+            _lib.check(_lib.load().gpmdm_pf_import(
+                self._h, _lib.dptr(states), _lib.i64ptr(classes), _lib.dptr(ll), _lib.dptr(log_w), _lib.dptr(w),
+                _lib.i64ptr(ridx), -1 if frame is None else int(frame)), "load_state")
         self._readout = None
+
+    def import_state(self, st: dict):
+        """Restore an ``export_state()`` dict (a checkpoint of this filter or of one with
+        the same configuration): ``load_state`` with every field it holds.  A Philox filter
+        must have been built with the exporter's seed (checked)."""
+        if self._rng == "philox" and "seed" in st and int(st["seed"]) != self._seed:
+            raise ValueError("the state was exported by a filter with another Philox seed")
+        self.load_state(st["states"], st["classes"], ll=st["ll"], log_w=st["log_w"], w=st["w"],
+                        resample_idx=st.get("resample_idx"), frame=st.get("frame"))
 
     def dynamics_rows(self) -> int:
         """Rows the last dynamics-GP pass evaluated (distinct ancestor/class keys when

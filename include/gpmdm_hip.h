@@ -131,6 +131,20 @@ int gpmdm_pf_shape(gpmdm_pf_t pf, int64_t* n_filters, int64_t* P);
  * (host).  Clears weights to 1/P and log-likelihoods to 0 as the reference does. */
 int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes);
 
+/* Restore a filter state exported by gpmdm_pf_export (checkpoint / resume):
+ * the reference filter's state _particle_states, _particle_classes, _log_likelihoods,
+ * _log_weights, _weights (gpmdm_pf.py:78-82, 100-104), all host.  states P x d, classes P,
+ * ll P, log_w P, w P (all required); ridx P (the last resample's ancestor indices within each
+ * filter, or NULL: none shared); frame >= 0 sets the Philox frame counter (< 0 keeps it).
+ * log_w must be ll - max(ll) per filter, computed as gpmdm_pf_export computes it (exact
+ * comparison; GPMDM_E_INVALID otherwise).  The read-outs right after the import equal the
+ * exporter's (posterior, mean, likelihood sum, bit for bit), and a filter of the same
+ * configuration and seed continues the exporter's trajectory bit for bit.  A replay
+ * filter's draws come from the caller's generator: saving its state is the caller's part.
+ * Drops a pending pre-switch; not between switch and resample. */
+int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes, const double* ll,
+                    const double* log_w, const double* w, const int64_t* ridx, int64_t frame);
+
 /* _propogate_markov_switching  (gpmdm_pf.py:137-151).  exp_draws: P x C host (replay)
  * or NULL (philox).  class_counts: C host, or NULL; when given, the post-switch class
  * counts are returned (the replay caller needs them to draw the per-class normals of the
