@@ -383,6 +383,53 @@ def nodedup_line(model, T, P_total, group, dist, device, zs, steps, rng):
                     "launch time"}
 
 
+def replay_line(model, T, P, zs, warmup, steps, headline_ms=None):
+    """The drop-in default at this size: rng='torch', the reference's draws from torch's
+    global generator in its order (gpmdm_pf.py:137-213), drawn on the host as parallel chunks
+    of torch's own samplers (replay.ParallelFrameDraws, bit for bit the serial draws) while
+    the GPU runs, and uploaded per frame.  Beside the headline, never the headline."""
+    import torch
+    from gpmdm_amd import GPMDM_PF, replay
+    torch.manual_seed(11)
+    pf = GPMDM_PF(model, T, P)                 # the reference's signature: rng='torch' by default
+
+    def frame(k):
+        pf.update(zs[k])
+        pf.get_most_likely_class()
+        pf.class_probabilities()
+        pf.current_state_mean()
+
+    for k in range(warmup):
+        frame(k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        frame(warmup + k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    dr = pf._draws
+    # the same frame's draws with torch's serial samplers (what the reference itself does)
+    ser = replay.FrameDraws(P, model.n_classes, model.d, P)
+    g = torch.Generator().manual_seed(1)
+    ser._gen = g
+    t1 = time.perf_counter()
+    for _ in range(3):
+        ser.switch()
+        ser.dynamics([P // 2, P - P // 2])
+        ser.resample()
+    serial_ms = (time.perf_counter() - t1) / 3 * 1e3
+    ms = el / steps * 1e3
+    return {"rng": "torch (host draws, the reference's order; GPMDM_PF's default)", "steps": steps,
+            "ms_per_step": ms, "value": P * steps / el,
+            "vs_headline": (headline_ms / ms) if headline_ms else None,
+            "draws": type(dr).__name__, "host_threads": getattr(dr, "threads", 1),
+            "prefetch_hits": getattr(dr, "prefetch_hits", None), "prefetch_misses": getattr(dr, "prefetch_misses", None),
+            "serial_draws_ms_per_frame": serial_ms,
+            "note": "update + get_most_likely_class + class_probabilities + current_state_mean per frame; "
+                    "serial_draws_ms_per_frame = torch's serial samplers for one frame's E, normals and U on "
+                    "this host (the cost the parallel, ahead-of-time draws take off the frame)"}
+
+
 def bank_line(model, T, F, P, zs, warmup, steps):
     """test_gpmdm_pf.ipynb cell 4's trial loop as one bank: F filters of P particles, each
     frame one bank update plus the read-outs (every filter sees its own observation; here
@@ -611,6 +658,9 @@ def main():
     ap.add_argument("--exchange", default="torch", choices=("torch", "library"),
                     help="multi-rank exchange: torch.distributed (process_group=) or the library's own RCCL "
                          "communicator (gpmdm_pf_set_comm)")
+    ap.add_argument("--replay-steps", type=int, default=None,
+                    help="frames of the rng='torch' (drop-in default) line beside a Philox headline "
+                         "(default 30 at config 2 on one GPU, 0 = off)")
     ap.add_argument("--library-steps", type=int, default=20,
                     help="multi-rank RCCL runs: frames of the library-exchange line (0 = off)")
     ap.add_argument("--steps", type=int, default=None,
@@ -788,6 +838,11 @@ def main():
     ess = float(1.0 / np.sum(w_last * w_last))
     bank = bank_line(model, T, args.bank, P_total, zs, args.warmup, args.steps) if args.bank and world == 1 else None
     nodedup = None if args.no_nodedup else nodedup_line(model, T, P_total, group, dist, device, zs, args.steps, rng)
+    rep = None
+    if args.replay_steps is None:
+        args.replay_steps = 30 if (args.config == 2 and rng == "philox" and args.stream == "mocap") else 0
+    if args.replay_steps and world == 1:
+        rep = replay_line(model, T, P_total, zs, 3, args.replay_steps, elapsed / args.steps * 1e3)
     libx = None
     if world > 1 and backend == "nccl" and args.library_steps > 0:
         if comm is None:
@@ -869,6 +924,8 @@ def main():
     }
     if libx is not None:
         rec["library_exchange"] = libx
+    if rep is not None:
+        rec["replay"] = rep
     if bank is not None:
         rec["bank"] = bank
     if spread is not None:

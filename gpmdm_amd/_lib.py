@@ -86,6 +86,10 @@ _SIGS = {
     "gpmdm_gp_factor": (c_int, [c_int, _dp, c_int64, c_int32, _dp, _dp, c_double, c_double, c_double,
                                 _dp, c_int64, _dp, _dp]),
     "gpmdm_spd_inverse": (c_int, [c_int, c_void_p, c_int64, _dp, c_void_p]),
+    "gpmdm_rng_walk_create": (c_int, [c_void_p, c_int64, POINTER(c_void_p)]),
+    "gpmdm_rng_walk_reset": (c_int, [c_void_p, c_void_p, c_int64]),
+    "gpmdm_rng_walk_state": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "gpmdm_rng_walk_destroy": (c_int, [c_void_p]),
     "gpmdm_last_error": (c_char_p, []),
     "gpmdm_version": (c_char_p, []),
 }

@@ -52,6 +52,11 @@ from . import _lib, replay
 from .model import GPMDM
 
 
+# Replay filters from this many particles draw torch's streams as parallel chunks
+# (replay.ParallelFrameDraws); below it the serial draws cost less than the threads' hand-offs.
+PARALLEL_REPLAY_P = 16384
+
+
 def _as_f64_vector(z) -> np.ndarray:
     """The observation as a contiguous float64 vector (the reference casts it with
     torch.tensor(z, dtype=float64), gpmdm_pf.py:123; float32 -> float64 is exact)."""
@@ -196,7 +201,12 @@ class GPMDM_PF:
         P, C, d = self._num_particles, self.num_classes, self.latent_dim
         if self._rng == "torch":
             if self._draws is None:
-                self._draws = replay.FrameDraws(P, C, d, P if self._resample_mode == "multinomial" else 1)
+                nu = P if self._resample_mode == "multinomial" else 1
+                if P >= PARALLEL_REPLAY_P and replay.host_threads() > 1:
+                    # torch's own samplers in parallel chunks, bit for bit the serial streams
+                    self._draws = replay.ParallelFrameDraws(P, C, d, nu)
+                else:
+                    self._draws = replay.FrameDraws(P, C, d, nu)
                 self._counts = np.zeros(C, dtype=np.int64)
                 dr = self._draws           # the draws land in place: their pointers are fixed
                 self._draw_ptr = (_lib.dptr(dr.E), _lib.i64ptr(self._counts), _lib.dptr(dr.N), _lib.dptr(dr.U))

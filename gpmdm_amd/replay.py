@@ -97,3 +97,253 @@ class FrameDraws:
     def resample(self) -> np.ndarray:
         self._U.uniform_(0, 1, generator=self._gen)
         return self.U
+
+
+# ---- parallel replay (large filters) ---------------------------------------------------
+STATE_BYTES = 5056                    # torch CPU generator state (GPMDM_TORCH_GEN_STATE_BYTES)
+_CACHE = slice(5016, 5056)            # the normal-sample caches of that state (double and float)
+
+
+def host_threads() -> int:
+    """Cores this process may really use: the CPU affinity capped by the cgroup's CPU quota
+    (a GPU box shows 256 CPUs and grants 16) and by OMP_NUM_THREADS when set."""
+    import os
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(np.ceil(int(q) / int(per)))))
+    except Exception:
+        pass
+    v = os.environ.get("OMP_NUM_THREADS", "")
+    if v.isdigit() and int(v) > 0:
+        n = min(n, int(v))
+    return max(1, n)
+
+
+class _Walk:
+    """gpmdm_rng_walk: generator states at draw offsets of one stretch of the stream."""
+
+    def __init__(self):
+        import ctypes
+        from . import _lib
+        self._lib, self._ct = _lib, ctypes
+        self._h = None
+        self.n_draws = 0
+
+    def reset(self, state: np.ndarray, n_draws: int) -> "_Walk":
+        ct, lib = self._ct, self._lib.load()
+        buf = ct.c_void_p(state.ctypes.data)
+        if self._h is None:
+            h = ct.c_void_p()
+            self._lib.check(lib.gpmdm_rng_walk_create(buf, int(n_draws), ct.byref(h)), "rng walk")
+            self._h = h
+        else:
+            self._lib.check(lib.gpmdm_rng_walk_reset(self._h, buf, int(n_draws)), "rng walk")
+        self.n_draws = int(n_draws)
+        return self
+
+    def state(self, draws: int, cache_from: Optional[np.ndarray] = None) -> torch.Tensor:
+        out = torch.empty(STATE_BYTES, dtype=torch.uint8)
+        cf = None if cache_from is None else cache_from.ctypes.data
+        self._lib.check(self._lib.load().gpmdm_rng_walk_state(self._h, int(draws), cf, out.data_ptr()), "rng walk")
+        return out
+
+    def __del__(self):
+        try:
+            if self._h:
+                self._lib.load().gpmdm_rng_walk_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class ParallelFrameDraws:
+    """The per-frame streams of FrameDraws (the reference's order: E_k, per-class normals,
+    U_k; gpmdm_pf.py:137-213) bit for bit, with torch's own samplers run as parallel chunks.
+
+    torch's CPU samplers are serial: ~13 ms per frame at P = 100k on one core, twice the GPU
+    frame.  Each chunk here runs the same sampler (exponential_, normal_, uniform_) on a
+    private generator placed at the exact state the serial draw would have reached at that
+    chunk (gpmdm_rng_walk, torch_rng.cpp).  exponential_ and uniform_ take one random64 per
+    value; normal_ on n >= 16 values fills n uniforms and Box-Mullers blocks of 16
+    (recomputing the last 16 with 16 fresh uniforms when 16 does not divide n), so the chunks
+    of a class start at multiples of 16 values and the last chunk carries the class's tail; a
+    class of fewer than 16 values takes torch's serial path (pairs, with the generator's
+    normal cache), run on one private generator whose cache then carries on.  The global
+    generator ends each frame where the serial draws would leave it.
+
+    What does not depend on the device's results is drawn ahead, on a background thread,
+    while the GPU runs the frame: as soon as a frame's last draw is placed (``resample``),
+    the walk over the next frame's stretch, its Exp(1) switch draws, and the normals of its
+    first non-empty class -- that class's values start at a fixed place of the stream (right
+    after E) and its blocks of 16 do not depend on its length, so the normals are drawn for
+    the longest length it can have and only its last 16 (when 16 does not divide its length)
+    are drawn again once the switch's counts are known.  ``begin()`` uses them only if the
+    global generator still stands where the frame ended (any other draw in between
+    invalidates them, and they are drawn again there and then), so the streams are the
+    reference's whatever the caller does between frames."""
+
+    def __init__(self, P: int, C: int, d: int, n_uniform: int, threads: Optional[int] = None,
+                 chunk: int = 4096):
+        from concurrent.futures import ThreadPoolExecutor
+        self.P, self.C, self.d, self.nu = int(P), int(C), int(d), int(n_uniform)
+        self.threads = threads or host_threads()
+        self._pool = ThreadPoolExecutor(max_workers=self.threads)
+        self._bg = ThreadPoolExecutor(max_workers=1)
+        self._chunk = int(chunk)
+        self._E = torch.empty((P, C), dtype=torch.float64)
+        self._N = torch.empty((P, d), dtype=torch.float64)
+        self._U = torch.empty((self.nu,), dtype=torch.float64)
+        self.E, self.N, self.U = self._E.numpy(), self._N.numpy(), self._U.numpy()
+        self._walks = (_Walk(), _Walk())   # this frame's and the next frame's (buffers reused)
+        self._wi = 0
+        self._walk = None
+        self._cache = None              # a state holding the stream's current normal-cache bytes
+        self._spec = False              # N holds the first class's normals drawn ahead
+        self._pos = 0                   # draws consumed in the frame so far
+        self._expect = None             # global state the last frame ended in
+        self._pending = None            # background future (the next frame's walk, E, first normals)
+        self.prefetch_hits = 0
+        self.prefetch_misses = 0
+        self.record = False             # keep copies of the frame's draws (last_E/N/U; tests): E
+                                        # and N are refilled ahead for the next frame
+
+    # draws of one frame at most: E, the normals (+16 per class for a tail, a small class
+    # at most 16), U
+    def _frame_draws(self) -> int:
+        return self.P * self.C + self.P * self.d + 16 * self.C + self.nu
+
+    def _run(self, tasks):
+        list(self._pool.map(lambda f: f(), tasks))
+
+    @staticmethod
+    def _gen(state: torch.Tensor) -> torch.Generator:
+        g = torch.Generator()
+        g.set_state(state)
+        return g
+
+    def _normal_tasks(self, walk: _Walk, cache: np.ndarray, seg: torch.Tensor, pos: int, tasks: list):
+        """Chunks of one class's normal_ (n = seg.numel() >= 16 values from draw ``pos``)."""
+        n = seg.numel()
+        step = max(16 * -(-self._chunk // 16), 16 * -(-n // (16 * self.threads)))
+        a = 0
+        while a < n:
+            b = n if n - a < step + 16 else a + step   # the last chunk: >= 16 values, the tail
+            st = walk.state(pos + a, cache)
+            tasks.append(lambda a=a, b=b, st=st, seg=seg: seg[a:b].normal_(0, 1, generator=self._gen(st)))
+            a = b
+
+    def _ahead(self, walk: _Walk, state: np.ndarray):
+        """The frame's draws that need no device result: E, and the first class's normals
+        for the longest length (all P particles)."""
+        walk.reset(state, self._frame_draws())
+        flat = self._E.view(-1)
+        n, step = flat.numel(), max(self._chunk, -(-flat.numel() // self.threads))
+        tasks = []
+        for a in range(0, n, step):
+            b = min(n, a + step)
+            st = walk.state(a, state)
+            tasks.append(lambda a=a, b=b, st=st: flat[a:b].exponential_(1, generator=self._gen(st)))
+        spec = self.P * self.d >= 16
+        if spec:
+            self._normal_tasks(walk, state, self._N.view(-1), self.P * self.C, tasks)
+        self._run(tasks)
+        return walk, state, spec
+
+    def begin(self) -> np.ndarray:
+        """The frame's Exp(1) switch draws (P x C), from the global generator's state."""
+        cur = torch.get_rng_state()
+        got = None
+        if self._pending is not None:
+            got = self._pending.result()
+            self._pending = None
+        if got is not None and self._expect is not None and torch.equal(cur, self._expect):
+            self._walk, self._cache, self._spec = got
+            self.prefetch_hits += 1
+        else:
+            self._wi ^= 1 if got is None else 0
+            self._walk, self._cache, self._spec = self._ahead(self._walks[self._wi], cur.numpy().copy())
+            self.prefetch_misses += 1
+        self._pos = self.P * self.C
+        if self.record:
+            self.last_E = self.E.copy()
+        return self.E
+
+    switch = begin                      # FrameDraws' name for the frame's first draw
+
+    def dynamics(self, counts) -> np.ndarray:
+        """Per-class standard normals (sum_c P_c) x d in class order."""
+        walk, d = self._walk, self.d
+        flat = self._N.view(-1)
+        tasks, row, first = [], 0, True
+        if int(sum(int(c) for c in counts)) != self.P:
+            raise ValueError(f"class counts sum to {sum(counts)}, not {self.P}")
+        for p_c in counts:
+            p_c = int(p_c)
+            if p_c == 0:
+                continue
+            n = p_c * d
+            seg = flat[row * d:(row + p_c) * d]
+            if n < 16:                  # torch's serial path: pairs and the normal cache
+                self._run(tasks)        # (the chunks before it do not depend on it: order kept simple)
+                tasks = []
+                g = self._gen(walk.state(self._pos, self._cache))
+                seg.normal_(0, 1, generator=g)
+                after = g.get_state().numpy()
+                self._cache = self._cache.copy()
+                self._cache[_CACHE] = after[_CACHE]
+                self._pos += _consumed(after, walk, self._pos)
+            elif first and self._spec:  # drawn ahead; only a tail's last 16 are drawn again
+                if n % 16:
+                    st = walk.state(self._pos + n, self._cache)
+                    tasks.append(lambda st=st, seg=seg, n=n: seg[n - 16:n].normal_(0, 1, generator=self._gen(st)))
+                self._pos += n + (16 if n % 16 else 0)
+            else:
+                self._normal_tasks(walk, self._cache, seg, self._pos, tasks)
+                self._pos += n + (16 if n % 16 else 0)
+            first = False
+            row += p_c
+        self._run(tasks)
+        if self.record:
+            self.last_N = self.N.copy()
+        return self.N
+
+    def resample(self) -> np.ndarray:
+        """The resampling uniforms; the global generator then stands where the serial
+        frame would leave it, and the next frame's draws ahead start in the background."""
+        walk, n = self._walk, self.nu
+        step = max(self._chunk, -(-n // self.threads))
+        tasks = []
+        for a in range(0, n, step):
+            b = min(n, a + step)
+            st = walk.state(self._pos + a, self._cache)
+            tasks.append(lambda a=a, b=b, st=st: self._U[a:b].uniform_(0, 1, generator=self._gen(st)))
+        self._run(tasks)
+        if self.record:
+            self.last_U = self.U.copy()
+        self._pos += n
+        end = walk.state(self._pos, self._cache)
+        torch.set_rng_state(end)
+        self._expect = end
+        self._wi ^= 1
+        self._pending = self._bg.submit(self._ahead, self._walks[self._wi], end.numpy().copy())
+        return self.U
+
+    def close(self):
+        if self._pending is not None:
+            self._pending.result()
+            self._pending = None
+        self._pool.shutdown(wait=True)
+        self._bg.shutdown(wait=True)
+
+
+def _consumed(state_after: np.ndarray, walk: _Walk, pos: int) -> int:
+    """Draws between ``pos`` and a state reached from it by a short serial draw (< 32)."""
+    for k in range(0, 34):
+        if np.array_equal(walk.state(pos + k).numpy()[8:24 + 8 * 624], state_after[8:24 + 8 * 624]):
+            return k
+    raise RuntimeError("could not place a serial normal draw on the generator's stream")

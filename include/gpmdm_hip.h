@@ -330,6 +330,23 @@ int gpmdm_gp_factor(int device, const double* X, int64_t n, int32_t d, const dou
  * A matrix that is not positive definite is GPMDM_E_INVALID and *logdet is NaN. */
 int gpmdm_spd_inverse(int device, double* A_dev, int64_t n, double* logdet, void* stream);
 
+/* Replay-mode host helper (no GPU): positions along torch's CPU generator stream, so the
+ * reference's per-frame draws (gpmdm_pf.py:137-213: exponential_, normal_, the multinomial's
+ * uniforms, all from torch's global generator) can run as parallel chunks of torch's own
+ * samplers, each on a private generator set to the state the serial draw would have reached
+ * at that chunk -- bit for bit the serial streams.  `state` is torch.Generator.get_state()'s
+ * byte image (CPUGeneratorImplState, GPMDM_TORCH_GEN_STATE_BYTES bytes; MT19937,
+ * ATen/core/MT19937RNGEngine.h).  A walk covers n_draws random64 draws (two MT outputs each)
+ * from `state`; gpmdm_rng_walk_state writes the state after `draws` of them, with the
+ * normal-sample cache bytes of `cache_from` (NULL: the start state's). */
+#define GPMDM_TORCH_GEN_STATE_BYTES 5056
+typedef struct gpmdm_rng_walk* gpmdm_rng_walk_t;
+int gpmdm_rng_walk_create(const uint8_t* state, int64_t n_draws, gpmdm_rng_walk_t* out);
+/* restart a walk at another state (its buffer is reused when large enough) */
+int gpmdm_rng_walk_reset(gpmdm_rng_walk_t walk, const uint8_t* state, int64_t n_draws);
+int gpmdm_rng_walk_state(gpmdm_rng_walk_t walk, int64_t draws, const uint8_t* cache_from, uint8_t* out_state);
+int gpmdm_rng_walk_destroy(gpmdm_rng_walk_t walk);
+
 /* Message of the last failed call on this thread ("" if none). */
 const char* gpmdm_last_error(void);
 

@@ -1,0 +1,85 @@
+"""GPU: the drop-in default (rng='torch': the reference's draws from torch's global
+generator, gpmdm_pf.py:137-213) at the headline's particle count.
+
+From 16384 particles the filter draws torch's streams as parallel chunks of torch's own
+samplers (replay.ParallelFrameDraws, placed by gpmdm_rng_walk), the next frame's switch
+draws and first-class normals ahead on a background thread.  It must be bit for bit the
+serial draws: the same filter with the serial FrameDraws takes the same classes, counts,
+states and read-outs over several frames, and leaves torch's generator in the same state;
+one step against the oracle with the draws it consumed checks the device side."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_step_matches, load_fixture, oracle_model, product_model
+
+pytestmark = pytest.mark.gpu
+
+P = 100_000
+
+
+@pytest.fixture(scope="module")
+def model():
+    f = load_fixture("config2_n2000_p1000")
+    return f, product_model(f), torch.tensor(np.asarray(f["T"], dtype=np.float64))
+
+
+def _frames(pf, Y, n, between=None):
+    outs = []
+    for k in range(n):
+        pf.update(np.asarray(Y[60 + 7 * k], dtype=np.float64) + 0.01)
+        outs.append((pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), pf._counts.copy(),
+                     torch.get_rng_state().clone()))
+        if between is not None and k == 1:
+            between()
+    return outs, pf.export_state()
+
+
+@pytest.mark.parametrize("interleave", [False, True])
+def test_parallel_replay_is_the_serial_replay(model, monkeypatch, interleave):
+    from gpmdm_amd import GPMDM_PF, replay
+    from gpmdm_amd import pf as pfmod
+    f, m, T = model
+    Y = m.get_Y()
+    between = (lambda: torch.randn(5)) if interleave else None   # a user's own draw between frames
+    torch.manual_seed(17)
+    par = GPMDM_PF(m, T, P)
+    a, sa = _frames(par, Y, 4, between)
+    assert isinstance(par._draws, replay.ParallelFrameDraws)
+    assert par._draws.prefetch_hits >= (1 if interleave else 3)
+    monkeypatch.setattr(pfmod, "PARALLEL_REPLAY_P", 10 ** 12)
+    torch.manual_seed(17)
+    ser = GPMDM_PF(m, T, P)
+    b, sb = _frames(ser, Y, 4, between)
+    assert isinstance(ser._draws, replay.FrameDraws)
+    for k, (x, y) in enumerate(zip(a, b)):
+        assert np.array_equal(x[2], y[2]), (k, "class counts")
+        assert np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]), (k, "read-outs")
+        assert torch.equal(x[3], y[3]), (k, "torch generator state after the frame")
+    for key in ("states", "classes", "ll", "w", "resample_idx"):
+        assert np.array_equal(sa[key], sb[key]), key
+
+
+def test_parallel_replay_step_vs_oracle(model):
+    """One resynced step at P = 100k: the device consumes the parallel draws as the oracle
+    consumes them (weights, resample indices, states, read-outs)."""
+    from gpmdm_amd import GPMDM_PF
+    from oracle import gpmdm_oracle as O
+    f, m, T = model
+    Y = m.get_Y()
+    om = oracle_model(f)
+    torch.manual_seed(23)
+    pf = GPMDM_PF(m, T, P)
+    pf.update(np.asarray(Y[30], dtype=np.float64) + 0.01)
+    pf._draws.record = True                 # copies of the frame's draws (E and N are refilled ahead)
+    pre = pf.export_state()
+    z = np.asarray(Y[31], dtype=np.float64) + 0.01
+    pf.update(z)
+    dr = pf._draws
+    post = pf.export_state()
+    r = O.step(om, f["T"], pre["states"], pre["classes"], z, dr.last_E, dr.last_N, dr.last_U)
+    assert np.array_equal(r.classes_switched, O.switch_classes(pre["classes"], f["T"], dr.last_E))
+    counts = np.bincount(r.classes_switched, minlength=T.shape[0])
+    assert np.array_equal(counts, pf._counts)             # the device's counts are the oracle's
+    assert_step_matches(post, r, pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), dr.last_U,
+                        what="replay P=100k")
