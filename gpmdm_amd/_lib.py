@@ -55,6 +55,8 @@ _SIGS = {
     "gpmdm_pf_shape": (c_int, [c_void_p, _i64p, _i64p]),
     "gpmdm_pf_init": (c_int, [c_void_p, _dp, _i64p]),
     "gpmdm_pf_import": (c_int, [c_void_p, _dp, _i64p, _dp, _dp, _dp, _i64p, c_int64]),
+    "gpmdm_pf_draw_buffers": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p)]),
+    "gpmdm_pf_draws_free": (c_int, [c_void_p, c_int]),
     "gpmdm_pf_switch": (c_int, [c_void_p, _dp, _i64p, c_void_p]),
     "gpmdm_pf_propagate": (c_int, [c_void_p, _dp, _dp, c_void_p]),
     "gpmdm_pf_propagate_dynamics": (c_int, [c_void_p, _dp, c_void_p]),

@@ -242,7 +242,8 @@ struct gpmdm_pf {
   hipError_t upload_draws(int k, double* dst, const double* src, size_t n, hipStream_t s) {
     hipError_t e = hipEventSynchronize(rep_ev[k]);   // the buffer's previous readers have run
     if (e != hipSuccess) return e;
-    std::memcpy(rep_pin[k], src, sizeof(double) * n);
+    // draws written straight into the staging buffer (gpmdm_pf_draw_buffers): no copy
+    if (src != rep_pin[k]) std::memcpy(rep_pin[k], src, sizeof(double) * n);
     if (sizeof(double) * n <= kZeroCopyBytes && rep_dev[k]) {
       rep_src[k] = rep_dev[k];
       return hipSuccess;
@@ -825,6 +826,24 @@ int gpmdm_pf_create(gpmdm_model_t m, const double* T, int64_t P, int rng_mode, u
 int gpmdm_bank_create(gpmdm_model_t m, const double* T, int64_t n_filters, int64_t P, uint64_t seed,
                       int resample_mode, gpmdm_pf_t* out) {
   return pf_create(m, T, n_filters, P, GPMDM_RNG_PHILOX, seed, resample_mode, 1, 0, out);
+}
+
+int gpmdm_pf_draw_buffers(gpmdm_pf_t pf, double** exp_draws, double** normals, double** uniforms) {
+  CHECK(pf, "null handle");
+  CHECK(pf->rng_mode == GPMDM_RNG_REPLAY, "draw buffers belong to replay filters");
+  if (exp_draws) *exp_draws = pf->rep_pin[0];
+  if (normals) *normals = pf->rep_pin[1];
+  if (uniforms) *uniforms = pf->rep_pin[2];
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_draws_free(gpmdm_pf_t pf, int which) {
+  CHECK(pf, "null handle");
+  CHECK(pf->rng_mode == GPMDM_RNG_REPLAY, "draw buffers belong to replay filters");
+  CHECK(which >= 0 && which < 3, "which: 0 exp draws, 1 normals, 2 uniforms");
+  HIPCHK(hipSetDevice(pf->m->device));
+  HIPCHK(hipEventSynchronize(pf->rep_ev[which]));
+  return GPMDM_OK;
 }
 
 int gpmdm_pf_shape(gpmdm_pf_t pf, int64_t* n_filters, int64_t* P) {

@@ -145,6 +145,9 @@ class GPMDM_PF:
 
     def __del__(self):
         try:
+            dr = getattr(self, "_draws", None)
+            if dr is not None and hasattr(dr, "close"):
+                dr.close()                      # draws ahead write into the handle's buffers: join them
             if getattr(self, "_h", None) is not None and self._h.value:
                 _lib.load().gpmdm_pf_destroy(self._h)
                 self._h = None
@@ -203,8 +206,18 @@ class GPMDM_PF:
             if self._draws is None:
                 nu = P if self._resample_mode == "multinomial" else 1
                 if P >= PARALLEL_REPLAY_P and replay.host_threads() > 1:
-                    # torch's own samplers in parallel chunks, bit for bit the serial streams
-                    self._draws = replay.ParallelFrameDraws(P, C, d, nu)
+                    # torch's own samplers in parallel chunks, bit for bit the serial streams,
+                    # drawn straight into the library's pinned staging buffers (no copy)
+                    pe, pn, pu = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+                    _lib.check(lib.gpmdm_pf_draw_buffers(h, ctypes.byref(pe), ctypes.byref(pn), ctypes.byref(pu)),
+                               "draw buffers")
+                    bufs = (np.ctypeslib.as_array(ctypes.cast(pe, ctypes.POINTER(ctypes.c_double)), (P, C)),
+                            np.ctypeslib.as_array(ctypes.cast(pn, ctypes.POINTER(ctypes.c_double)), (P, d)),
+                            np.ctypeslib.as_array(ctypes.cast(pu, ctypes.POINTER(ctypes.c_double)), (nu,)))
+                    hh = self._h
+                    self._draws = replay.ParallelFrameDraws(
+                        P, C, d, nu, buffers=bufs,
+                        wait_free=lambda k: _lib.check(_lib.load().gpmdm_pf_draws_free(hh, k), "draw buffer"))
                 else:
                     self._draws = replay.FrameDraws(P, C, d, nu)
                 self._counts = np.zeros(C, dtype=np.int64)

@@ -188,17 +188,22 @@ class ParallelFrameDraws:
     reference's whatever the caller does between frames."""
 
     def __init__(self, P: int, C: int, d: int, n_uniform: int, threads: Optional[int] = None,
-                 chunk: int = 4096):
+                 chunk: int = 8192, buffers=None, wait_free=None):
+        """``buffers``: (E, N, U) float64 numpy arrays to draw into (e.g. the library's
+        pinned staging buffers, gpmdm_pf_draw_buffers), else own ones; ``wait_free(k)``
+        (k = 0 E, 1 N, 2 U) returns once buffer k may be rewritten (gpmdm_pf_draws_free)."""
         from concurrent.futures import ThreadPoolExecutor
         self.P, self.C, self.d, self.nu = int(P), int(C), int(d), int(n_uniform)
         self.threads = threads or host_threads()
         self._pool = ThreadPoolExecutor(max_workers=self.threads)
         self._bg = ThreadPoolExecutor(max_workers=1)
         self._chunk = int(chunk)
-        self._E = torch.empty((P, C), dtype=torch.float64)
-        self._N = torch.empty((P, d), dtype=torch.float64)
-        self._U = torch.empty((self.nu,), dtype=torch.float64)
-        self.E, self.N, self.U = self._E.numpy(), self._N.numpy(), self._U.numpy()
+        if buffers is None:
+            buffers = (np.empty((P, C)), np.empty((P, d)), np.empty((self.nu,)))
+        self.E, self.N, self.U = (np.asarray(b, dtype=np.float64) for b in buffers)
+        assert self.E.shape == (P, C) and self.N.shape == (P, d) and self.U.shape == (self.nu,)
+        self._E, self._N, self._U = (torch.from_numpy(b) for b in (self.E, self.N, self.U))
+        self._wait_free = wait_free or (lambda k: None)
         self._walks = (_Walk(), _Walk())   # this frame's and the next frame's (buffers reused)
         self._wi = 0
         self._walk = None
@@ -241,6 +246,8 @@ class ParallelFrameDraws:
         """The frame's draws that need no device result: E, and the first class's normals
         for the longest length (all P particles)."""
         walk.reset(state, self._frame_draws())
+        self._wait_free(0)
+        self._wait_free(1)
         flat = self._E.view(-1)
         n, step = flat.numel(), max(self._chunk, -(-flat.numel() // self.threads))
         tasks = []
@@ -316,6 +323,7 @@ class ParallelFrameDraws:
         """The resampling uniforms; the global generator then stands where the serial
         frame would leave it, and the next frame's draws ahead start in the background."""
         walk, n = self._walk, self.nu
+        self._wait_free(2)
         step = max(self._chunk, -(-n // self.threads))
         tasks = []
         for a in range(0, n, step):

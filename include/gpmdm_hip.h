@@ -145,6 +145,15 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes);
 int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes, const double* ll,
                     const double* log_w, const double* w, const int64_t* ridx, int64_t frame);
 
+/* Replay filters: the library's own pinned staging buffers of the three draw streams
+ * (exp draws P x C, normals P x d, uniforms P), so a host can draw straight into them.
+ * Passing these very pointers to gpmdm_pf_switch / gpmdm_pf_propagate / gpmdm_pf_resample
+ * skips the copy into staging.  A buffer may be written only when gpmdm_pf_draws_free
+ * (which = 0, 1, 2) has returned: it waits until the launches that read the buffer's last
+ * contents have run. */
+int gpmdm_pf_draw_buffers(gpmdm_pf_t pf, double** exp_draws, double** normals, double** uniforms);
+int gpmdm_pf_draws_free(gpmdm_pf_t pf, int which);
+
 /* _propogate_markov_switching  (gpmdm_pf.py:137-151).  exp_draws: P x C host (replay)
  * or NULL (philox).  class_counts: C host, or NULL; when given, the post-switch class
  * counts are returned (the replay caller needs them to draw the per-class normals of the
