@@ -194,6 +194,11 @@ struct gpmdm_pf {
   unsigned seed_lo = 0, seed_hi = 0, frame = 0;
   bool initialised = false, switched = false, propagated = false;
   bool dyn_done = false;             // gpmdm_pf_propagate_dynamics ran, gpmdm_pf_weigh not yet
+  // replay filters whose caller draws the normals after the switch's class counts: the
+  // switch launches the dynamics-GP tiles (they need no normals) before it waits for the
+  // counts, so they run while the host draws; propagate then launches the finish only
+  bool gemm_ahead = false;
+  hipEvent_t cnt_done = nullptr;      // after the switch's class counts (replay, large filters)
   bool dedup = true;                  // ancestor de-duplication of the dynamics GP
   int dyn_tiles = GPMDM_DYN_TILES_AUTO;   // gpmdm_pf_set_dyn_tiles
   bool wide_dyn() const { return dyn_tiles == GPMDM_DYN_TILES_WIDE || (dyn_tiles == GPMDM_DYN_TILES_AUTO && !dedup); }
@@ -383,6 +388,7 @@ struct gpmdm_pf {
     if (cnt_ev) (void)hipEventDestroy(cnt_ev);
     if (sw_ev) (void)hipEventDestroy(sw_ev);
     if (ro_ev) (void)hipEventDestroy(ro_ev);
+    if (cnt_done) (void)hipEventDestroy(cnt_done);
     if (ro_pin) (void)hipHostFree(ro_pin);
     for (int k = 0; k < 2; ++k) {
       if (zpin[k]) (void)hipHostFree(zpin[k]);
@@ -799,6 +805,10 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
       pf->T_host.assign(T, T + (size_t)C * C);
     }
   }
+  if (rng_mode == GPMDM_RNG_REPLAY && hipEventCreateWithFlags(&pf->cnt_done, hipEventDisableTiming) != hipSuccess) {
+    delete pf;
+    return fail(GPMDM_E_HIP, "filter events");
+  }
   if (hipEventCreateWithFlags(&pf->sw_ev, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&pf->ro_ev, hipEventDisableTiming) != hipSuccess) {
     delete pf;
@@ -982,7 +992,7 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   pf->ro_ev_ok = true;
   pf->initialised = true;
   pf->own_valid = false;               // no ancestors yet: identity ownership
-  pf->switched = pf->propagated = pf->dyn_done = pf->ll_pending = false;
+  pf->switched = pf->propagated = pf->dyn_done = pf->ll_pending = pf->gemm_ahead = false;
   return GPMDM_OK;
 }
 
@@ -1056,9 +1066,11 @@ int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes,
   HIPCHK(hipDeviceSynchronize());
   pf->ro_ev_ok = true;
   pf->initialised = true;
-  pf->switched = pf->propagated = pf->dyn_done = false;
+  pf->switched = pf->propagated = pf->dyn_done = pf->gemm_ahead = false;
   return GPMDM_OK;
 }
+
+static void launch_dyn_gemm(gpmdm_pf* pf, hipStream_t s);
 
 static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipStream_t s) {
   gpmdm_model* m = pf->m;
@@ -1194,7 +1206,17 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
       HIPCHK(hipMemcpyAsync(tmp, pf->counts(), sizeof(int) * C, hipMemcpyDeviceToHost, s));
       src = tmp;
     }
-    HIPCHK(hipStreamSynchronize(s));
+    if (pf->cnt_done && pf->nloc > 0) {
+      // the dynamics-GP tiles need the switch's tables, not the normals the caller draws
+      // from these counts: they run while it draws (propagate launches the finish only)
+      HIPCHK(hipEventRecord(pf->cnt_done, s));
+      launch_dyn_gemm(pf, s);
+      HIPCHK(hipGetLastError());
+      pf->gemm_ahead = true;
+      HIPCHK(hipEventSynchronize(pf->cnt_done));
+    } else {
+      HIPCHK(hipStreamSynchronize(s));
+    }
     for (int c = 0; c < C; ++c) class_counts[c] = src[c];
   }
   pf->switched = true;
@@ -1220,6 +1242,62 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   return do_switch(pf, E, class_counts, s);
 }
 
+// The dynamics-GP tile launches of this rank's rows (per class, segments of at most kMaxSeg
+// classes per launch): narrow tiles for the de-duplicated rows, the wide image when every
+// particle is evaluated.  They need the switch's tables only, not the normals.
+static void launch_dyn_gemm(gpmdm_pf* pf, hipStream_t s) {
+  gpmdm_model* m = pf->m;
+  const int C = m->C, d = m->d;
+  const long long nl = pf->nloc;
+  const std::vector<GpImage>& dset = m->dyn_set(pf->wide_dyn());
+  // Diagnostic (GPMDM_DYN_EXACT_GRID=1): read the leader tile counts back (a host sync)
+  // and launch exactly the non-empty tiles instead of the device-unknown upper bound --
+  // measures what the empty workgroups of the bound cost.  Not the production schedule.
+  static const bool exact_grid = std::getenv("GPMDM_DYN_EXACT_GRID") != nullptr;
+  int ltiles[kMaxClasses + 1] = {0};
+  if (exact_grid && pf->dedup) {
+    (void)hipMemcpyAsync(ltiles, pf->lseg_tiles(), sizeof(int) * (C + 1), hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
+  }
+  hipEvent_t t0;
+  pf->mark_begin(s, GPMDM_STAGE_DYN_GEMM, t0);
+  for (int c0 = 0; c0 < C; c0 += kMaxSeg) {
+    const int ns = std::min(kMaxSeg, C - c0);
+    TileParams tp{};
+    int njm = 0;
+    for (int k = 0; k < ns; ++k) {
+      tp.seg[k] = dset[c0 + k].seg();
+      njm = std::max(njm, dset[c0 + k].n_j);
+    }
+    tp.n_seg = ns;
+    tp.geo = dset[c0].geo;           // tile starts computed on the device in units of pt
+    tp.tiles_ub = (int)(cdiv(nl, tp.geo.pt()) + ns);
+    if (exact_grid && pf->dedup) tp.tiles_ub = std::max(ltiles[c0 + ns] - ltiles[c0], 1);
+    tp.n_j_max = njm;
+    if (pf->dedup) {                  // one row per (ancestor, class) leader
+      tp.seg_pos_begin = pf->lseg_begin() + c0;
+      tp.seg_pos_end = pf->lseg_end() + c0;
+      tp.seg_out_base = pf->lseg_out() + c0;
+      tp.seg_tile_start = pf->lseg_tiles() + c0;
+      tp.perm = pf->lperm;
+    } else {
+      tp.seg_pos_begin = pf->seg_begin() + c0;
+      tp.seg_pos_end = pf->seg_end() + c0;
+      tp.seg_out_base = pf->seg_out() + c0;
+      tp.seg_tile_start = pf->seg_tiles() + c0;
+      tp.perm = pf->perm;
+    }
+    tp.X = pf->X;
+    fill_tile_common(tp, m, true);
+    tp.qpart = pf->qdyn;
+    tp.ld_q = nl;
+    tp.mu = pf->mudyn;
+    tp.ld_mu = d;
+    launch_gp_tile(tp, d, true, s);
+  }
+  pf->mark_end(s, GPMDM_STAGE_DYN_GEMM, t0);
+}
+
 // _propogate_dynamics for this rank's particles (gpmdm_pf.py:153-168): the dynamics GP per
 // class (de-duplicated rows or every particle) and the new states X_prop.
 // zstage: the frame's observation, already in the mapped staging slot zpin[zslot] (the
@@ -1233,55 +1311,10 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
   }
   const long long nl = pf->nloc;
   if (nl > 0) {
-    // ---- dynamics GP per class (segments of at most kMaxSeg classes per launch) ----
-    // narrow tiles for the de-duplicated rows, the wide image when every particle is evaluated
     const std::vector<GpImage>& dset = m->dyn_set(pf->wide_dyn());
-    // Diagnostic (GPMDM_DYN_EXACT_GRID=1): read the leader tile counts back (a host sync)
-    // and launch exactly the non-empty tiles instead of the device-unknown upper bound --
-    // measures what the empty workgroups of the bound cost.  Not the production schedule.
-    static const bool exact_grid = std::getenv("GPMDM_DYN_EXACT_GRID") != nullptr;
-    int ltiles[kMaxClasses + 1] = {0};
-    if (exact_grid && pf->dedup) {
-      HIPCHK(hipMemcpyAsync(ltiles, pf->lseg_tiles(), sizeof(int) * (C + 1), hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-    }
+    if (!pf->gemm_ahead) launch_dyn_gemm(pf, s);   // (replay: launched by the switch already)
+    pf->gemm_ahead = false;
     hipEvent_t t0;
-    pf->mark_begin(s, GPMDM_STAGE_DYN_GEMM, t0);
-    for (int c0 = 0; c0 < C; c0 += kMaxSeg) {
-      const int ns = std::min(kMaxSeg, C - c0);
-      TileParams tp{};
-      int njm = 0;
-      for (int k = 0; k < ns; ++k) {
-        tp.seg[k] = dset[c0 + k].seg();
-        njm = std::max(njm, dset[c0 + k].n_j);
-      }
-      tp.n_seg = ns;
-      tp.geo = dset[c0].geo;           // tile starts computed on the device in units of pt
-      tp.tiles_ub = (int)(cdiv(nl, tp.geo.pt()) + ns);
-      if (exact_grid && pf->dedup) tp.tiles_ub = std::max(ltiles[c0 + ns] - ltiles[c0], 1);
-      tp.n_j_max = njm;
-      if (pf->dedup) {                  // one row per (ancestor, class) leader
-        tp.seg_pos_begin = pf->lseg_begin() + c0;
-        tp.seg_pos_end = pf->lseg_end() + c0;
-        tp.seg_out_base = pf->lseg_out() + c0;
-        tp.seg_tile_start = pf->lseg_tiles() + c0;
-        tp.perm = pf->lperm;
-      } else {
-        tp.seg_pos_begin = pf->seg_begin() + c0;
-        tp.seg_pos_end = pf->seg_end() + c0;
-        tp.seg_out_base = pf->seg_out() + c0;
-        tp.seg_tile_start = pf->seg_tiles() + c0;
-        tp.perm = pf->perm;
-      }
-      tp.X = pf->X;
-      fill_tile_common(tp, m, true);
-      tp.qpart = pf->qdyn;
-      tp.ld_q = nl;
-      tp.mu = pf->mudyn;
-      tp.ld_mu = d;
-      launch_gp_tile(tp, d, true, s);
-    }
-    pf->mark_end(s, GPMDM_STAGE_DYN_GEMM, t0);
     pf->mark_begin(s, GPMDM_STAGE_DYN_FINISH, t0);
     DynFinishArgs fa{};
     fa.n_out = nl;
