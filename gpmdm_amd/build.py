@@ -97,7 +97,7 @@ def _build_lib(force: bool = False, verbose: bool = False) -> Path:
         # snapshot of the tree) never sees a partly written file
         tmp = LIB.with_suffix(".so.tmp")
         run([cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs,
-             "-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
+             "-L/opt/rocm/lib", "-lrocsolver", "-lrocblas", "-ldl", "-Wl,-rpath,/opt/rocm/lib"])
         os.replace(tmp, LIB)
     return LIB
 

@@ -9,7 +9,11 @@
 #include <string>
 #include <vector>
 
-#include <rccl/rccl.h>
+#include <dlfcn.h>
+#include <mutex>
+#include <type_traits>
+
+#include <rccl/rccl.h>   // types only: the entry points are resolved at run time (rccl())
 
 #include "../../include/gpmdm_hip.h"
 #include "common.h"
@@ -28,6 +32,59 @@ int fail(int code, const std::string& msg) {
 }  // namespace gpmdm
 
 static_assert(kMaxClassesDesc == kMaxClasses, "descriptor check and kernels agree on the class limit");
+
+// RCCL entry points, resolved from librccl.so.1 on the first call that needs a communicator
+// (gpmdm_comm_*, gpmdm_pf_set_comm): a single-GPU user needs no RCCL at build or load time,
+// and a process that already holds torch's RCCL gets that same library (same soname).
+struct RcclApi {
+  bool ok = false;
+  std::string why;
+  ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*CommCount)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*CommUserRank)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*CommCuDevice)(const ncclComm_t, int*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+
+static const RcclApi& rccl() {
+  static RcclApi api;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+      const char* e = dlerror();
+      api.why = std::string("RCCL is not available (librccl.so.1): ") + (e ? e : "");
+      return;
+    }
+    bool all = true;
+    auto get = [&](auto& fp, const char* name) {
+      fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+      if (!fp) {
+        all = false;
+        api.why = std::string("librccl.so.1 lacks ") + name;
+      }
+    };
+    get(api.AllGather, "ncclAllGather");
+    get(api.CommCount, "ncclCommCount");
+    get(api.CommUserRank, "ncclCommUserRank");
+    get(api.CommCuDevice, "ncclCommCuDevice");
+    get(api.CommInitRank, "ncclCommInitRank");
+    get(api.CommDestroy, "ncclCommDestroy");
+    get(api.GetUniqueId, "ncclGetUniqueId");
+    get(api.GetErrorString, "ncclGetErrorString");
+    api.ok = all;
+  });
+  return api;
+}
+
+#define RCCL_OR_FAIL()                                                      \
+  do {                                                                     \
+    if (!rccl().ok) return fail(GPMDM_E_HIP, rccl().why);                  \
+  } while (0)
 
 namespace {
 
@@ -1464,14 +1521,14 @@ static int pack_part(gpmdm_pf* pf, double* send, int part, hipStream_t s);
 static int unpack_part(gpmdm_pf* pf, const double* recv, int part, hipStream_t s);
 
 static int nccl_fail(ncclResult_t r, const char* what) {
-  return fail(GPMDM_E_HIP, std::string(what) + ": " + ncclGetErrorString(r));
+  return fail(GPMDM_E_HIP, std::string(what) + ": " + (rccl().ok ? rccl().GetErrorString(r) : "RCCL missing"));
 }
 
 // rows [0, pad) of every rank's send buffer -> recv (even shards) or the staging buffer,
 // whose rank-k rows are then copied to [lo_k, hi_k) of recv (uneven shards), on cstream
 static int gather_rows(gpmdm_pf* pf, const double* send, double* recv, double* stage, int width) {
   const size_t cnt = (size_t)pf->pad * width;
-  const ncclResult_t r = ncclAllGather(send, pf->padded ? stage : recv, cnt, ncclDouble, pf->comm, pf->cstream);
+  const ncclResult_t r = rccl().AllGather(send, pf->padded ? stage : recv, cnt, ncclDouble, pf->comm, pf->cstream);
   if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
   if (pf->padded) {
     for (int k = 0; k < pf->n_ranks; ++k) {
@@ -1538,13 +1595,14 @@ int gpmdm_pf_set_comm(gpmdm_pf_t pf, void* rccl_comm, int flags) {
   pf->release_comm();
   if (!rccl_comm) return GPMDM_OK;
   CHECK(pf->F == 1, "filter banks shard filters, not particles: no communicator");
+  RCCL_OR_FAIL();
   ncclComm_t comm = (ncclComm_t)rccl_comm;
   int n = 0, r = 0, dev = -1;
-  ncclResult_t e = ncclCommCount(comm, &n);
+  ncclResult_t e = rccl().CommCount(comm, &n);
   if (e != ncclSuccess) return nccl_fail(e, "ncclCommCount");
-  e = ncclCommUserRank(comm, &r);
+  e = rccl().CommUserRank(comm, &r);
   if (e != ncclSuccess) return nccl_fail(e, "ncclCommUserRank");
-  e = ncclCommCuDevice(comm, &dev);
+  e = rccl().CommCuDevice(comm, &dev);
   if (e != ncclSuccess) return nccl_fail(e, "ncclCommCuDevice");
   CHECK(n == pf->n_ranks && r == pf->rank, "communicator size/rank differ from the filter's n_ranks/rank");
   CHECK(dev == pf->m->device, "communicator is on another device than the model");
@@ -1575,8 +1633,9 @@ int gpmdm_pf_set_comm(gpmdm_pf_t pf, void* rccl_comm, int flags) {
 
 int gpmdm_comm_unique_id(void* id) {
   CHECK(id, "null argument");
+  RCCL_OR_FAIL();
   ncclUniqueId u;
-  const ncclResult_t e = ncclGetUniqueId(&u);
+  const ncclResult_t e = rccl().GetUniqueId(&u);
   if (e != ncclSuccess) return nccl_fail(e, "ncclGetUniqueId");
   static_assert(sizeof(ncclUniqueId) == GPMDM_COMM_ID_BYTES, "ncclUniqueId size");
   std::memcpy(id, &u, sizeof(u));
@@ -1586,11 +1645,12 @@ int gpmdm_comm_unique_id(void* id) {
 int gpmdm_comm_init(int n_ranks, int rank, const void* id, int device, void** comm) {
   CHECK(id && comm && n_ranks >= 1 && rank >= 0 && rank < n_ranks, "bad argument");
   *comm = nullptr;
+  RCCL_OR_FAIL();
   HIPCHK(hipSetDevice(device));
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof(u));
   ncclComm_t c = nullptr;
-  const ncclResult_t e = ncclCommInitRank(&c, n_ranks, u, rank);
+  const ncclResult_t e = rccl().CommInitRank(&c, n_ranks, u, rank);
   if (e != ncclSuccess) return nccl_fail(e, "ncclCommInitRank");
   *comm = c;
   return GPMDM_OK;
@@ -1598,7 +1658,8 @@ int gpmdm_comm_init(int n_ranks, int rank, const void* id, int device, void** co
 
 int gpmdm_comm_destroy(void* comm) {
   if (!comm) return GPMDM_OK;
-  const ncclResult_t e = ncclCommDestroy((ncclComm_t)comm);
+  RCCL_OR_FAIL();
+  const ncclResult_t e = rccl().CommDestroy((ncclComm_t)comm);
   return e == ncclSuccess ? GPMDM_OK : nccl_fail(e, "ncclCommDestroy");
 }
 

@@ -92,7 +92,9 @@ class GPMDM(torch.nn.Module):
     (``.to()`` moves them as for any module); the device model -- factors and packed tile
     images in libgpmdm_hip -- lives on ``device`` and is rebuilt whenever the parameters
     change, including in-place updates by an optimiser (detected through the parameters'
-    version counters on the next use).
+    version counters on the next use).  An edit through ``.data`` (``m.X.data.mul_(2)``)
+    bypasses the version counter and is not detected: call ``refresh(force=True)`` after
+    one.
 
     Constructor arguments are those of the reference (gpmdm.py:96-109).  ``dtype`` must be
     float64 (the reference default, required for parity: SURVEY.md §8(c)).  ``device`` is
@@ -188,6 +190,15 @@ class GPMDM(torch.nn.Module):
         optimiser step over parameters(), a .to(), an in-place edit)."""
         if self.X is not None and self._handle is not None and self._uploaded != self._param_versions():
             self._precompute_kernel_inverses()
+
+    def refresh(self, force: bool = False) -> None:
+        """Rebuild the device model if the parameters changed (``force``: always -- after
+        edits through ``.data``, which the parameters' version counters do not see).
+        Filters built on the model rebind on their next call."""
+        if force and self.X is not None:
+            self._precompute_kernel_inverses()
+        else:
+            self._refresh()
 
     # ---- reference API: data registry (gpmdm.py:239-309) -------------------------
     def set_evaluation_mode(self):
@@ -663,16 +674,33 @@ class GPMDM(torch.nn.Module):
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
         """nn.Module.load_state_dict by the reference's names (gpmdm.py:1402), then the device
         model is rebuilt (filters built on this model rebind on their next call).  A model
-        without latents yet takes X's shape from the state dict."""
-        if self.X is None and "X" in state_dict:
-            self._set_param("X", state_dict["X"])
+        without latents yet takes X's shape from the state dict.  As nn.Module, the whole
+        dict is checked before anything is installed: with ``strict`` missing / unexpected
+        keys raise, and a value whose shape differs from its parameter's (X: another number
+        of latents than the model holds) raises a size-mismatch error naming the key; a
+        rejected dict leaves the model unchanged."""
         missing = [k for k in self._PARAMS if k not in state_dict]
         unexpected = [k for k in state_dict if k not in self._PARAMS]
         if strict and (missing or unexpected):
             raise RuntimeError(f"load_state_dict: missing keys {missing}, unexpected keys {unexpected}")
+        vals = {}
         for k in self._PARAMS:
-            if k in state_dict:
-                self._set_param(k, torch.as_tensor(_to_np(state_dict[k])).reshape(getattr(self, k).shape))
+            if k not in state_dict:
+                continue
+            v = torch.as_tensor(_to_np(state_dict[k]))
+            cur = getattr(self, k)
+            if cur is None:                          # X of a model without latents yet
+                if v.dim() != 2 or v.shape[1] != self.d:
+                    raise RuntimeError(f"load_state_dict: size mismatch for {k}: expected (N, {self.d}), "
+                                       f"got {tuple(v.shape)}")
+            elif v.numel() != cur.numel() or (v.dim() > 1 and tuple(v.shape) != tuple(cur.shape)):
+                raise RuntimeError(f"load_state_dict: size mismatch for {k}: copying a param with shape "
+                                   f"{tuple(v.shape)}, the shape in the current model is {tuple(cur.shape)}")
+            else:
+                v = v.reshape(cur.shape)
+            vals[k] = v
+        for k, v in vals.items():
+            self._set_param(k, v)
         if self.X is not None:
             self._precompute_kernel_inverses()
         return torch.nn.modules.module._IncompatibleKeys(missing, unexpected)
@@ -686,7 +714,13 @@ class GPMDM(torch.nn.Module):
           ``GPMDM.load`` and this class's ``load`` both read;
         * ``.npz``: a pickle-free archive (the torch layout holds numpy arrays, which
           ``torch.load(weights_only=True)`` reads only with numpy allow-listed)."""
-        if Path(file_path).suffix != ".npz":
+        suffix = Path(file_path).suffix
+        if suffix != ".npz":
+            if suffix not in (".pth", ".pt"):
+                import warnings
+                warnings.warn(f"GPMDM.save({str(file_path)!r}): writing the reference's torch layout (a pickle) "
+                              "to exactly this path; use a '.npz' suffix for the pickle-free archive",
+                              stacklevel=2)
             return self._save_reference_layout(file_path)
         return self._save_npz(file_path)
 

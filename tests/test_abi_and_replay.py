@@ -133,3 +133,13 @@ def test_frame_draws_are_the_replay_streams():
         assert np.array_equal(fd.resample(), U)
     with pytest.raises(ValueError):
         fd.dynamics([1, 2, 3])
+
+
+def test_rccl_is_not_a_load_time_dependency():
+    """RCCL is resolved at run time by the communicator calls only: a
+    single-GPU user's process never needs librccl to load the library."""
+    import subprocess
+    from gpmdm_amd import _lib as L
+    out = subprocess.run(["readelf", "-d", str(L.LIB_PATH)], capture_output=True, text=True).stdout
+    needed = [ln for ln in out.splitlines() if "NEEDED" in ln]
+    assert needed and not any("rccl" in ln for ln in needed), needed

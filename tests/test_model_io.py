@@ -118,6 +118,39 @@ def test_state_dict_matches_reference_checkpoint():
         raise AssertionError("strict load_state_dict accepted a partial state")
 
 
+def test_load_state_dict_rejects_before_installing():
+    """A size mismatch names its key and, like a strict key mismatch, leaves the model as
+    it was (nothing is installed before the whole dict is checked)."""
+    from pathlib import Path
+    import pytest
+    pth = Path(__file__).resolve().parent / "golden" / "ref_checkpoint_config1.pth"
+    m = GPMDM.load(pth, upload=False)
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    bad = dict(before)
+    bad["y_log_lambdas"] = before["y_log_lambdas"] + 1.0
+    bad["X"] = before["X"][:-3]                      # fewer latents than the model holds
+    with pytest.raises(RuntimeError, match="size mismatch for X"):
+        m.load_state_dict(bad)
+    bad2 = dict(before, y_log_lambdas=before["y_log_lambdas"] + 1.0, extra=torch.zeros(1))
+    with pytest.raises(RuntimeError, match="unexpected keys"):
+        m.load_state_dict(bad2)
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, before[k]), k
+
+
+def test_save_warns_on_an_unusual_suffix(tmp_path):
+    import warnings
+    from pathlib import Path
+    pth = Path(__file__).resolve().parent / "golden" / "ref_checkpoint_config1.pth"
+    m = GPMDM.load(pth, upload=False)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        m.save(tmp_path / "model.bin")
+        m.save(tmp_path / "model.pth")
+    assert len(w) == 1 and "pickle" in str(w[0].message)
+    assert (tmp_path / "model.bin").exists() and (tmp_path / "model.pth").exists()
+
+
 def _structure(cfg, sd):
     """Keys, types, dtypes and shapes of a checkpoint (values aside)."""
     def desc(v):
