@@ -44,6 +44,9 @@ struct RcclApi {
   ncclResult_t (*CommUserRank)(const ncclComm_t, int*) = nullptr;
   ncclResult_t (*CommCuDevice)(const ncclComm_t, int*) = nullptr;
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
@@ -73,6 +76,9 @@ static const RcclApi& rccl() {
     get(api.CommUserRank, "ncclCommUserRank");
     get(api.CommCuDevice, "ncclCommCuDevice");
     get(api.CommInitRank, "ncclCommInitRank");
+    get(api.CommInitAll, "ncclCommInitAll");
+    get(api.GroupStart, "ncclGroupStart");
+    get(api.GroupEnd, "ncclGroupEnd");
     get(api.CommDestroy, "ncclCommDestroy");
     get(api.GetUniqueId, "ncclGetUniqueId");
     get(api.GetErrorString, "ncclGetErrorString");
@@ -1524,45 +1530,67 @@ static int nccl_fail(ncclResult_t r, const char* what) {
   return fail(GPMDM_E_HIP, std::string(what) + ": " + (rccl().ok ? rccl().GetErrorString(r) : "RCCL missing"));
 }
 
-// rows [0, pad) of every rank's send buffer -> recv (even shards) or the staging buffer,
-// whose rank-k rows are then copied to [lo_k, hi_k) of recv (uneven shards), on cstream
+// rows [0, pad) of every rank's send buffer -> recv (even shards) or the staging buffer
+// (uneven shards), on cstream: the collective only (inside an ncclGroupStart/End a
+// host-driven copy would be enqueued before the grouped collective itself)
 static int gather_rows(gpmdm_pf* pf, const double* send, double* recv, double* stage, int width) {
   const size_t cnt = (size_t)pf->pad * width;
   const ncclResult_t r = rccl().AllGather(send, pf->padded ? stage : recv, cnt, ncclDouble, pf->comm, pf->cstream);
   if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
-  if (pf->padded) {
-    for (int k = 0; k < pf->n_ranks; ++k) {
-      const long long lo = pf->P * k / pf->n_ranks, hi = pf->P * (k + 1) / pf->n_ranks;
-      if (hi > lo)
-        HIPCHK(hipMemcpyAsync(recv + lo * width, stage + (size_t)k * cnt, sizeof(double) * (hi - lo) * width,
-                              hipMemcpyDeviceToDevice, pf->cstream));
-    }
+  return GPMDM_OK;
+}
+
+// uneven shards: each rank k's rows of the staging buffer down to [lo_k, hi_k) of recv
+static int gather_copy_down(gpmdm_pf* pf, double* recv, const double* stage, int width) {
+  if (!pf->padded) return GPMDM_OK;
+  const size_t cnt = (size_t)pf->pad * width;
+  for (int k = 0; k < pf->n_ranks; ++k) {
+    const long long lo = pf->P * k / pf->n_ranks, hi = pf->P * (k + 1) / pf->n_ranks;
+    if (hi > lo)
+      HIPCHK(hipMemcpyAsync(recv + lo * width, stage + (size_t)k * cnt, sizeof(double) * (hi - lo) * width,
+                            hipMemcpyDeviceToDevice, pf->cstream));
   }
   return GPMDM_OK;
 }
 
-// propagate with the library's own exchange (gpmdm_pf_set_comm), the schedule of
-// gpmdm_amd/pf.py's process-group path: {class, state} all-gathered on the library stream
-// while the observation GP runs on the caller's stream, then {ll}; the caller's stream
-// waits for both gathers before unpacking (replaces the reference's single-process
-// normalise/resample inputs, gpmdm_pf.py:194-213).
-static int propagate_exchange(gpmdm_pf* pf, const double* zh, const double* normals, hipStream_t s) {
-  const int d = pf->m->d;
+// The library's exchange (gpmdm_pf_set_comm) in stages, the schedule of gpmdm_amd/pf.py's
+// process-group path: {class, state} all-gathered on the library stream while the
+// observation GP runs on the caller's stream, then {ll}; the caller's stream waits for both
+// gathers before unpacking (replaces the reference's single-process hand-over to
+// normalise / resample, gpmdm_pf.py:194-213).  One rank per process runs them in sequence
+// (propagate_exchange); one process driving several devices runs each stage for every
+// rank and groups the collectives (gpmdm_pf_propagate_multi).
+static int exch_states(gpmdm_pf* pf, const double* normals, hipStream_t s) {
   TRY(propagate_dynamics(pf, normals, s));
   TRY(pack_part(pf, pf->xs_send, GPMDM_PACK_STATES, s));
   HIPCHK(hipEventRecord(pf->cev[0], s));
   HIPCHK(hipStreamWaitEvent(pf->cstream, pf->cev[0], 0));
-  TRY(gather_rows(pf, pf->xs_send, pf->xs_recv, pf->xs_stage, d + 1));
+  return GPMDM_OK;
+}
+static int exch_ll(gpmdm_pf* pf, const double* zh, hipStream_t s) {
   TRY(weigh(pf, zh, s));
   TRY(pack_part(pf, pf->xl_send, GPMDM_PACK_LL, s));
   HIPCHK(hipEventRecord(pf->cev[1], s));
   HIPCHK(hipStreamWaitEvent(pf->cstream, pf->cev[1], 0));
-  TRY(gather_rows(pf, pf->xl_send, pf->xl_recv, pf->xl_stage, 1));
+  return GPMDM_OK;
+}
+static int exch_finish(gpmdm_pf* pf, hipStream_t s) {
   HIPCHK(hipEventRecord(pf->cev[2], pf->cstream));
   HIPCHK(hipStreamWaitEvent(s, pf->cev[2], 0));
   TRY(unpack_part(pf, pf->xs_recv, GPMDM_PACK_STATES, s));
   TRY(unpack_part(pf, pf->xl_recv, GPMDM_PACK_LL, s));
   return GPMDM_OK;
+}
+
+static int propagate_exchange(gpmdm_pf* pf, const double* zh, const double* normals, hipStream_t s) {
+  const int d = pf->m->d;
+  TRY(exch_states(pf, normals, s));
+  TRY(gather_rows(pf, pf->xs_send, pf->xs_recv, pf->xs_stage, d + 1));
+  TRY(gather_copy_down(pf, pf->xs_recv, pf->xs_stage, d + 1));
+  TRY(exch_ll(pf, zh, s));
+  TRY(gather_rows(pf, pf->xl_send, pf->xl_recv, pf->xl_stage, 1));
+  TRY(gather_copy_down(pf, pf->xl_recv, pf->xl_stage, 1));
+  return exch_finish(pf, s);
 }
 
 int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, void* stream) {
@@ -1584,6 +1612,58 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
     return rc;
   }
   return weigh(pf, zh, (hipStream_t)stream);
+}
+
+// One stage's all-gathers of every rank's filter driven by this thread, grouped (a single
+// thread that drives several ranks must group their collectives), then the copy-downs.
+static int group_gather(gpmdm_pf* const* pfs, int n, bool states) {
+  ncclResult_t e = rccl().GroupStart();
+  if (e != ncclSuccess) return nccl_fail(e, "ncclGroupStart");
+  int rc = GPMDM_OK;
+  for (int i = 0; i < n && rc == GPMDM_OK; ++i) {
+    gpmdm_pf* pf = pfs[i];
+    rc = states ? gather_rows(pf, pf->xs_send, pf->xs_recv, pf->xs_stage, pf->m->d + 1)
+                : gather_rows(pf, pf->xl_send, pf->xl_recv, pf->xl_stage, 1);
+  }
+  e = rccl().GroupEnd();
+  if (rc != GPMDM_OK) return rc;
+  if (e != ncclSuccess) return nccl_fail(e, "ncclGroupEnd");
+  for (int i = 0; i < n; ++i) {
+    gpmdm_pf* pf = pfs[i];
+    HIPCHK(hipSetDevice(pf->m->device));
+    TRY(states ? gather_copy_down(pf, pf->xs_recv, pf->xs_stage, pf->m->d + 1)
+               : gather_copy_down(pf, pf->xl_recv, pf->xl_stage, 1));
+  }
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_propagate_multi(gpmdm_pf_t* pfs, int n, const double* zh, const double* normals,
+                             void* const* streams) {
+  CHECK(pfs && zh && streams && n >= 1, "null argument");
+  RCCL_OR_FAIL();
+  for (int i = 0; i < n; ++i) {
+    gpmdm_pf* pf = pfs[i];
+    CHECK(pf, "null handle");
+    CHECK(pf->comm, "gpmdm_pf_propagate_multi needs every filter's communicator (gpmdm_pf_set_comm)");
+    CHECK(pf->n_ranks == n && pf->rank == i, "filter i must be rank i of n");
+    if (!pf->switched || pf->preswitched) return fail(GPMDM_E_STATE, "propagate called before switch");
+    if (pf->rng_mode == GPMDM_RNG_REPLAY) CHECK(normals, "replay mode needs the dynamics normals");
+  }
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipSetDevice(pfs[i]->m->device));
+    TRY(exch_states(pfs[i], normals, (hipStream_t)streams[i]));
+  }
+  TRY(group_gather(pfs, n, true));
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipSetDevice(pfs[i]->m->device));
+    TRY(exch_ll(pfs[i], zh, (hipStream_t)streams[i]));
+  }
+  TRY(group_gather(pfs, n, false));
+  for (int i = 0; i < n; ++i) {
+    HIPCHK(hipSetDevice(pfs[i]->m->device));
+    TRY(exch_finish(pfs[i], (hipStream_t)streams[i]));
+  }
+  return GPMDM_OK;
 }
 
 int gpmdm_pf_set_comm(gpmdm_pf_t pf, void* rccl_comm, int flags) {
@@ -1653,6 +1733,16 @@ int gpmdm_comm_init(int n_ranks, int rank, const void* id, int device, void** co
   const ncclResult_t e = rccl().CommInitRank(&c, n_ranks, u, rank);
   if (e != ncclSuccess) return nccl_fail(e, "ncclCommInitRank");
   *comm = c;
+  return GPMDM_OK;
+}
+
+int gpmdm_comm_init_all(int n, const int* devices, void** comms) {
+  CHECK(n >= 1 && devices && comms, "bad argument");
+  RCCL_OR_FAIL();
+  std::vector<ncclComm_t> c((size_t)n, nullptr);
+  const ncclResult_t e = rccl().CommInitAll(c.data(), n, devices);
+  if (e != ncclSuccess) return nccl_fail(e, "ncclCommInitAll");
+  for (int i = 0; i < n; ++i) comms[i] = c[(size_t)i];
   return GPMDM_OK;
 }
 

@@ -148,6 +148,8 @@ class GPMDM(torch.nn.Module):
         self.sigma_n_num_X = float(sigma_n_num_X)
         self.class_aware_observations_list = [[] for _ in range(self.n_classes)]
         self._handle = None
+        self._extra_devices = set()  # further GPUs holding the device model (handle_on)
+        self._extra_handles = {}
         self._uploaded = None       # parameter versions the device model was built from
         # where _precompute_kernel_inverses runs: None = torch on the CPU for N <= 4096 (the
         # reference's own arithmetic), the library's device factor (gpmdm_gp_factor:
@@ -458,11 +460,38 @@ class GPMDM(torch.nn.Module):
                    "gpmdm_model_create")
         self._handle = handle
         self.generation += 1
+        # the same image on the other devices a multi-device filter asked for (handle_on)
+        for dev in sorted(self._extra_devices):
+            h = ctypes.c_void_p()
+            _lib.check(lib.gpmdm_model_create(ctypes.byref(desc), int(dev), ctypes.byref(h)), "gpmdm_model_create")
+            self._extra_handles[dev] = h
+
+    def handle_on(self, device_index: int):
+        """The device model on GPU ``device_index`` (GPMDM_PF(devices=[...]): one image per
+        device, all built from the same host factors).  The first request for a device other
+        than ``self.device`` re-uploads the model to every requested device (filters rebind)."""
+        dev = int(device_index)
+        if dev == self.device.index:
+            return self.handle
+        h = self.handle and self._extra_handles.get(dev)
+        if h is None:
+            self._extra_devices.add(dev)
+            try:
+                self._precompute_kernel_inverses()
+            except Exception:
+                self._extra_devices.discard(dev)
+                raise
+            h = self._extra_handles[dev]
+        return h
 
     def _release(self):
         if getattr(self, "_handle", None) is not None and self._handle.value:
             _lib.load().gpmdm_model_destroy(self._handle)
         self._handle = None
+        for h in getattr(self, "_extra_handles", {}).values():
+            if h is not None and h.value:
+                _lib.load().gpmdm_model_destroy(h)
+        self._extra_handles = {}
 
     def __del__(self):
         try:

@@ -16,6 +16,13 @@ every per-frame computation runs in the HIP library.  Extra keyword options:
   same replicated filter whatever its local torch RNG state; replay mode (``rng='torch'``)
   consumes the host generator on every rank and therefore requires identical torch RNG
   states on all ranks (checked at construction: ``ValueError`` otherwise);
+* ``devices=[d0, d1, ...]``: one process drives one rank per GPU (SURVEY §5's config row;
+  a notebook uses several GPUs without torchrun): a library handle per device on the
+  model's image there (``GPMDM.handle_on``), communicators made together
+  (``gpmdm_comm_init_all``), and per frame every rank's stages with their all-gathers grouped
+  (``gpmdm_pf_propagate_multi``); rank r owns ``device_shard_plan``'s particle range.  The
+  read-outs and exports come from rank 0 (the filter is replicated).  ``devices=[0]`` is the
+  plain filter bit for bit;
 * ``shard=(world, rank)``: sharding with a caller-driven exchange (``exchange=`` or the
   staged calls); a Philox filter then needs an explicit ``seed`` (nothing to broadcast).
   ``exchange(recv, send)`` is called twice per frame: with the (P x (d+1)) / (P_r x (d+1))
@@ -57,6 +64,21 @@ from .model import GPMDM
 PARALLEL_REPLAY_P = 16384
 
 
+def device_shard_plan(P: int, devices) -> list:
+    """(device, rank, lo, hi) of a one-process multi-device filter (GPMDM_PF(devices=...)):
+    rank r runs on devices[r] and owns particles [r P / R, (r + 1) P / R) -- the library's
+    own shard rule (gpmdm_pf_create), so the filter is bitwise the one-rank filter's."""
+    devs = [int(x) for x in devices]
+    if not devs:
+        raise ValueError("devices must name at least one GPU")
+    if len(set(devs)) != len(devs):
+        raise ValueError(f"devices must be distinct (one rank per GPU; RCCL refuses two on one device): {devs}")
+    if any(x < 0 for x in devs):
+        raise ValueError(f"bad device index in {devs}")
+    R = len(devs)
+    return [(dev, r, P * r // R, P * (r + 1) // R) for r, dev in enumerate(devs)]
+
+
 def _as_f64_vector(z) -> np.ndarray:
     """The observation as a contiguous float64 vector (the reference casts it with
     torch.tensor(z, dtype=float64), gpmdm_pf.py:123; float32 -> float64 is exact)."""
@@ -69,7 +91,7 @@ class GPMDM_PF:
     def __init__(self, gpmdm: GPMDM, markov_switching_model, num_particles: int, *,
                  rng: str = "torch", seed=None, resample: str = "multinomial", process_group=None,
                  shard=None, exchange=None, dedup: bool = True, shard_order: bool = True,
-                 dyn_tiles: str = "auto"):
+                 dyn_tiles: str = "auto", devices=None):
         self._gpmdm = gpmdm
         self._gpmdm.set_evaluation_mode()
         self._markov_switching_model = torch.as_tensor(markov_switching_model).type(self.dtype)
@@ -85,7 +107,13 @@ class GPMDM_PF:
         self._resample_mode = resample
         self._group = process_group
         self._exchange_fn = exchange
-        if process_group is not None:
+        self._devices = None
+        if devices is not None:                 # one process, one handle per device (device_shard_plan)
+            if process_group is not None or shard is not None or exchange is not None:
+                raise ValueError("devices= drives every rank itself: no process_group, shard or exchange")
+            self._devices = [p[0] for p in device_shard_plan(self._num_particles, devices)]
+            self._world, self._rank = len(self._devices), 0
+        elif process_group is not None:
             import torch.distributed as dist
             self._world, self._rank = dist.get_world_size(process_group), dist.get_rank(process_group)
         elif shard is not None:                 # (world, rank) with a caller-driven exchange
@@ -108,28 +136,47 @@ class GPMDM_PF:
         self._seed = int(seed)
         lib = _lib.load()
         T = np.ascontiguousarray(self._markov_switching_model.numpy(), dtype=np.float64)
-        h = ctypes.c_void_p()
-        _lib.check(lib.gpmdm_pf_create(
-            gpmdm.handle, _lib.dptr(T), self._num_particles,
-            _lib.GPMDM_RNG_REPLAY if rng == "torch" else _lib.GPMDM_RNG_PHILOX,
-            ctypes.c_uint64(self._seed & (2 ** 64 - 1)),
-            _lib.GPMDM_RESAMPLE_MULTINOMIAL if resample == "multinomial" else _lib.GPMDM_RESAMPLE_SYSTEMATIC,
-            self._world, self._rank, ctypes.byref(h)), "GPMDM_PF")
-        self._h = h
-        self._model_gen = gpmdm.generation
-        _lib.check(lib.gpmdm_pf_set_dedup(h, 1 if dedup else 0), "dedup")
-        _lib.check(lib.gpmdm_pf_set_shard_order(h, 1 if shard_order else 0), "shard_order")
         if dyn_tiles not in _lib.DYN_TILES:
             raise ValueError("dyn_tiles must be 'auto', 'narrow' or 'wide'")
-        _lib.check(lib.gpmdm_pf_set_dyn_tiles(h, _lib.DYN_TILES[dyn_tiles]), "dyn_tiles")
+
+        def create(model_handle, rank):
+            h = ctypes.c_void_p()
+            _lib.check(lib.gpmdm_pf_create(
+                model_handle, _lib.dptr(T), self._num_particles,
+                _lib.GPMDM_RNG_REPLAY if rng == "torch" else _lib.GPMDM_RNG_PHILOX,
+                ctypes.c_uint64(self._seed & (2 ** 64 - 1)),
+                _lib.GPMDM_RESAMPLE_MULTINOMIAL if resample == "multinomial" else _lib.GPMDM_RESAMPLE_SYSTEMATIC,
+                self._world, rank, ctypes.byref(h)), "GPMDM_PF")
+            _lib.check(lib.gpmdm_pf_set_dedup(h, 1 if dedup else 0), "dedup")
+            _lib.check(lib.gpmdm_pf_set_shard_order(h, 1 if shard_order else 0), "shard_order")
+            _lib.check(lib.gpmdm_pf_set_dyn_tiles(h, _lib.DYN_TILES[dyn_tiles]), "dyn_tiles")
+            return h
+
+        self._peers = []                        # devices=: ranks 1.. as (handle, device index)
+        self._comms = []
+        if self._devices is None:
+            self._h = create(gpmdm.handle, self._rank)
+            self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        else:
+            hs = [create(gpmdm.handle_on(dev), r) for r, dev in enumerate(self._devices)]
+            self._h, self._dev_index = hs[0], self._devices[0]
+            self._peers = list(zip(hs[1:], self._devices[1:]))
+            # one communicator per device, made together (ncclCommInitAll); rank r on devices[r]
+            n = len(self._devices)
+            comms = (ctypes.c_void_p * n)()
+            _lib.check(lib.gpmdm_comm_init_all(n, (ctypes.c_int * n)(*self._devices), comms), "gpmdm_comm_init_all")
+            self._comms = [ctypes.c_void_p(c) for c in comms]
+            for h, c in zip(hs, self._comms):
+                _lib.check(lib.gpmdm_pf_set_comm(h, c, 0), "set_comm")
+        self._model_gen = gpmdm.generation
         self._readout = None
-        self._comm = None
-        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self._comm = self._comms[0] if self._comms else None
         # read-out landing buffers and their pointers, made once (read per frame)
         C, d = self.num_classes, self.latent_dim
         self._ro = (np.zeros(C), np.zeros(d), np.zeros(1))
         self._ro_ptr = tuple(_lib.dptr(a) for a in self._ro)
-        if self._world > 1:
+        if self._world > 1 and self._devices is None:
+            h = self._h
             w, lo, hi = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
             lib.gpmdm_pf_exchange_width(h, ctypes.byref(w), ctypes.byref(lo), ctypes.byref(hi))
             dev = self.device
@@ -148,9 +195,15 @@ class GPMDM_PF:
             dr = getattr(self, "_draws", None)
             if dr is not None and hasattr(dr, "close"):
                 dr.close()                      # draws ahead write into the handle's buffers: join them
+            for h, _ in getattr(self, "_peers", []):
+                _lib.load().gpmdm_pf_destroy(h)
+            self._peers = []
             if getattr(self, "_h", None) is not None and self._h.value:
                 _lib.load().gpmdm_pf_destroy(self._h)
                 self._h = None
+            for c in getattr(self, "_comms", []):   # after the filters using them
+                _lib.load().gpmdm_comm_destroy(c)
+            self._comms = []
         except Exception:
             pass
 
@@ -166,8 +219,26 @@ class GPMDM_PF:
         a reload into the same object) rebind the device filter to the new image."""
         self._gpmdm._refresh()                  # parameters changed in place (an optimiser step)?
         if self._gpmdm.generation != self._model_gen:
-            _lib.check(_lib.load().gpmdm_pf_set_model(self._h, self._gpmdm.handle), "rebind to the rebuilt model")
+            lib = _lib.load()
+            if self._devices is None:
+                _lib.check(lib.gpmdm_pf_set_model(self._h, self._gpmdm.handle), "rebind to the rebuilt model")
+            else:
+                for h, dev in [(self._h, self._devices[0])] + self._peers:
+                    _lib.check(lib.gpmdm_pf_set_model(h, self._gpmdm.handle_on(dev)), "rebind to the rebuilt model")
             self._model_gen = self._gpmdm.generation
+
+    def _all(self):
+        """(handle, raw stream) of every rank this process drives (devices=: all of them)."""
+        out = [(self._h, self._stream())]
+        for h, dev in self._peers:
+            out.append((h, ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(dev))))
+        return out
+
+    def _each(self, fn_name, *args, what=""):
+        """The same library call (handle, *args, stream) on every rank this process drives."""
+        lib = _lib.load()
+        for h, s in self._all():
+            _lib.check(getattr(lib, fn_name)(h, *args, s), what or fn_name)
 
     def _divide_into_n_parts(self, x: int, n: int) -> list:
         """gpmdm_pf.py:287-292."""
@@ -188,7 +259,8 @@ class GPMDM_PF:
             states = np.ascontiguousarray(broadcast_array(states, self._group, self.device))
             classes = np.ascontiguousarray(broadcast_array(classes, self._group, self.device))
         self._sync_model()
-        _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "init")
+        for h in [self._h] + [p[0] for p in self._peers]:
+            _lib.check(_lib.load().gpmdm_pf_init(h, _lib.dptr(states), _lib.i64ptr(classes)), "init")
         self._readout = None
 
     def reset(self):
@@ -227,14 +299,16 @@ class GPMDM_PF:
             pE, pC, pN, pU = self._draw_ptr
             dr.switch()
             _lib.check(lib.gpmdm_pf_switch(h, pE, pC, s), "switch")
+            for hp, sp in self._all()[1:]:      # devices=: every rank switches all P (replay)
+                _lib.check(lib.gpmdm_pf_switch(hp, pE, None, sp), "switch")
             dr.dynamics(counts)
             self._propagate(z, dr.N, s, pN)
             dr.resample()
-            _lib.check(lib.gpmdm_pf_resample(h, pU, s), "resample")
+            self._each("gpmdm_pf_resample", pU, what="resample")
         else:
-            _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
+            self._each("gpmdm_pf_switch", None, None, what="switch")
             self._propagate(z, None, s)
-            _lib.check(lib.gpmdm_pf_resample(h, None, s), "resample")
+            self._each("gpmdm_pf_resample", None, what="resample")
         self._readout = None
 
     step = update    # north-star name (BASELINE.json): one filter step
@@ -250,11 +324,11 @@ class GPMDM_PF:
         lib, h, s = _lib.load(), self._h, self._stream()
         P, C, d = self._num_particles, self.num_classes, self.latent_dim
         E = np.ascontiguousarray(exp_draws, dtype=np.float64).reshape(P, C)
-        _lib.check(lib.gpmdm_pf_switch(h, _lib.dptr(E), None, s), "switch")
+        self._each("gpmdm_pf_switch", _lib.dptr(E), None, what="switch")
         nrm = np.ascontiguousarray(normals, dtype=np.float64).reshape(P, d)
         self._propagate(z, nrm, s)
         U = np.ascontiguousarray(uniforms, dtype=np.float64).reshape(-1)
-        _lib.check(lib.gpmdm_pf_resample(h, _lib.dptr(U), s), "resample")
+        self._each("gpmdm_pf_resample", _lib.dptr(U), what="resample")
         self._readout = None
 
     def set_comm(self, comm, pad_rows: bool = False):
@@ -263,6 +337,8 @@ class GPMDM_PF:
         this filter's (world, rank), on the model's device; ``None`` detaches).
         ``pad_rows`` forces the uneven-shard gather path (tests).  The communicator must
         outlive the filter's use of it."""
+        if self._devices is not None:
+            raise ValueError("a devices= filter holds its own communicators")
         ptr = getattr(comm, "ptr", comm)
         _lib.check(_lib.load().gpmdm_pf_set_comm(self._h, ctypes.c_void_p(ptr) if ptr else None,
                                                  _lib.GPMDM_COMM_PAD_ROWS if pad_rows else 0), "set_comm")
@@ -275,6 +351,13 @@ class GPMDM_PF:
         its communicator (set_comm), or here over the process group / exchange callback."""
         lib, h = _lib.load(), self._h
         nrm = normals_ptr if normals_ptr is not None else (None if normals is None else _lib.dptr(normals))
+        if self._devices is not None:
+            # one thread drives every rank: the library stages them and groups the collectives
+            hs = self._all()
+            n = len(hs)
+            _lib.check(lib.gpmdm_pf_propagate_multi((ctypes.c_void_p * n)(*[x[0] for x in hs]), n, _lib.dptr(z), nrm,
+                                                    (ctypes.c_void_p * n)(*[x[1] for x in hs])), "propagate")
+            return
         if self._world == 1 or self._comm is not None:
             _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), nrm, s), "propagate")
             return
@@ -359,7 +442,10 @@ class GPMDM_PF:
         log-likelihoods / states.  The arithmetic is the reference's (NaN propagates);
         these counts say when it happened."""
         n = np.zeros(len(_lib.HEALTH), dtype=np.int64)
-        _lib.check(_lib.load().gpmdm_pf_health(self._h, _lib.i64ptr(n), 1 if reset else 0, self._stream()), "health")
+        for h, s in self._all():                # devices=: each rank counts its own slice's events
+            m = np.zeros(len(_lib.HEALTH), dtype=np.int64)
+            _lib.check(_lib.load().gpmdm_pf_health(h, _lib.i64ptr(m), 1 if reset else 0, s), "health")
+            n += m
         return {k: int(v) for k, v in zip(_lib.HEALTH, n)}
 
     # ---- introspection (tests, checkpoint of the filter state) --------------------
@@ -390,15 +476,17 @@ class GPMDM_PF:
         classes = np.ascontiguousarray(classes, dtype=np.int64).reshape(P)
         full = (ll, log_w, w)
         if all(x is None for x in full) and resample_idx is None and frame is None:
-            _lib.check(_lib.load().gpmdm_pf_init(self._h, _lib.dptr(states), _lib.i64ptr(classes)), "load_state")
+            for h in [self._h] + [p[0] for p in self._peers]:
+                _lib.check(_lib.load().gpmdm_pf_init(h, _lib.dptr(states), _lib.i64ptr(classes)), "load_state")
         else:
             if any(x is None for x in full):
                 raise ValueError("a full state import needs ll, log_w and w together")
             ll, log_w, w = (np.ascontiguousarray(x, dtype=np.float64).reshape(P) for x in full)
             ridx = None if resample_idx is None else np.ascontiguousarray(resample_idx, dtype=np.int64).reshape(P)
-            _lib.check(_lib.load().gpmdm_pf_import(
-                self._h, _lib.dptr(states), _lib.i64ptr(classes), _lib.dptr(ll), _lib.dptr(log_w), _lib.dptr(w),
-                _lib.i64ptr(ridx), -1 if frame is None else int(frame)), "load_state")
+            for h in [self._h] + [p[0] for p in self._peers]:
+                _lib.check(_lib.load().gpmdm_pf_import(
+                    h, _lib.dptr(states), _lib.i64ptr(classes), _lib.dptr(ll), _lib.dptr(log_w), _lib.dptr(w),
+                    _lib.i64ptr(ridx), -1 if frame is None else int(frame)), "load_state")
         self._readout = None
 
     def import_state(self, st: dict):

@@ -219,6 +219,18 @@ int gpmdm_comm_unique_id(void* id);
 int gpmdm_comm_init(int n_ranks, int rank, const void* id, int device, void** comm);
 int gpmdm_comm_destroy(void* comm);
 
+/* One process driving several devices (GPMDM_PF(devices=[...])): gpmdm_comm_init_all makes
+ * the n communicators of devices[0..n-1] at once (ncclCommInitAll), comms[i] for rank i.
+ * gpmdm_pf_propagate_multi is gpmdm_pf_propagate for the n filters pfs[i] (rank i of n,
+ * each with comms[i] set by gpmdm_pf_set_comm, each switched) on streams[i]: every stage
+ * runs for every rank and each stage's all-gathers are grouped (ncclGroupStart/End), as a
+ * single thread that drives several ranks must.  z and the replay normals are the same
+ * host arrays for every rank (the filter is replicated).  RCCL is resolved at run time
+ * (librccl.so.1) by these and the calls above; GPMDM_E_HIP when it is missing. */
+int gpmdm_comm_init_all(int n, const int* devices, void** comms);
+int gpmdm_pf_propagate_multi(gpmdm_pf_t* pfs, int n, const double* z, const double* normals,
+                             void* const* streams);
+
 /* _update_weights' normalisation + _resample + the read-outs  (gpmdm_pf.py:194-262,
  * 302-312).  uniforms: P host (replay, multinomial), 1 host (replay, systematic) or NULL.
  * Philox filters then launch the next frame's switch on the same stream (see

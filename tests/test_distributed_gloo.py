@@ -121,3 +121,19 @@ def test_gather_plan():
     assert gather_plan(10, 3)[0] == [3, 3, 4]
     with pytest.raises(ValueError):
         gather_plan(7, 2, pad_rows=3)
+
+
+def test_device_shard_plan():
+    """GPMDM_PF(devices=[...]): rank r on devices[r] owns the library's shard of particles."""
+    from gpmdm_amd.pf import device_shard_plan
+    from gpmdm_amd.distributed import shard_range
+    for P in (1, 7, 100_000, 1_000_001):
+        for devs in ([0], [0, 1], [3, 1, 2], list(range(8))):
+            plan = device_shard_plan(P, devs)
+            assert [p[0] for p in plan] == devs and [p[1] for p in plan] == list(range(len(devs)))
+            assert plan[0][2] == 0 and plan[-1][3] == P
+            assert all(plan[k][3] == plan[k + 1][2] for k in range(len(devs) - 1))
+            assert all((p[2], p[3]) == shard_range(P, len(devs), p[1]) for p in plan)
+    for bad in ([], [0, 0], [1, -1]):
+        with pytest.raises(ValueError):
+            device_shard_plan(10, bad)

@@ -1,0 +1,63 @@
+"""GPU: a one-process multi-device filter (GPMDM_PF(devices=[...])): one library
+handle per device, communicators from gpmdm_comm_init_all, every frame's stages driven for
+every rank with the all-gathers grouped (gpmdm_pf_propagate_multi).  On a one-GPU box the
+one-device case runs: it must be bit for bit the plain filter (Philox and replay draws,
+multinomial and systematic), with read-outs, exports, predict and a checkpoint import."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_fixture, product_model
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def model():
+    f = load_fixture("config2_n2000_p1000")
+    m = product_model(f)
+    return m, torch.tensor(np.asarray(f["T"], dtype=np.float64)), m.get_Y()
+
+
+@pytest.mark.parametrize("rng,resample,P", [("philox", "multinomial", 5000), ("philox", "systematic", 777),
+                                            ("torch", "multinomial", 3000), ("torch", "multinomial", 20000)])
+def test_one_device_is_the_plain_filter(model, rng, resample, P):
+    from gpmdm_amd import GPMDM_PF
+    m, T, Y = model
+    seed = 5 if rng == "philox" else None
+    out = []
+    for devices in (None, [0]):
+        torch.manual_seed(8)
+        pf = GPMDM_PF(m, T, P, rng=rng, seed=seed, resample=resample, devices=devices)
+        res = []
+        for k in range(4):
+            pf.update(np.asarray(Y[20 + 9 * k], dtype=np.float64) + 0.01)
+            res.append((pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), pf.log_likelihood()))
+        st = pf.export_state()
+        res.append(pf.predict().numpy())
+        res.append(pf.health())
+        pf.import_state(st)
+        pf.update(np.asarray(Y[70], dtype=np.float64))
+        res.append(pf.export_state())
+        out.append((res, st, torch.get_rng_state()))
+    (a, sa, ga), (b, sb, gb) = out
+    for k in range(4):
+        assert np.array_equal(a[k][0], b[k][0]) and np.array_equal(a[k][1], b[k][1]) and a[k][2] == b[k][2], k
+    for key in ("states", "classes", "ll", "w", "resample_idx"):
+        assert np.array_equal(sa[key], sb[key]), key
+        assert np.array_equal(a[-1][key], b[-1][key]), key
+    assert np.array_equal(a[4], b[4]) and a[5] == b[5]
+    assert torch.equal(ga, gb)
+
+
+def test_devices_validation(model):
+    from gpmdm_amd import GPMDM_PF
+    m, T, _ = model
+    with pytest.raises(ValueError):
+        GPMDM_PF(m, T, 100, devices=[0, 0])
+    with pytest.raises(ValueError):
+        GPMDM_PF(m, T, 100, devices=[0], shard=(1, 0))
+    n = torch.cuda.device_count()
+    if n < 2:
+        with pytest.raises((RuntimeError, ValueError)):
+            GPMDM_PF(m, T, 100, rng="philox", seed=1, devices=[0, n])   # no such device
