@@ -282,7 +282,7 @@ def predictive_stream(pf, model, frames, seed=5):
 SPREAD_LAMBDA = 0.05   # observation-GP output scale of the spread-cloud line (see spread_line)
 
 
-def spread_line(device, steps, warmup=5, y_lambda=SPREAD_LAMBDA):
+def spread_line(device, steps, warmup=5, y_lambda=SPREAD_LAMBDA, dyn_tiles="auto"):
     """The headline step on a cloud that stays spread out: the same configuration with the
     observation GP's output scales exp(y_log_lambdas) = y_lambda (a less peaked likelihood)
     and the predictive observation stream (predictive_stream), so resampling keeps many
@@ -302,7 +302,7 @@ def spread_line(device, steps, warmup=5, y_lambda=SPREAD_LAMBDA):
 
     def new_filter():
         torch.manual_seed(11)
-        return GPMDM_PF(model, T, P, rng="philox", seed=11)
+        return GPMDM_PF(model, T, P, rng="philox", seed=11, dyn_tiles=dyn_tiles)
 
     zs, check = predictive_stream(new_filter(), model, warmup + steps)
     pf = new_filter()
@@ -340,14 +340,14 @@ def spread_line(device, steps, warmup=5, y_lambda=SPREAD_LAMBDA):
                     "(ms_per_step includes them)"}
 
 
-def nodedup_line(model, T, P_total, group, dist, device, zs, steps, rng):
+def nodedup_line(model, T, P_total, group, dist, device, zs, steps, rng, dyn_tiles="auto"):
     """The same step with ancestor de-duplication off (every particle's dynamics GP)."""
     import torch
     from gpmdm_amd import GPMDM_PF
     n_nd = min(steps, 20)
     torch.manual_seed(11)
     pf_nd = GPMDM_PF(model, T, P_total, rng=rng, seed=11 if rng == "philox" else None, process_group=group,
-                     dedup=False)
+                     dedup=False, dyn_tiles=dyn_tiles)
     for k in range(3):
         pf_nd.update(zs[k])
     torch.cuda.synchronize()
@@ -837,7 +837,8 @@ def main():
     w_last = pf.export_state()["w"]
     ess = float(1.0 / np.sum(w_last * w_last))
     bank = bank_line(model, T, args.bank, P_total, zs, args.warmup, args.steps) if args.bank and world == 1 else None
-    nodedup = None if args.no_nodedup else nodedup_line(model, T, P_total, group, dist, device, zs, args.steps, rng)
+    nodedup = None if args.no_nodedup else nodedup_line(model, T, P_total, group, dist, device, zs, args.steps, rng,
+                                                                args.dyn_tiles)
     rep = None
     if args.replay_steps is None:
         args.replay_steps = 30 if (args.config == 2 and rng == "philox" and args.stream == "mocap") else 0
@@ -850,7 +851,7 @@ def main():
         libx = library_exchange_line(new_filter, zs, min(args.steps, args.library_steps), dist, device, P_total)
     if args.spread_steps is None:
         args.spread_steps = 30 if (args.config == 2 and args.stream == "mocap" and args.y_lambda == 1.0) else 0
-    spread = spread_line(device, args.spread_steps) if args.spread_steps and world == 1 else None
+    spread = spread_line(device, args.spread_steps, dyn_tiles=args.dyn_tiles) if args.spread_steps and world == 1 else None
     N, D, d = model.X.shape[0], model.D, model.d
     P_local = P_total // world
     alg, dense, executed = obs_kernel_flops(N, D)

@@ -404,6 +404,15 @@ struct gpmdm_pf {
   hipEvent_t ro_ev = nullptr;         // after the last read-out (gpmdm_pf_read waits on it)
   bool ro_ev_ok = false;
   int* rows_last() const { return small + 504; }   // rows of the last dynamics pass
+  // Tile height of the dynamics pass on the 16 x 256 image: 16, 32 or 64 particle rows per
+  // workgroup give bitwise the same results (same column blocks, same per-row association),
+  // so the height is a pure schedule choice: short grids of few rows want 16-row tiles, long
+  // grids 64-row ones (a B fragment feeds 4 row groups).  Chosen per frame from the row count
+  // of the dynamics pass the last gpmdm_pf_read saw (k_dyn_finish writes it to rows_pin).
+  int* rows_pin = nullptr;
+  int* rows_pdev = nullptr;
+  int rows_hint = 0;
+  TileGeo dyn_geo_frame{};            // this frame's dynamics launch shape (set by the switch)
   // timing
   bool timing = false;
   std::vector<hipEvent_t> pool;
@@ -446,6 +455,7 @@ struct gpmdm_pf {
     for (auto ev : pool) (void)hipEventDestroy(ev);
     if (rpin) (void)hipHostFree(rpin);
     if (cnt_pin) (void)hipHostFree(cnt_pin);
+    if (rows_pin) (void)hipHostFree(rows_pin);
     if (cls_pin) (void)hipHostFree(cls_pin);
     if (cls_ev) (void)hipEventDestroy(cls_ev);
     if (cnt_ev) (void)hipEventDestroy(cnt_ev);
@@ -834,6 +844,16 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
     }
     pf->ro_dev = (double*)rv;
   }
+  {
+    void* rv = nullptr;
+    if (hipHostMalloc((void**)&pf->rows_pin, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(&rv, pf->rows_pin, 0) != hipSuccess) {
+      delete pf;
+      return fail(GPMDM_E_NOMEM, "mapped row-count buffer");
+    }
+    pf->rows_pdev = (int*)rv;
+    *pf->rows_pin = 0;
+  }
   if (rng_mode == GPMDM_RNG_REPLAY) {
     const long long n[3] = {P * C, P * d, P};      // E, normals, U
     // mapped, coherent (fine-grained): kernels may read the small draws in place
@@ -1135,6 +1155,23 @@ int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes,
 
 static void launch_dyn_gemm(gpmdm_pf* pf, hipStream_t s);
 
+// Rows from which the de-duplicated dynamics pass runs 32- / 64-row tiles of the 16 x 256
+// image (per rank, the last read frame's count; tools/dyn_family.sh).  GPMDM_DYN_MT=1|2|4
+// forces a height (A/B).
+constexpr int kDynMt2Rows = 1 << 30, kDynMt4Rows = 1 << 30;
+
+static TileGeo dyn_frame_geo(const gpmdm_pf* pf) {
+  const TileGeo g = pf->m->dyn_set(pf->wide_dyn())[0].geo;
+  if (g.nw != kGeo16x256.nw || g.mt != kGeo16x256.mt || g.ntw != kGeo16x256.ntw) return g;
+  static const char* env = std::getenv("GPMDM_DYN_MT");
+  int mt = 1;
+  if (env && (env[0] == '1' || env[0] == '2' || env[0] == '4'))
+    mt = env[0] - '0';
+  else
+    mt = pf->rows_hint >= kDynMt4Rows ? 4 : (pf->rows_hint >= kDynMt2Rows ? 2 : 1);
+  return TileGeo{g.nw, mt, g.ntw};
+}
+
 static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipStream_t s) {
   gpmdm_model* m = pf->m;
   const int C = m->C;
@@ -1174,10 +1211,11 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
     sa.hi = pf->hi;
   }
   sa.own = pf->own_order();
+  pf->dyn_geo_frame = dyn_frame_geo(pf);
   ScanArgs sc{};
   sc.nb = nbs;
   sc.C = C;
-  sc.pt = m->dyn_set(pf->wide_dyn())[0].geo.pt();   // tile unit of the dynamics pass
+  sc.pt = pf->dyn_geo_frame.pt();      // tile unit of the dynamics pass
   sc.lo = sl ? 0 : pf->lo;
   sc.hi = sl ? pf->nloc : pf->hi;
   sc.own = pf->own_order();
@@ -1210,7 +1248,7 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
     la.npos = nsw;
     la.nb = nbs;
     la.C = C;
-    la.pt = m->dyn_set(pf->wide_dyn())[0].geo.pt();
+    la.pt = pf->dyn_geo_frame.pt();
     la.perm = pf->perm;
     la.cls_new = pf->cls_new;
     la.anc = pf->ridx;
@@ -1333,7 +1371,7 @@ static void launch_dyn_gemm(gpmdm_pf* pf, hipStream_t s) {
       njm = std::max(njm, dset[c0 + k].n_j);
     }
     tp.n_seg = ns;
-    tp.geo = dset[c0].geo;           // tile starts computed on the device in units of pt
+    tp.geo = pf->dyn_geo_frame;      // tile starts computed on the device in units of pt
     tp.tiles_ub = (int)(cdiv(nl, tp.geo.pt()) + ns);
     if (exact_grid && pf->dedup) tp.tiles_ub = std::max(ltiles[c0 + ns] - ltiles[c0], 1);
     tp.n_j_max = njm;
@@ -1412,6 +1450,7 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
     fa.rows_e = pf->dedup ? pf->lseg_end() : pf->seg_end();
     fa.n_rows_seg = C;
     fa.rows_out = pf->rows_last();
+    fa.rows_host = pf->rows_pdev;
     if (zstage) {
       fa.z_src = pf->zdev[pf->zslot];
       fa.z_dst = pf->z;
@@ -1909,6 +1948,7 @@ int gpmdm_pf_read(gpmdm_pf_t pf, double* post, double* mean, double* lik, void* 
   } else {
     HIPCHK(hipStreamSynchronize(s));
   }
+  pf->rows_hint = *(volatile int*)pf->rows_pin;   // its dynamics pass has run (the read-out follows it)
   for (int f = 0; f < pf->F; ++f) {
     const double* b = src + (size_t)f * nr;
     if (post) std::memcpy(post + (size_t)f * m->C, b, sizeof(double) * m->C);

@@ -139,6 +139,8 @@ struct DynFinishArgs {
   const int* rows_e;
   int n_rows_seg;
   int* rows_out;                  // or nullptr
+  int* rows_host;                 // the same count into mapped host memory (the next frames'
+                                  // tile-height choice, capi.hip dyn_frame_geo), or nullptr
   // the frame's observation copied by outputs < z_n from host-mapped memory to the device
   // buffer the observation GP reads (no copy launch on the critical path), or z_n = 0
   const double* z_src;

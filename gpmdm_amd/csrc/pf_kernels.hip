@@ -544,6 +544,7 @@ __global__ __launch_bounds__(kB) void k_dyn_finish(DynFinishArgs a) {
     int r = 0;
     for (int c = 0; c < a.n_rows_seg; ++c) r += a.rows_e[c] - a.rows_b[c];
     a.rows_out[0] = r;
+    if (a.rows_host) a.rows_host[0] = r;
   }
   if (o >= a.n_out) return;
   const int c = a.seg_out_base ? seg_of(a.seg_out_base, a.n_seg, (int)a.n_out, (int)o) : 0;
