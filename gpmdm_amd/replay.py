@@ -223,7 +223,13 @@ class ParallelFrameDraws:
         return self.P * self.C + self.P * self.d + 16 * self.C + self.nu
 
     def _run(self, tasks):
-        list(self._pool.map(lambda f: f(), tasks))
+        """Run the chunks: all but the first on the pool, the first on this thread."""
+        if not tasks:
+            return
+        futs = [self._pool.submit(f) for f in tasks[1:]]
+        tasks[0]()
+        for f in futs:
+            f.result()
 
     @staticmethod
     def _gen(state: torch.Tensor) -> torch.Generator:
