@@ -27,6 +27,10 @@ namespace gpmdm {
 thread_local std::string g_err;
 int fail(int code, const std::string& msg) {
   g_err = msg;
+  // a failed HIP call stays this thread's "last error" until read: reported here, it must
+  // not surface again in a later call's launch check (a refused hipSetDevice of a missing
+  // device, say, in front of an unrelated filter's first hipGetLastError)
+  if (code == GPMDM_E_HIP || code == GPMDM_E_NOMEM) (void)hipGetLastError();
   return code;
 }
 }  // namespace gpmdm

@@ -61,3 +61,8 @@ def test_devices_validation(model):
     if n < 2:
         with pytest.raises((RuntimeError, ValueError)):
             GPMDM_PF(m, T, 100, rng="philox", seed=1, devices=[0, n])   # no such device
+        # the refused device's HIP error was reported once: it must not surface in the next
+        # call's launch checks (it did, in the device precompute of the next test module)
+        pf = GPMDM_PF(m, T, 300, rng="philox", seed=1)
+        pf.update(np.asarray(m.get_Y()[5], dtype=np.float64))
+        assert np.isfinite(pf.class_probabilities().numpy()).all()
