@@ -67,6 +67,19 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     return lib
 
 
+def _deps(path: Path, seen=None) -> set:
+    """The file and every local header it includes (#include "..."), transitively."""
+    seen = set() if seen is None else seen
+    if path in seen or not path.exists():
+        return seen
+    seen.add(path)
+    for line in path.read_text(errors="replace").splitlines():
+        s = line.strip()
+        if s.startswith("#include \""):
+            _deps((path.parent / s.split('"')[1]).resolve(), seen)
+    return seen
+
+
 def _build_lib(force: bool = False, verbose: bool = False) -> Path:
     newest_hdr = max(h.stat().st_mtime for h in HEADERS)
     newest_src = max((CSRC / src).stat().st_mtime for src in SOURCES)
@@ -78,7 +91,8 @@ def _build_lib(force: bool = False, verbose: bool = False) -> Path:
     for src in SOURCES:
         s = CSRC / src
         o = OBJ / (src + ".o")
-        if force or not o.exists() or o.stat().st_mtime < max(s.stat().st_mtime, newest_hdr):
+        newest = max(p.stat().st_mtime for p in _deps(s.resolve()))   # the source and its headers
+        if force or not o.exists() or o.stat().st_mtime < newest:
             jobs.append([cc, *_flags(), "-c", str(s), "-o", str(o)])
 
     def run(cmd):

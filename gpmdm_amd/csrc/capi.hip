@@ -287,13 +287,24 @@ struct gpmdm_pf {
   unsigned* owner = nullptr;
   int *slot = nullptr, *lflag = nullptr, *lblock = nullptr, *ltab = nullptr, *lperm = nullptr;
   // ancestor-ordered shards (multi-rank philox filters, shard_order.hip): own = particles
-  // in order of their resampling ancestor's bucket; this rank evaluates positions [lo, hi)
+  // in order of their resampling uniform's bucket; this rank evaluates positions [lo, hi)
   int* own = nullptr;
   int* own_inv = nullptr;            // own_inv[own[r]] = r
   unsigned char* own_tmp = nullptr;
   size_t own_tmp_bytes = 0;
   bool own_valid = false;
   bool shard_order = true;            // gpmdm_pf_set_shard_order
+  // Exchanged rows read in place (gpmdm_pf_unpack_part): the all-gathered {class, state} rows
+  // are read by the resample's gathers through the ownership order (only the ancestors' rows
+  // are ever touched) and the {ll} column by a launch inside the resample that also writes
+  // the normaliser's block maxima, instead of two unpack passes over every particle.  Rows
+  // are in position order (row r = particle own[r]); *_w = doubles per row.  flush_rows
+  // writes them out for a reader that needs X_prop / cls_new / ll first (export).
+  const double* rows_st = nullptr;   // column 0 = class, 1..d = state
+  int rows_st_w = 0;
+  const double* rows_ll = nullptr;   // column 0 = ll
+  int rows_ll_w = 0;
+  const int* rows_inv = nullptr;     // the ownership order the rows were gathered in (nullptr: identity)
   // observation upload through two pinned slots (a pageable hipMemcpyAsync is staged by the
   // runtime and stalls the launching thread); each slot's event guards its reuse
   double* zpin[2] = {nullptr, nullptr};
@@ -363,6 +374,7 @@ struct gpmdm_pf {
   // k_norm_max (bmax_ready: produced by this frame's weigh, not yet consumed)
   unsigned long long* bmax = nullptr;
   bool bmax_ready = false;
+  unsigned long long* bmax_rows = nullptr;   // multi-rank filters: k_rows_ll's block maxima
   // the leader election's owner table is all 0xffffffff (the last compaction restored it)
   bool owner_clean = false;
   double *e = nullptr, *local = nullptr, *blocksum = nullptr, *blockoffw = nullptr, *total = nullptr,
@@ -453,6 +465,7 @@ struct gpmdm_pf {
     dfree(own_tmp);
     dfree(gmax);
     dfree(bmax);
+    dfree(bmax_rows);
     dfree(owner);
     dfree(health);
     for (auto& r : recs) { pool.push_back(r.a); pool.push_back(r.b); }
@@ -802,6 +815,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   }
   ALLOC(gmax, F);
   if (F == 1 && n_ranks == 1) ALLOC(bmax, pf->nb);
+  if (F == 1 && n_ranks > 1) ALLOC(bmax_rows, rows_ll_blocks(P));
   ALLOC(e, P);
   ALLOC(local, P);
   ALLOC(blocksum, F * pf->nbf);
@@ -817,7 +831,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
     ALLOC(sys_block, F * pf->nbf);
   }
   if (n_ranks > 1 && rng_mode == GPMDM_RNG_PHILOX) {
-    pf->own_tmp_bytes = std::max<size_t>(ancestor_order_temp_bytes(P), 1);
+    pf->own_tmp_bytes = std::max<size_t>(uniform_order_temp_bytes(P), 1);
     ALLOC(own, P);
     ALLOC(own_inv, P);
     ALLOC(own_tmp, pf->own_tmp_bytes);
@@ -1079,6 +1093,7 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   pf->ro_ev_ok = true;
   pf->initialised = true;
   pf->own_valid = false;               // no ancestors yet: identity ownership
+  pf->rows_st = pf->rows_ll = nullptr;
   pf->switched = pf->propagated = pf->dyn_done = pf->ll_pending = pf->gemm_ahead = false;
   return GPMDM_OK;
 }
@@ -1143,12 +1158,10 @@ int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes,
   ra.X_src = pf->X;
   launch_resample(ra, nullptr);
   HIPCHK(hipGetLastError());
+  // the next frame's shards: the identity order (the exporter's uniforms are not part of the
+  // state; the ownership order changes which rank evaluates a particle, never its values)
   pf->own_valid = false;
-  if (pf->own && pf->dedup && pf->shard_order) {   // the next frame's shards, as a resample sets them
-    if (launch_ancestor_order(pf->ridx, pf->own, pf->own_inv, pf->P, pf->own_tmp, pf->own_tmp_bytes, nullptr) != 0)
-      return fail(GPMDM_E_HIP, "ancestor-order pass failed");
-    pf->own_valid = true;
-  }
+  pf->rows_st = pf->rows_ll = nullptr;
   HIPCHK(hipEventRecord(pf->ro_ev, nullptr));
   HIPCHK(hipDeviceSynchronize());
   pf->ro_ev_ok = true;
@@ -1859,13 +1872,12 @@ int gpmdm_pf_unpack_part(gpmdm_pf_t pf, const double* recv, int part, void* stre
   return unpack_part(pf, recv, part, (hipStream_t)stream);
 }
 
-static int unpack_part(gpmdm_pf* pf, const double* recv, int part, hipStream_t s) {
+static int launch_unpack_rows(gpmdm_pf* pf, const double* recv, int part, const int* inv, hipStream_t s) {
   PackArgs a{};
   a.n = pf->P;
   a.lo = 0;
   a.d = pf->m->d;
-  a.own = pf->own_order();
-  a.inv = pf->own_valid ? pf->own_inv : nullptr;
+  a.inv = inv;
   a.buf = const_cast<double*>(recv);
   a.part = part;
   a.ll = pf->ll;
@@ -1873,6 +1885,51 @@ static int unpack_part(gpmdm_pf* pf, const double* recv, int part, hipStream_t s
   a.X = pf->X_prop;
   launch_unpack(a, s);
   HIPCHK(hipGetLastError());
+  return GPMDM_OK;
+}
+
+// Exchanged rows are read in place by the next resample (gpmdm_pf.rows_*) when it runs the
+// multi-kernel path (the one-workgroup small path reads the unpacked arrays).
+// GPMDM_NO_ROWS_IN_PLACE=1 unpacks at once (A/B).
+static bool rows_in_place(gpmdm_pf* pf) {
+  static const bool off = std::getenv("GPMDM_NO_ROWS_IN_PLACE") != nullptr;
+  return !off && pf->F == 1 && !small_resample_ok(norm_args(pf), resample_args(pf));
+}
+
+static int unpack_part(gpmdm_pf* pf, const double* recv, int part, hipStream_t s) {
+  const int* inv = pf->own_valid ? pf->own_inv : nullptr;
+  if (!rows_in_place(pf)) return launch_unpack_rows(pf, recv, part, inv, s);
+  const int d = pf->m->d;
+  const int w = part == GPMDM_PACK_ALL ? d + 2 : (part == GPMDM_PACK_STATES ? d + 1 : 1);
+  if (part != GPMDM_PACK_LL) {
+    pf->rows_st = recv + (part == GPMDM_PACK_ALL ? 1 : 0);
+    pf->rows_st_w = w;
+  }
+  if (part != GPMDM_PACK_STATES) {
+    pf->rows_ll = recv;
+    pf->rows_ll_w = w;
+  }
+  pf->rows_inv = inv;
+  return GPMDM_OK;
+}
+
+// Write rows held in place out to cls_new / X_prop / ll, for a reader that comes before the
+// resample (export).
+static int flush_rows(gpmdm_pf* pf, hipStream_t s) {
+  const int d = pf->m->d;
+  if (pf->rows_st && pf->rows_st_w == d + 2) {            // one {ll, class, state} buffer
+    TRY(launch_unpack_rows(pf, pf->rows_st - 1, GPMDM_PACK_ALL, pf->rows_inv, s));
+    if (pf->rows_ll == pf->rows_st - 1) pf->rows_ll = nullptr;
+  } else if (pf->rows_st) {
+    TRY(launch_unpack_rows(pf, pf->rows_st, GPMDM_PACK_STATES, pf->rows_inv, s));
+  }
+  if (pf->rows_ll) {
+    if (pf->rows_ll_w == d + 2)
+      TRY(launch_unpack_rows(pf, pf->rows_ll, GPMDM_PACK_ALL, pf->rows_inv, s));
+    else
+      TRY(launch_unpack_rows(pf, pf->rows_ll, GPMDM_PACK_LL, pf->rows_inv, s));
+  }
+  pf->rows_st = pf->rows_ll = nullptr;
   return GPMDM_OK;
 }
 
@@ -1891,9 +1948,30 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   pf->mark_begin(s, GPMDM_STAGE_RESAMPLE, t0);
   ResampleArgs ra = resample_args(pf);
   ra.U = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->rep_src[2] : nullptr;
-  const bool cls_host = pf->cls_pin && small_resample_ok(norm_args(pf), ra);
+  NormArgs na = norm_args(pf);
+  const bool small = small_resample_ok(na, ra);
+  if (small || !pf->bmax_rows) TRY(flush_rows(pf, s));    // (unpack_part holds rows only for this path)
+  if (pf->rows_ll) {                   // the exchanged ll column, and its maximum for the normaliser
+    RowsLLArgs la{};
+    la.P = pf->P;
+    la.rows = pf->rows_ll;
+    la.w = pf->rows_ll_w;
+    la.inv = pf->rows_inv;
+    la.ll = pf->ll;
+    la.bmax = pf->bmax_rows;
+    launch_rows_ll(la, s);
+    na.bmax = pf->bmax_rows;
+    na.nbmax = rows_ll_blocks(pf->P);
+  }
+  if (pf->rows_st) {                   // the gathers read the exchanged rows in place
+    ra.rows = pf->rows_st;
+    ra.rows_w = pf->rows_st_w;
+    ra.rows_inv = pf->rows_inv;
+  }
+  pf->rows_st = pf->rows_ll = nullptr;
+  const bool cls_host = pf->cls_pin && small;
   if (cls_host) ra.cls_host = pf->cls_pdev;
-  launch_normalise_resample(norm_args(pf), ra, s);
+  launch_normalise_resample(na, ra, s);
   pf->bmax_ready = false;
   pf->cls_host_ok = cls_host;
   if (cls_host) {
@@ -1902,11 +1980,14 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   }
   pf->ll_pending = false;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(2, s));
-  // next frame's ownership order (identical on every rank: same replicated ancestors)
+  // next frame's ownership order (identical on every rank: the same draws), after the
+  // gathers that read this frame's rows through the current one; systematic uniforms rise
+  // with the slot, so the identity order already groups the slots by ancestor
   pf->own_valid = false;
-  if (pf->own && pf->dedup && pf->shard_order) {
-    if (launch_ancestor_order(pf->ridx, pf->own, pf->own_inv, pf->P, pf->own_tmp, pf->own_tmp_bytes, s) != 0)
-      return fail(GPMDM_E_HIP, "ancestor-order pass failed");
+  if (pf->own && pf->dedup && pf->shard_order && !sys && uniform_order_supported(pf->P)) {
+    if (launch_uniform_order(pf->P, pf->frame, pf->seed_lo, pf->seed_hi, pf->own, pf->own_inv, pf->own_tmp,
+                             pf->own_tmp_bytes, s) != 0)
+      return fail(GPMDM_E_HIP, "ownership-order pass failed");
     pf->own_valid = true;
   }
   pf->mark_end(s, GPMDM_STAGE_RESAMPLE, t0);
@@ -1969,6 +2050,7 @@ int gpmdm_pf_export(gpmdm_pf_t pf, double* states, int64_t* classes, double* ll,
   HIPCHK(hipSetDevice(m->device));
   hipStream_t s = (hipStream_t)stream;
   TRY(flush_ll(pf, s));
+  TRY(flush_rows(pf, s));
   HIPCHK(hipStreamSynchronize(s));
   const long long P = pf->P;
   if (states) HIPCHK(hipMemcpy(states, pf->X, sizeof(double) * P * m->d, hipMemcpyDeviceToHost));

@@ -189,9 +189,23 @@ struct NormArgs {
   // kernel computes ll itself first, the multi-kernel path launches k_obs_ll first
   ObsFinishArgs obs;
   int obs_pending;
-  // k_obs_ll's block maxima of ll (single filters, nb keys): the maximum without k_norm_max
+  // k_obs_ll's block maxima of ll (single filters, nb keys; k_rows_ll: nbmax keys): the
+  // maximum without k_norm_max
   const unsigned long long* bmax;
+  int nbmax;                      // keys in bmax (0: nb)
 };
+
+// k_rows_ll: the exchanged {ll} column into particle order + block maxima (single filters)
+struct RowsLLArgs {
+  long long P;
+  const double* rows;             // column 0 of row r = ll of particle own[r]
+  int w;                          // doubles per row
+  const int* inv;                 // particle p's row (nullptr: p)
+  double* ll;
+  unsigned long long* bmax;       // rows_ll_blocks(P) keys
+};
+int rows_ll_blocks(long long P);
+void launch_rows_ll(const RowsLLArgs& a, hipStream_t s);
 
 struct ResampleArgs {
   long long P;                    // particles per filter
@@ -215,6 +229,11 @@ struct ResampleArgs {
                                   // single replay filters: the next switch's counts on the host), or nullptr
   int* guide;                     // F x (GB + 3): guide[b] = first i with cum[i] >= b / GB
   long long GB;                   // guide buckets per filter
+  // exchanged {class, state} rows read in place instead of cls_src / X_src (multi-rank
+  // filters: row rows_inv[p] holds particle p, column 0 its class, 1..d its state), or nullptr
+  const double* rows;
+  int rows_w;
+  const int* rows_inv;
   // systematic resampling by scan (no per-slot search): run starts of each particle's
   // offspring marked in sys_mark (F x P), block-local max-scan in place, block maxima
   // (F x nb) scanned; slot s's ancestor = max(local[s], block prefix).  nullptr: search.
@@ -242,14 +261,15 @@ struct PackArgs {
   double* X;
 };
 
-// Ancestor-ordered shards (shard_order.hip): own = particles in stable order of their
-// resampling ancestor's bucket (256 contiguous ancestor ranges), so each rank's contiguous
-// slice of that order covers a contiguous range of ancestors.  Deterministic (identical on
-// every rank).  temp: ancestor_order_temp_bytes(P) of device memory.
-size_t ancestor_order_temp_bytes(long long P);
-// inv: the inverse permutation, inv[own[r]] = r (unpack reads particle p's row inv[p])
-int launch_ancestor_order(const int* anc, int* own, int* inv, long long P, void* temp, size_t temp_bytes,
-                          hipStream_t s);
+// Ancestor-ordered shards (shard_order.hip): own = slots in stable order of the bucket
+// floor(256 u) of their resampling uniform (Philox draw of `frame`, single filters), so each
+// rank's contiguous slice of that order descends from a contiguous range of ancestors.
+// Deterministic (identical on every rank).  temp: uniform_order_temp_bytes(P) of device memory.
+size_t uniform_order_temp_bytes(long long P);
+bool uniform_order_supported(long long P);   // P <= 33.5M (larger filters keep the identity order)
+// inv: the inverse permutation, inv[own[r]] = r (particle p's exchanged row is inv[p])
+int launch_uniform_order(long long P, unsigned frame, unsigned seed_lo, unsigned seed_hi, int* own, int* inv,
+                         void* temp, size_t temp_bytes, hipStream_t s);
 
 void launch_switch(const SwitchArgs& a, hipStream_t s);
 void launch_scan_counts(const ScanArgs& a, hipStream_t s);

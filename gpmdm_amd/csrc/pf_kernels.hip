@@ -712,7 +712,8 @@ __global__ __launch_bounds__(kB) void k_norm_exp_scan(NormArgs a) {
     // single filter: the maximum over k_obs_ll's block maxima (no k_norm_max launch); every
     // block computes it, block 0 publishes it for the resample and export
     unsigned long long key = 0;
-    for (int i = tid; i < a.nb; i += kB) key = a.bmax[i] > key ? a.bmax[i] : key;
+    const int nk = a.nbmax ? a.nbmax : a.nb;
+    for (int i = tid; i < nk; i += kB) key = a.bmax[i] > key ? a.bmax[i] : key;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       const unsigned long long y = __shfl_xor(key, off);
@@ -791,18 +792,65 @@ __global__ __launch_bounds__(kB) void k_cdf(NormArgs a) {
 // Guide table for the inverse-CDF search: guide[b] = first i with cum[i] >= b / GB (P if
 // none), for b = 0 .. GB + 2.  The queries b / GB are sorted, so neighbouring threads walk
 // nearly the same binary-search path (cache-friendly, unlike the random uniforms).
+//
+// A wave's 64 queries are consecutive, so their answers lie between those of its first and
+// last query: lanes 0-31 and 32-63 find those two by 32-way searches (32 independent probes
+// per step: four steps span 10^6 particles, against 20 dependent loads of a binary search),
+// then each lane searches the usually short range between them -- in registers when it holds
+// at most 64 particles (a collapsed cloud's range is often a single particle).  For a monotone
+// CDF every form returns the binary search's answer.
 __global__ __launch_bounds__(kB) void k_guide(ResampleArgs a) {
   const long long f = blockIdx.y;
+  const int lane = threadIdx.x & 63;
   const long long b = (long long)blockIdx.x * kB + threadIdx.x;
-  if (b > a.GB + 2) return;
-  const double t = (double)b / (double)a.GB;
+  const long long nb = a.GB + 3;                       // queries b = 0 .. GB + 2
+  const long long b0 = b - lane;                       // the wave's first query
+  if (b0 >= nb) return;                                // (wave-uniform)
+  const long long bl = b0 + 63 < nb - 1 ? b0 + 63 : nb - 1;   // its last query
   const double* cum = a.cum + f * a.P;
-  long long lo = 0, hi = a.P;
-  while (hi - lo > 0) {
-    const long long mid = lo + (hi - lo) / 2;
-    if (cum[mid] < t) lo = mid + 1; else hi = mid;
+  // two 32-way searches in lock step: half h finds the first index with cum >= t(h ? bl : b0)
+  const int h = lane >> 5, k = lane & 31;
+  const unsigned long long hm = h ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+  const double th = (double)(h ? bl : b0) / (double)a.GB;
+  long long L = 0, H = a.P;
+  while (__ballot(H - L > 32)) {
+    const long long st = (H - L + 31) / 32;
+    const bool live = H - L > 32;
+    long long q = (L + (long long)(k + 1) * st < H ? L + (long long)(k + 1) * st : H) - 1;
+    q = q > 0 ? q : 0;
+    const long long c = __popcll(__ballot(live && cum[q] < th) & hm);
+    if (live) {
+      const long long nH = L + (c + 1) * st < H ? L + (c + 1) * st : H;
+      L = L + c * st < H ? L + c * st : H;
+      H = nH;
+    }
   }
-  a.guide[f * (a.GB + 3) + b] = (int)lo;
+  {
+    const long long q = L + k;
+    L += __popcll(__ballot(q < H && cum[q] < th) & hm);
+  }
+  const long long A0 = __shfl(L, 0), A1 = __shfl(L, 32);
+  const double t = (double)b / (double)a.GB;
+  long long lo = A0, hi = A1;                          // this lane's answer is in [A0, A1]
+  if (A1 - A0 <= 64) {
+    // the range's CDF values in registers, one per lane; per lane a binary search over them
+    const double v = A0 + lane < A1 ? cum[A0 + lane] : 0.0;
+    int l = 0, r = (int)(A1 - A0);
+    while (__ballot(r > l)) {
+      const int m = l + (r - l) / 2;
+      const double vm = __shfl(v, m < 63 ? m : 63);
+      if (r > l) {
+        if (vm < t) l = m + 1; else r = m;
+      }
+    }
+    lo = A0 + l;
+  } else {
+    while (hi - lo > 0) {
+      const long long mid = lo + (hi - lo) / 2;
+      if (cum[mid] < t) lo = mid + 1; else hi = mid;
+    }
+  }
+  if (b < nb) a.guide[f * nb + b] = (int)lo;
 }
 
 // ---------------------------------------------------------------------------------
@@ -904,6 +952,7 @@ __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
   const bool act = s < a.P;
   long long idx = 0;                                       // source, within filter f
   int cnew = -1;
+  const double* xs = nullptr;                              // the source particle's state
   double e2 = 0.0, wv = 0.0;
   if (act) {
     if (a.identity) {
@@ -938,11 +987,17 @@ __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
       }
       idx = lo;
     }
-    cnew = a.cls_src[g0 + idx];
+    if (a.rows) {                 // the exchanged row of particle idx, read in place
+      const double* row = a.rows + (a.rows_inv ? (long long)a.rows_inv[g0 + idx] : g0 + idx) * a.rows_w;
+      cnew = (int)row[0];
+      xs = row + 1;
+    } else {
+      cnew = a.cls_src[g0 + idx];
+      xs = a.X_src + (g0 + idx) * d;
+    }
     if (!a.identity) {
       a.ridx[g0 + s] = (int)idx;
       a.cls_dst[g0 + s] = cnew;
-      for (int j = 0; j < d; ++j) a.X_dst[(g0 + s) * d + j] = a.X_src[(g0 + idx) * d + j];
     }
     // read-outs: post-resample class/state at slot s, pre-resample ll/log_w at slot s
     const double M = ord_dec(a.gmax[f]);
@@ -951,12 +1006,26 @@ __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
     e2 = exp((llv + lw) - M);                  // ll + log_w - max(ll + log_w); that max is M
     wv = a.e[g0 + s] / a.total[f];
   }
+  if (!a.identity) {
+    // The wave's 64 new states are one contiguous run of X_dst: lane l stores its elements
+    // l, l + 64, ... of that run (8-byte stores, each instruction one contiguous 512 bytes)
+    // from the source rows it finds through the owning lanes' pointers -- rows this wave has
+    // just read.  Per-lane stores of d doubles at stride 8 d bytes ran at ~1 TB/s.
+    const long long s0 = s - lane;                         // the wave's first slot
+    const long long nv = a.P - s0 < 64 ? a.P - s0 : 64;   // its slots in range (wave-uniform)
+    const long long n = nv * d;
+    for (long long e = lane; e < 64LL * d; e += 64) {
+      const int l2 = (int)(e / d), i2 = (int)(e - (long long)l2 * d);
+      const double* src = (const double*)__shfl((long long)xs, l2);
+      if (e < n) a.X_dst[(g0 + s0) * d + e] = src[i2];
+    }
+  }
   for (int k = 0; k < nq; ++k) {
     double v = 0.0;
     if (act) {
       if (k < C) v = (cnew == k) ? e2 : 0.0;
       else if (k == C) v = e2;
-      else v = a.X_src[(g0 + idx) * d + (k - C - 1)] * wv;
+      else v = xs[k - C - 1] * wv;
     }
     v = wave_sum(v);
     if (lane == 0) red[w][k] = v;
@@ -966,6 +1035,40 @@ __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
     double t = 0.0;
     for (int v = 0; v < kB / 64; ++v) t += red[v][tid];
     a.partials[(f * a.nb + blockIdx.x) * nq + tid] = t;
+  }
+}
+
+// The all-gathered {ll} column (rows in position order: row r holds particle own[r]) into
+// particle order, with each kRowsLL-particle block's maximum as an ord_enc key: the
+// normaliser's maximum (gpmdm_pf.py:200) without k_norm_max, as k_obs_ll gives it to a
+// single rank.  The maximum of a set in ord_enc's total order does not depend on how the
+// set is split, so it is k_norm_max's result exactly.
+constexpr int kRowsLLPer = 8;
+constexpr long long kRowsLL = (long long)kRowsLLPer * kB;
+__global__ __launch_bounds__(kB) void k_rows_ll(RowsLLArgs a) {
+  __shared__ unsigned long long wk[kB / 64];
+  unsigned long long key = 0;            // below ord_enc of any double
+#pragma unroll
+  for (int k = 0; k < kRowsLLPer; ++k) {
+    const long long p = (long long)blockIdx.x * kRowsLL + (long long)k * kB + threadIdx.x;
+    if (p < a.P) {
+      const double v = a.rows[(a.inv ? (long long)a.inv[p] : p) * a.w];
+      a.ll[p] = v;
+      const unsigned long long kk = ord_enc(fmax(-INFINITY, v));   // k_norm_max's value set: NaN ignored
+      key = kk > key ? kk : key;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long y = __shfl_xor(key, off);
+    key = y > key ? y : key;
+  }
+  if ((threadIdx.x & 63) == 0) wk[threadIdx.x >> 6] = key;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = wk[0];
+    for (int i = 1; i < kB / 64; ++i) m = wk[i] > m ? wk[i] : m;
+    a.bmax[blockIdx.x] = m;
   }
 }
 
@@ -1412,6 +1515,10 @@ void launch_normalise_resample(const NormArgs& na, const ResampleArgs& ra, hipSt
   if (na.obs_pending) launch_obs_finish(na.obs, s);
   launch_normalise(na, s);
   launch_resample(ra, s);
+}
+int rows_ll_blocks(long long P) { return (int)nblk(P, kRowsLL); }
+void launch_rows_ll(const RowsLLArgs& a, hipStream_t s) {
+  if (a.P > 0) hipLaunchKernelGGL(k_rows_ll, dim3(nblk(a.P, kRowsLL)), dim3(kB), 0, s, a);
 }
 void launch_pack(const PackArgs& a, hipStream_t s) {
   if (a.n > 0) hipLaunchKernelGGL(k_pack, dim3(nblk(a.n, kB)), dim3(kB), 0, s, a);

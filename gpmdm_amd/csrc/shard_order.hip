@@ -7,149 +7,179 @@
 // covers a contiguous ancestor range, and the dynamics GP's ancestor de-duplication keeps
 // ~1/R of the distinct (ancestor, class) keys per rank instead of nearly all of them.
 //
-// The order is a stable bucket sort on the ancestor's bucket b = anc * 256 / P (256
-// contiguous ancestor ranges; particle order inside a bucket).  Exact ancestor order is not
-// needed: a rank's slice spans whole buckets except at its two ends, so at most the
-// ancestors of two buckets are shared with neighbours.  Every step is deterministic (block
-// histograms, fixed-order scans, ranks counted in particle order), so every rank computes
-// the same order.  Four small launches, O(P):
-//   k_bucket_hist     per-block bucket histograms, bucket-major H[b][block]
-//   k_chunk_scan      exclusive scan of H inside 1024-entry chunks, chunk totals
-//   k_chunk_offsets   one workgroup: exclusive scan of the chunk totals
-//   k_bucket_scatter  own[start(b, block) + rank in block] = particle, and its inverse
-// (rocPRIM's radix sort of the same keys measured 145 us at P = 800k on MI355X,
-// tools/microbench/sort_probe.hip; this pass is a few us per launch.)
+// The order is a stable bucket sort of the slots on the bucket of their resampling uniform,
+// b = floor(256 u_s).  The inverse-CDF search maps u monotonically to the ancestor, so a
+// bucket's slots descend from one contiguous ancestor range and a rank's slice spans whole
+// buckets except at its two ends -- the same locality as sorting on the ancestor itself, but
+// computed from the draws alone (Philox, keyed by slot and frame): no ancestor array is
+// read, nothing waits for the search.  Systematic resampling needs no pass at all (its
+// uniforms, hence its ancestors, rise with the slot index: the identity order).  Every step
+// is deterministic (block histograms, fixed-order scans, ranks counted in slot order), so
+// every rank builds the same order.  Three launches, O(P):
+//   k_ubucket_hist        per-block bucket histograms (2048 slots per block), bucket-major H[b][block]
+//   k_ubucket_chunk_scan  exclusive scan of H inside 1024-entry chunks, chunk totals
+//   k_ubucket_scatter     (each block first scans the chunk totals in LDS)
+//                         own[offset(b, block) + rank of the slot among the block's bucket-b slots]
+//                         = slot, and its inverse
+// (rocPRIM's radix sort of such keys measured 145 us at P = 800k on MI355X,
+// tools/microbench/sort_probe.hip.)
 #include "pf_kernels.h"
 
 namespace gpmdm {
 
 namespace {
 
-constexpr int kOB = 256;          // particles per block = buckets
-constexpr int kChunk = 1024;      // H entries per scan chunk (4 per thread)
+constexpr int kT = 256;           // threads per block = buckets
+constexpr int kPer = 8;           // rounds of kT consecutive slots per block
+constexpr int kBlk = kT * kPer;   // slots per block
 
-__device__ __forceinline__ int bucket_of(int anc, long long P) { return (int)(((long long)anc * kOB) / P); }
+// bucket of slot s's resampling uniform (k_resample's Philox draw, bit for bit)
+__device__ __forceinline__ int ubucket(long long s, unsigned frame, uint2 key) {
+  const uint4 r = philox4x32_10(make_uint4((unsigned)s, frame, kStreamResample, 0u), key);
+  const int b = (int)(u01_co(r.x, r.y) * (double)kT);
+  return b < kT - 1 ? b : kT - 1;
+}
 
-__global__ __launch_bounds__(kOB) void k_bucket_hist(const int* anc, long long P, int nblk, int* H) {
-  __shared__ int hist[kOB];
+__global__ __launch_bounds__(kT) void k_ubucket_hist(long long P, unsigned frame, uint2 key, int nblk, int* H) {
+  __shared__ int hist[kT];
   const int tid = threadIdx.x;
   hist[tid] = 0;
   __syncthreads();
-  const long long s = (long long)blockIdx.x * kOB + tid;
-  if (s < P) atomicAdd(&hist[bucket_of(anc[s], P)], 1);
+  const long long s0 = (long long)blockIdx.x * kBlk + tid;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const long long s = s0 + (long long)k * kT;
+    if (s < P) atomicAdd(&hist[ubucket(s, frame, key)], 1);
+  }
   __syncthreads();
   H[(long long)tid * nblk + blockIdx.x] = hist[tid];
 }
 
-__global__ __launch_bounds__(256) void k_chunk_scan(int* H, long long n, int* chunk_tot) {
-  __shared__ int part[256];
-  const int tid = threadIdx.x;
+// Exclusive scan of H inside kChunk-entry chunks (in place), and each chunk's total.
+constexpr int kChunk = 1024;                   // H entries per chunk (4 per thread)
+constexpr int kMaxChunks = 4096;               // k_ubucket_scatter scans the chunk totals in LDS
+__global__ __launch_bounds__(kT) void k_ubucket_chunk_scan(int* H, long long n, int* chunk_tot) {
+  __shared__ int wtot[kT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const long long base = (long long)blockIdx.x * kChunk + tid * 4;
-  int v[4], run = 0;
+  int v[4], t = 0;
+#pragma unroll
   for (int k = 0; k < 4; ++k) {
     v[k] = base + k < n ? H[base + k] : 0;
+    t += v[k];
+  }
+  int x = t;                                   // inclusive wave scan of the thread totals
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wtot[w] = x;
+  __syncthreads();
+  int run = x - t;
+  for (int u = 0; u < w; ++u) run += wtot[u];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (base + k < n) H[base + k] = run;
     run += v[k];
   }
-  part[tid] = run;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {          // Hillis-Steele inclusive scan
-    const int x = tid >= off ? part[tid - off] : 0;
-    __syncthreads();
-    part[tid] += x;
-    __syncthreads();
-  }
-  int e = tid ? part[tid - 1] : 0;
-  for (int k = 0; k < 4; ++k) {
-    if (base + k < n) H[base + k] = e;
-    e += v[k];
-  }
-  if (tid == 255) chunk_tot[blockIdx.x] = part[255];
+  if (tid == kT - 1) chunk_tot[blockIdx.x] = run;
 }
 
-__global__ __launch_bounds__(1024) void k_chunk_offsets(int* chunk_tot, int nchunk) {
-  __shared__ int part[1024];
-  const int tid = threadIdx.x;
-  const int per = (nchunk + 1023) / 1024;
-  int s = 0;
-  for (int i = 0; i < per; ++i) {
-    const int c = tid * per + i;
-    if (c < nchunk) s += chunk_tot[c];
-  }
-  part[tid] = s;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const int x = tid >= off ? part[tid - off] : 0;
+__global__ __launch_bounds__(kT) void k_ubucket_scatter(long long P, unsigned frame, uint2 key, int nblk,
+                                                        const int* H, const int* chunk_tot, int nchunk,
+                                                        int* own, int* inv) {
+  constexpr int kW = kT / 64;
+  constexpr int kCPer = kMaxChunks / kT;
+  __shared__ int cnt[kW][kT];                  // this round's bucket counts per wave
+  __shared__ int run[kT];                      // the block's earlier rounds' counts per bucket
+  __shared__ int coff[kMaxChunks];             // exclusive prefix of the chunk totals
+  __shared__ int wtot[kW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  {                                            // every block scans the (few) chunk totals itself
+    int v[kCPer], t = 0;
+#pragma unroll
+    for (int k = 0; k < kCPer; ++k) {
+      const int c = tid * kCPer + k;
+      v[k] = c < nchunk ? chunk_tot[c] : 0;
+      t += v[k];
+    }
+    int x = t;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wtot[w] = x;
     __syncthreads();
-    part[tid] += x;
-    __syncthreads();
-  }
-  int run = tid ? part[tid - 1] : 0;
-  for (int i = 0; i < per; ++i) {
-    const int c = tid * per + i;
-    if (c < nchunk) {
-      const int t = chunk_tot[c];
-      chunk_tot[c] = run;
-      run += t;
+    int e = x - t;
+    for (int u = 0; u < w; ++u) e += wtot[u];
+#pragma unroll
+    for (int k = 0; k < kCPer; ++k) {
+      coff[tid * kCPer + k] = e;
+      e += v[k];
     }
   }
-}
-
-__global__ __launch_bounds__(kOB) void k_bucket_scatter(const int* anc, long long P, int nblk, const int* H,
-                                                         const int* chunk_off, int* own, int* inv) {
-  constexpr int kW = kOB / 64;
-  __shared__ int cnt[kW][kOB];                        // bucket counts per wave
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const long long s = (long long)blockIdx.x * kOB + tid;
-  const int b = s < P ? bucket_of(anc[s], P) : -1;
-  for (int i = tid; i < kW * kOB; i += kOB) (&cnt[0][0])[i] = 0;
-  // rank among this block's bucket-b particles, in particle order: lanes of this wave with
-  // the same bucket (ballots over the bucket's 8 bits and its validity), then the earlier
-  // waves' counts of that bucket -- deterministic, so every rank builds the same order
-  unsigned long long same = ~0ull;
+  run[tid] = 0;
+  for (int k = 0; k < kPer; ++k) {
+    const long long s = (long long)blockIdx.x * kBlk + (long long)k * kT + tid;
+    const int b = s < P ? ubucket(s, frame, key) : -1;
+    for (int i = tid; i < kW * kT; i += kT) (&cnt[0][0])[i] = 0;
+    // rank among this wave's bucket-b slots (ballots over the bucket's 8 bits and validity)
+    unsigned long long same = ~0ull;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const bool bit = (b >> k) & 1;
-    const unsigned long long m = __ballot(bit);
-    same &= bit ? m : ~m;
+    for (int j = 0; j < 8; ++j) {
+      const bool bit = (b >> j) & 1;
+      const unsigned long long m = __ballot(bit);
+      same &= bit ? m : ~m;
+    }
+    const unsigned long long valid = __ballot(b >= 0);
+    same &= b >= 0 ? valid : ~valid;
+    const int r_wave = __popcll(same & ((1ull << lane) - 1));
+    __syncthreads();
+    if (b >= 0 && r_wave == 0) cnt[w][b] = __popcll(same);   // one writer per (wave, bucket)
+    __syncthreads();
+    if (b >= 0) {
+      int r = run[b] + r_wave;
+      for (int v = 0; v < w; ++v) r += cnt[v][b];
+      const long long h = (long long)b * nblk + blockIdx.x;
+      const int pos = coff[h / kChunk] + H[h] + r;
+      own[pos] = (int)s;
+      inv[s] = pos;
+    }
+    __syncthreads();
+    int t = 0;
+    for (int v = 0; v < kW; ++v) t += cnt[v][tid];
+    run[tid] += t;
   }
-  const unsigned long long valid = __ballot(b >= 0);
-  same &= b >= 0 ? valid : ~valid;
-  const int r_wave = __popcll(same & ((1ull << lane) - 1));
-  __syncthreads();
-  if (b >= 0 && r_wave == 0) cnt[w][b] = __popcll(same);   // one writer per (wave, bucket)
-  __syncthreads();
-  if (b < 0) return;
-  int r = r_wave;
-  for (int v = 0; v < w; ++v) r += cnt[v][b];
-  const long long h = (long long)b * nblk + blockIdx.x;
-  const int pos = chunk_off[h / kChunk] + H[h] + r;
-  own[pos] = (int)s;
-  inv[s] = pos;
 }
 
-inline unsigned nblocks(long long n, int b) { return (unsigned)((n + b - 1) / b); }
+inline unsigned nblocks(long long n, long long b) { return (unsigned)((n + b - 1) / b); }
 
 }  // namespace
 
-size_t ancestor_order_temp_bytes(long long P) {
-  const long long nblk = (P + kOB - 1) / kOB;
-  const long long n = nblk * kOB;
-  const long long nchunk = (n + kChunk - 1) / kChunk;
-  return sizeof(int) * (size_t)(n + nchunk);
+bool uniform_order_supported(long long P) {
+  return nblocks((long long)kT * nblocks(P, kBlk), kChunk) <= (unsigned)kMaxChunks;   // P <= 33.5M
 }
 
-int launch_ancestor_order(const int* anc, int* own, int* inv, long long P, void* temp, size_t temp_bytes,
-                          hipStream_t s) {
-  const int nblk = (int)nblocks(P, kOB);
-  const long long n = (long long)nblk * kOB;
+size_t uniform_order_temp_bytes(long long P) {
+  const long long n = (long long)kT * nblocks(P, kBlk);
+  return sizeof(int) * (size_t)(n + nblocks(n, kChunk));
+}
+
+int launch_uniform_order(long long P, unsigned frame, unsigned seed_lo, unsigned seed_hi, int* own, int* inv,
+                         void* temp, size_t temp_bytes, hipStream_t s) {
+  const int nblk = (int)nblocks(P, kBlk);
+  const long long n = (long long)kT * nblk;
   const int nchunk = (int)nblocks(n, kChunk);
-  if (temp_bytes < ancestor_order_temp_bytes(P)) return -1;
+  if (temp_bytes < uniform_order_temp_bytes(P) || !uniform_order_supported(P)) return -1;
   int* H = static_cast<int*>(temp);
-  int* chunk = H + n;
-  hipLaunchKernelGGL(k_bucket_hist, dim3(nblk), dim3(kOB), 0, s, anc, P, nblk, H);
-  hipLaunchKernelGGL(k_chunk_scan, dim3(nchunk), dim3(256), 0, s, H, n, chunk);
-  hipLaunchKernelGGL(k_chunk_offsets, dim3(1), dim3(1024), 0, s, chunk, nchunk);
-  hipLaunchKernelGGL(k_bucket_scatter, dim3(nblk), dim3(kOB), 0, s, anc, P, nblk, H, chunk, own, inv);
+  int* chunk_tot = H + n;
+  const uint2 key = make_uint2(seed_lo, seed_hi);   // filter_key(seed, 0): a single filter
+  hipLaunchKernelGGL(k_ubucket_hist, dim3(nblk), dim3(kT), 0, s, P, frame, key, nblk, H);
+  hipLaunchKernelGGL(k_ubucket_chunk_scan, dim3(nchunk), dim3(kT), 0, s, H, n, chunk_tot);
+  hipLaunchKernelGGL(k_ubucket_scatter, dim3(nblk), dim3(kT), 0, s, P, frame, key, nblk, H, chunk_tot, nchunk,
+                     own, inv);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -186,7 +186,12 @@ int gpmdm_pf_weigh(gpmdm_pf_t pf, const double* z, void* stream);
 /* Multi-rank exchange: pack this rank's rows [lo, hi) as (hi-lo) x (d+2) doubles
  * {ll, class, state[d]}; unpack all P rows after an all-gather.  The _part forms move
  * column subsets: GPMDM_PACK_STATES = {class, state[d]} (d+1 wide; valid after
- * propagate_dynamics), GPMDM_PACK_LL = {ll} (1 wide; valid after weigh). */
+ * propagate_dynamics), GPMDM_PACK_LL = {ll} (1 wide; valid after weigh).
+ * Unpacking hands the gathered rows to the filter, which reads them in place during the
+ * next gpmdm_pf_resample (its gathers touch only the resampled ancestors' rows; the ll
+ * column is read once, with the normaliser's maximum): recv_dev must stay allocated and
+ * unmodified until that resample's kernels have run -- stream order on the resample's stream
+ * suffices (the next frame's all-gather into the same buffer, enqueued after it, is safe). */
 enum { GPMDM_PACK_ALL = 0, GPMDM_PACK_STATES = 1, GPMDM_PACK_LL = 2 };
 int gpmdm_pf_exchange_width(gpmdm_pf_t pf, int64_t* width, int64_t* lo, int64_t* hi);
 int gpmdm_pf_pack(gpmdm_pf_t pf, double* send_dev, void* stream);
@@ -293,10 +298,12 @@ int gpmdm_pf_dyn_rows(gpmdm_pf_t pf, int64_t* rows, void* stream);
 int gpmdm_pf_set_dyn_tiles(gpmdm_pf_t pf, int mode);
 
 /* Ancestor-ordered shards (multi-rank philox filters; default on).  After each resample the
- * particles are put in a stable order of their resampling ancestor's bucket (256 contiguous
- * ancestor ranges; identical on every rank) and rank r evaluates positions [lo, hi) of that
- * order instead of particles [lo, hi), so its slice covers a contiguous ancestor range and
- * de-duplication keeps ~1/R of the distinct (ancestor, class) keys.  Pack/unpack rows follow the same order, so the all-gathered
+ * particles are put in a stable order of their resampling uniform's bucket floor(256 u) (the
+ * inverse-CDF search is monotone in u, so a bucket descends from a contiguous ancestor range;
+ * identical on every rank; systematic resampling: the identity order, already ancestor-
+ * ordered) and rank r evaluates positions [lo, hi) of that order instead of particles
+ * [lo, hi), so its slice covers a contiguous ancestor range and de-duplication keeps ~1/R of
+ * the distinct (ancestor, class) keys.  Pack/unpack rows follow the same order, so the all-gathered
  * filter is bitwise the same either way.  No effect on one rank, replay draws or without
  * de-duplication.  Every rank must make the same call, outside switch..resample. */
 int gpmdm_pf_set_shard_order(gpmdm_pf_t pf, int enable);

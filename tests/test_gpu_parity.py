@@ -526,6 +526,50 @@ def test_logical_shards_match_one_rank(m2, world, rng_mode, order, P, split, res
             assert np.array_equal(ref.current_state_mean().numpy(), pf.current_state_mean().numpy())
 
 
+@pytest.mark.parametrize("P", [10_007, 300_001])
+def test_exchanged_rows_read_in_place(m2, P):
+    """gpmdm_pf_unpack_part hands the gathered rows to the filter: the resample reads the
+    {class, state} rows and the {ll} column in place (through the ownership order).  A reader
+    between unpack and resample (export_state) gets them written out first: its ll equals the
+    one-rank filter's pre-resample ll, and every frame stays bitwise the one-rank filter's.
+    P = 300001 runs the guide-table search (and its wave-cooperative wide brackets)."""
+    from gpmdm_amd import GPMDM_PF, _lib
+    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
+    Y = m2.get_Y()
+    world = 3
+    pfs = []
+    for r in [None] + list(range(world)):            # the same initial particles (torch draws)
+        torch.manual_seed(6)
+        pfs.append(GPMDM_PF(m2, T, P, rng="philox", seed=17, shard=None if r is None else (world, r)))
+    ref, ranks = pfs[0], pfs[1:]
+    lib = _lib.load()
+    for k in range(4):
+        z = np.ascontiguousarray(np.asarray(Y[40 + 5 * k], dtype=np.float64))
+        h, s = ref._h, ref._stream()
+        _lib.check(lib.gpmdm_pf_switch(h, None, None, s), "switch")
+        _lib.check(lib.gpmdm_pf_propagate(h, _lib.dptr(z), None, s), "propagate")
+        for pf in ranks:
+            _lib.check(lib.gpmdm_pf_switch(pf._h, None, None, pf._stream()), "switch")
+            _lib.check(lib.gpmdm_pf_propagate_dynamics(pf._h, None, pf._stream()), "propagate_dynamics")
+        _split_exchange(lib, ranks, z)
+        if k == 1:                                   # a reader before the resample
+            a = ref.export_state()
+            b = ranks[1].export_state()
+            assert np.array_equal(a["ll"], b["ll"])
+        _lib.check(lib.gpmdm_pf_resample(h, None, s), "resample")
+        ref._readout = None
+        for pf in ranks:
+            _lib.check(lib.gpmdm_pf_resample(pf._h, None, pf._stream()), "resample")
+            pf._readout = None
+        a = ref.export_state()
+        for pf in ranks:
+            b = pf.export_state()
+            for key in ("states", "classes", "ll", "w", "resample_idx"):
+                assert np.array_equal(a[key], b[key]), (k, key)
+            assert np.array_equal(ref.class_probabilities().numpy(), pf.class_probabilities().numpy())
+            assert np.array_equal(ref.current_state_mean().numpy(), pf.current_state_mean().numpy())
+
+
 def test_empty_class_segments(m2, fx_config2):
     """A class no particle switches into (its column of T is zero): its dynamics segment is
     empty every frame.  Three resynced steps against the oracle."""
