@@ -28,7 +28,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import assert_step_matches, nrel, oracle_model, product_model
+from conftest import assert_step_matches, nrel, oracle_model, product_model, record_ties
 
 pytestmark = pytest.mark.gpu
 
@@ -205,6 +205,7 @@ def test_one_million_particles_single_rank_vs_oracle(fx_config2):
     # resample indices: the oracle's search of the GPU's weights with the restated uniforms
     u = X.resample_uniforms(seed, frame, P)
     ref_idx = O.multinomial_resample_indices(post["w"], u)
+    record_ties("test_one_million_particles_single_rank_vs_oracle", len(idx), int(np.sum(ref_idx != idx)))
     assert int(np.sum(ref_idx != idx)) <= 2, int(np.sum(ref_idx != idx))
     # read-outs at the GPU's indices
     post_c = O.class_probabilities(post["ll"], post["log_w"], post["classes"], C)
