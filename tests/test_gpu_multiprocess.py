@@ -11,7 +11,6 @@ seeds is bitwise as well; with different seeds it must refuse (ValueError) inste
 silently diverging.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -26,12 +25,14 @@ P = 10_001
 FRAMES = 3
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _store_file():
+    """A fresh rendezvous file for a FileStore (no TCP port to race for: a port found free
+    and released can be taken again, or sit in TIME_WAIT, before the store listens)."""
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="gpmdm_store_")
+    os.close(fd)
+    os.unlink(path)
+    return path
 
 
 def _obs(m):
@@ -39,7 +40,7 @@ def _obs(m):
     return [np.asarray(Y[200 + 5 * k], dtype=np.float64) for k in range(FRAMES)]
 
 
-def _worker(rank, world, port, rng, seeds, out_q):
+def _worker(rank, world, store_path, rng, seeds, out_q):
     import faulthandler
     import sys
     import torch.distributed as dist
@@ -48,10 +49,8 @@ def _worker(rank, world, port, rng, seeds, out_q):
     faulthandler.dump_traceback_later(100, exit=True, file=sys.stderr)
     from conftest import load_fixture
     from gpmdm_amd import GPMDM_PF
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", store=dist.FileStore(store_path, world), rank=rank, world_size=world)
     try:
         m = product_model(load_fixture("config2_n2000_p1000"))
         T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
@@ -77,8 +76,8 @@ def _run(rng, seeds):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, rng, seeds, q)) for r in range(world)]
+    store = _store_file()
+    procs = [ctx.Process(target=_worker, args=(r, world, store, rng, seeds, q)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -130,7 +129,7 @@ def test_process_group_replay_refuses_different_torch_states():
         assert kind == "ValueError" and "identical torch RNG" in msg
 
 
-def _nccl_worker(port, out_q):
+def _nccl_worker(store_path, out_q):
     """World-size-1 RCCL group: the asynchronous all-gather GPMDM_PF overlaps with the
     observation GP (distributed.allgather_rows_start, nccl branch), with kernels queued on
     the current stream between start and wait.  Both branches run: the even
@@ -138,11 +137,9 @@ def _nccl_worker(port, out_q):
     uneven -- the padded gather with its copy-back in wait()."""
     import torch.distributed as dist
     from gpmdm_amd.distributed import allgather_rows_start
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    dist.init_process_group("nccl", store=dist.FileStore(store_path, 1), rank=0, world_size=1, device_id=dev)
     try:
         ok = True
         for P, W, pad in ((100_000, 4, None), (7, 1, None), (100_000, 4, 100_001), (7, 1, 9)):
@@ -166,7 +163,7 @@ def _nccl_worker(port, out_q):
 def test_rccl_async_allgather_world1():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p = ctx.Process(target=_nccl_worker, args=(_store_file(), q))
     p.start()
     try:
         kind, payload = q.get(timeout=130)
