@@ -42,7 +42,7 @@ Prints ONE JSON line (rank 0) with the contract fields plus:
                 per particle; SURVEY §8(d)'s dense 2N^2 + 2ND is reported beside it) / mean
                 launch time from HIP events on the launch stream; traffic = HBM bytes per
                 launch of the same kernel from the committed rocprofv3 PMC passes of this
-                bench command (profiles/r03_pmc_summary.json; its "commit" field names the
+                bench command (profiles/r04_pmc_summary.json; its "commit" field names the
                 build it measured -- the driver's bench run has no profiler attached), or null
   cpu_baseline  the CPU oracle (numpy fp64) on this configuration's own particle count
                 for N <= 2000 (a bounded sample of frames), a 1000-particle sample above;
@@ -141,7 +141,7 @@ def obs_model_bytes(N, D):
 def pmc_traffic(cfg):
     """(HBM bytes per launch of the obs tile kernel, source note) from the committed
     rocprofv3 PMC summary of this bench command (tools/pmc_passes.sh + tools/pmc_summary.py)."""
-    for name in ("r03_pmc_summary.json", "r02_pmc_summary.json", "pmc_summary.json"):
+    for name in ("r04_pmc_summary.json", "r03_pmc_summary.json", "r02_pmc_summary.json", "pmc_summary.json"):
         p = ROOT / "profiles" / name
         if not p.exists():
             continue
@@ -675,6 +675,9 @@ def main():
     ap.add_argument("--bank", type=int, default=None,
                     help="filters of the bank line (config 1: 39, the notebook's test trials)")
     ap.add_argument("--no-nodedup", action="store_true")
+    ap.add_argument("--spread-lambda", type=float, default=SPREAD_LAMBDA,
+                    help="observation-GP output scale of the spread line (configurations with more "
+                         "observation dimensions need a smaller one to keep the cloud spread)")
     ap.add_argument("--spread-steps", type=int, default=None,
                     help="frames of the spread-cloud line (config 2, one GPU; default 30, 0 = off)")
     ap.add_argument("--dyn-tiles", default="auto", choices=("auto", "narrow", "wide"),
@@ -851,7 +854,8 @@ def main():
         libx = library_exchange_line(new_filter, zs, min(args.steps, args.library_steps), dist, device, P_total)
     if args.spread_steps is None:
         args.spread_steps = 30 if (args.config == 2 and args.stream == "mocap" and args.y_lambda == 1.0) else 0
-    spread = spread_line(device, args.spread_steps, dyn_tiles=args.dyn_tiles) if args.spread_steps and world == 1 else None
+    spread = (spread_line(device, args.spread_steps, y_lambda=args.spread_lambda, dyn_tiles=args.dyn_tiles)
+              if args.spread_steps and world == 1 else None)
     N, D, d = model.X.shape[0], model.D, model.d
     P_local = P_total // world
     alg, dense, executed = obs_kernel_flops(N, D)
