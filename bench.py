@@ -850,8 +850,16 @@ def main():
     libx = None
     if world > 1 and backend == "nccl" and args.library_steps > 0:
         if comm is None:
-            comm = library_comm(world, rank, local, group, device)
-        libx = library_exchange_line(new_filter, zs, min(args.steps, args.library_steps), dist, device, P_total)
+            try:
+                comm = library_comm(world, rank, local, group, device)
+            except Exception as e:  # noqa: BLE001
+                libx = {"exchange": "gpmdm_pf_set_comm", "error": repr(e)[:400]}
+        if comm is not None:
+            try:    # an error here is reported in the line, not in place of the headline
+                libx = library_exchange_line(new_filter, zs, min(args.steps, args.library_steps), dist, device,
+                                             P_total)
+            except Exception as e:  # noqa: BLE001
+                libx = {"exchange": "gpmdm_pf_set_comm", "error": repr(e)[:400]}
     if args.spread_steps is None:
         args.spread_steps = 30 if (args.config == 2 and args.stream == "mocap" and args.y_lambda == 1.0) else 0
     spread = (spread_line(device, args.spread_steps, y_lambda=args.spread_lambda, dyn_tiles=args.dyn_tiles)
