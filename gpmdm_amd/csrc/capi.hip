@@ -294,6 +294,15 @@ struct gpmdm_pf {
   size_t own_tmp_bytes = 0;
   bool own_valid = false;
   bool shard_order = true;            // gpmdm_pf_set_shard_order
+  // The order a resample installs depends only on (seed, frame), so the pre-switch computes
+  // the next resample's order into own_next / inv_next behind the read-out (the GPU's gap
+  // while the host takes the outputs); that resample swaps it in instead of computing it.
+  int* own_next = nullptr;
+  int* inv_next = nullptr;
+  long long own_next_frame = -1;     // the frame own_next was computed for (-1: none)
+  bool order_wanted() const {
+    return own && dedup && shard_order && resample_mode != GPMDM_RESAMPLE_SYSTEMATIC && uniform_order_supported(P);
+  }
   // Exchanged rows read in place (gpmdm_pf_unpack_part): the all-gathered {class, state} rows
   // are read by the resample's gathers through the ownership order (only the ancestors' rows
   // are ever touched) and the {ll} column by a launch inside the resample that also writes
@@ -460,7 +469,7 @@ struct gpmdm_pf {
                     pred_q, pred_mu, pred_mu_p, pred_out};
     for (double* p : ds) dfree(p);
     int* is[] = {cls, cls_new, perm, ridx, blockcounts, blockoff, small, obs_tab,
-                 slot, lflag, lblock, ltab, lperm, guide, own, own_inv, sys_mark, sys_block};
+                 slot, lflag, lblock, ltab, lperm, guide, own, own_inv, own_next, inv_next, sys_mark, sys_block};
     for (int* p : is) dfree(p);
     dfree(own_tmp);
     dfree(gmax);
@@ -834,6 +843,8 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
     pf->own_tmp_bytes = std::max<size_t>(uniform_order_temp_bytes(P), 1);
     ALLOC(own, P);
     ALLOC(own_inv, P);
+    ALLOC(own_next, P);
+    ALLOC(inv_next, P);
     ALLOC(own_tmp, pf->own_tmp_bytes);
   }
 #undef ALLOC
@@ -1984,12 +1995,18 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   // gathers that read this frame's rows through the current one; systematic uniforms rise
   // with the slot, so the identity order already groups the slots by ancestor
   pf->own_valid = false;
-  if (pf->own && pf->dedup && pf->shard_order && !sys && uniform_order_supported(pf->P)) {
-    if (launch_uniform_order(pf->P, pf->frame, pf->seed_lo, pf->seed_hi, pf->own, pf->own_inv, pf->own_tmp,
-                             pf->own_tmp_bytes, s) != 0)
+  if (pf->order_wanted()) {
+    if (pf->own_next_frame == (long long)pf->frame) {
+      // computed behind the last read-out (the kernels above already hold the old pointers)
+      std::swap(pf->own, pf->own_next);
+      std::swap(pf->own_inv, pf->inv_next);
+    } else if (launch_uniform_order(pf->P, pf->frame, pf->seed_lo, pf->seed_hi, pf->own, pf->own_inv, pf->own_tmp,
+                                    pf->own_tmp_bytes, s) != 0) {
       return fail(GPMDM_E_HIP, "ownership-order pass failed");
+    }
     pf->own_valid = true;
   }
+  pf->own_next_frame = -1;
   pf->mark_end(s, GPMDM_STAGE_RESAMPLE, t0);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(pf->ro_ev, s));
@@ -2001,6 +2018,14 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
     HIPCHK(hipEventRecord(pf->sw_ev, s));
     pf->sw_stream = s;
     pf->preswitched = true;
+    if (pf->order_wanted() && !std::getenv("GPMDM_NO_ORDER_AHEAD")) {
+      // the next resample's ownership order (its uniforms are keyed by the frame), after the
+      // event the switch's consumers wait on, so it never delays the switch
+      if (launch_uniform_order(pf->P, pf->frame, pf->seed_lo, pf->seed_hi, pf->own_next, pf->inv_next, pf->own_tmp,
+                               pf->own_tmp_bytes, s) != 0)
+        return fail(GPMDM_E_HIP, "ownership-order pass failed");
+      pf->own_next_frame = (long long)pf->frame;
+    }
   }
   return GPMDM_OK;
 }
