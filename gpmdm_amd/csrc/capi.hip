@@ -1200,7 +1200,7 @@ static TileGeo dyn_frame_geo(const gpmdm_pf* pf) {
   return TileGeo{g.nw, mt, g.ntw};
 }
 
-static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipStream_t s) {
+static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipStream_t s, bool order_ahead = false) {
   gpmdm_model* m = pf->m;
   const int C = m->C;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
@@ -1321,6 +1321,14 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
   }
   const bool small_path = launch_switch_group(sa, sc, ga, sa.owner ? &la : nullptr, !pf->owner_clean, s);
   if (sa.owner) pf->owner_clean = !small_path;   // the small path presets in-kernel, leaves it dirty
+  if (order_ahead) {
+    // (pre-switch) the next resample's ownership order: its uniforms are keyed by the
+    // frame, so it is known now; timed with the switch
+    if (launch_uniform_order(pf->P, pf->frame, pf->seed_lo, pf->seed_hi, pf->own_next, pf->inv_next, pf->own_tmp,
+                             pf->own_tmp_bytes, s) != 0)
+      return fail(GPMDM_E_HIP, "ownership-order pass failed");
+    pf->own_next_frame = (long long)pf->frame;
+  }
   pf->mark_end(s, GPMDM_STAGE_SWITCH, t0);
   HIPCHK(hipGetLastError());
   if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(0, s));
@@ -2014,18 +2022,11 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   pf->frame += 1;
   pf->propagated = false;
   if (pf->preswitch) {                 // the next frame's switch, behind the read-out
-    TRY(do_switch(pf, nullptr, nullptr, s));
+    static const bool no_ahead = std::getenv("GPMDM_NO_ORDER_AHEAD") != nullptr;   // A/B
+    TRY(do_switch(pf, nullptr, nullptr, s, pf->order_wanted() && !no_ahead));
     HIPCHK(hipEventRecord(pf->sw_ev, s));
     pf->sw_stream = s;
     pf->preswitched = true;
-    if (pf->order_wanted() && !std::getenv("GPMDM_NO_ORDER_AHEAD")) {
-      // the next resample's ownership order (its uniforms are keyed by the frame), after the
-      // event the switch's consumers wait on, so it never delays the switch
-      if (launch_uniform_order(pf->P, pf->frame, pf->seed_lo, pf->seed_hi, pf->own_next, pf->inv_next, pf->own_tmp,
-                               pf->own_tmp_bytes, s) != 0)
-        return fail(GPMDM_E_HIP, "ownership-order pass failed");
-      pf->own_next_frame = (long long)pf->frame;
-    }
   }
   return GPMDM_OK;
 }
