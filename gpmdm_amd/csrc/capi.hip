@@ -132,7 +132,16 @@ struct GpImage {
     s.coff = coff;
     return s;
   }
-  int n_parts() const { return (int)cdiv(n_rows + coff, geo.nb()); }   // blocks holding R columns
+  // Read-out partials (gp_tile.h epilogue): one per column block, or for the 4-wave shapes
+  // with 8 column tiles per wave (32 x 512) one per 256-column part, indexed as the 16 x 256
+  // image's blocks (front padding col_offset(n_cols, 256)) -- so both images' partials are
+  // the same numbers in the same slots.
+  bool split() const { return geo.nw == 4 && geo.ntw == 8; }
+  int pnb() const { return split() ? geo.nb() / 2 : geo.nb(); }
+  int pcoff() const { return split() ? col_offset(n_rows + n_m, pnb()) : coff; }
+  int n_parts() const { return (int)cdiv(n_rows + pcoff(), pnb()); }              // parts holding R columns
+  int n_pblocks() const { return (int)cdiv(n_rows + n_m + pcoff(), pnb()); }      // all parts
+  int jm0() const { return (n_rows + pcoff()) / pnb(); }                          // first part with mean columns
   int tiles(long long n) const { return (int)cdiv(n, geo.pt()); }
 };
 
@@ -219,10 +228,9 @@ static void model_release(gpmdm_model* m) {
 // The observation launch's image and shape for filters of P particles each (all ranks;
 // a bank: per filter) whose shard holds n rows.
 // * Small models (N <= kSmallObsN, d <= 12) and filters (P <= kSmallObsP): the 16 x 256
-//   image (model.obs_small).  Its column blocks differ from the default image's, so the
-//   per-block partial sums combine in another order: results agree to rounding, not bit
-//   for bit, and the choice depends on the per-filter P only (every rank of a sharded
-//   filter, and a bank and its filters run alone, make the same one).
+//   image (model.obs_small).  The default 32 x 512 image reduces each 256-column half of
+//   its blocks into its own partial in the 16 x 256 order (gp_tile.h epilogue), so the two
+//   give bitwise the same results (tests/test_gpu_small_path.py).
 //   GPMDM_OBS_IMAGE16=0 does not build the image.
 // * Otherwise, with fewer 32-row tiles than one per CU per column block, 16-row tiles over
 //   the same 32 x 512 image (the image's fragment layout depends on the waves and column
@@ -235,7 +243,9 @@ constexpr long long kSmallObsN = 1024, kSmallObsP = 1024;
 static int obs_parts_max(const gpmdm_model* m) {
   return std::max(m->obs.n_parts(), m->obs_small.Bf ? m->obs_small.n_parts() : 0);
 }
-static int obs_blocks_max(const gpmdm_model* m) { return std::max(m->obs.n_j, m->obs_small.n_j); }
+static int obs_blocks_max(const gpmdm_model* m) {
+  return std::max(m->obs.n_pblocks(), m->obs_small.Bf ? m->obs_small.n_pblocks() : 0);
+}
 static const GpImage& obs_pick(const gpmdm_model* m, long long P, long long n, TileGeo& geo) {
   if (m->obs_small.Bf && P <= kSmallObsP) {
     geo = m->obs_small.geo;
@@ -269,6 +279,7 @@ struct gpmdm_pf {
   bool dedup = true;                  // ancestor de-duplication of the dynamics GP
   int dyn_tiles = GPMDM_DYN_TILES_AUTO;   // gpmdm_pf_set_dyn_tiles
   bool wide_dyn() const { return dyn_tiles == GPMDM_DYN_TILES_WIDE || (dyn_tiles == GPMDM_DYN_TILES_AUTO && !dedup); }
+  bool dyn_wide_frame = false;        // this frame's dynamics image (set by the switch: dyn_frame_wide)
   // device state
   double *T = nullptr, *X = nullptr, *X_prop = nullptr, *ll = nullptr;
   int *cls = nullptr, *cls_new = nullptr, *perm = nullptr, *ridx = nullptr;
@@ -1187,9 +1198,23 @@ static void launch_dyn_gemm(gpmdm_pf* pf, hipStream_t s);
 // image (per rank, the last read frame's count; tools/dyn_family.sh).  GPMDM_DYN_MT=1|2|4
 // forces a height (A/B).
 constexpr int kDynMt2Rows = 1 << 30, kDynMt4Rows = 1 << 30;
+// Rows from which an AUTO de-duplicated pass runs on the wide image instead of the narrow
+// one -- only where the two give bitwise the same results (the 32 x 512 wide image reduces
+// each 256-column half in the 16 x 256 order: d <= 12), so the choice, made per rank from
+// its last read frame's rows, never changes a result.  GPMDM_DYN_WIDE_ROWS overrides (A/B).
+constexpr int kDynWideRows = 1 << 30;
+
+static bool dyn_frame_wide(const gpmdm_pf* pf) {
+  if (pf->dyn_tiles != GPMDM_DYN_TILES_AUTO || !pf->dedup) return pf->wide_dyn();
+  const gpmdm_model* m = pf->m;
+  if (m->dynw.empty() || !m->dynw[0].split() || m->dyn[0].geo.nw != 4 || m->dyn[0].geo.ntw != 4) return false;
+  static const char* env = std::getenv("GPMDM_DYN_WIDE_ROWS");
+  static const long long thr = env ? std::atoll(env) : kDynWideRows;
+  return pf->rows_hint >= thr;
+}
 
 static TileGeo dyn_frame_geo(const gpmdm_pf* pf) {
-  const TileGeo g = pf->m->dyn_set(pf->wide_dyn())[0].geo;
+  const TileGeo g = pf->m->dyn_set(pf->dyn_wide_frame)[0].geo;
   if (g.nw != kGeo16x256.nw || g.mt != kGeo16x256.mt || g.ntw != kGeo16x256.ntw) return g;
   static const char* env = std::getenv("GPMDM_DYN_MT");
   int mt = 1;
@@ -1239,6 +1264,7 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
     sa.hi = pf->hi;
   }
   sa.own = pf->own_order();
+  pf->dyn_wide_frame = dyn_frame_wide(pf);
   pf->dyn_geo_frame = dyn_frame_geo(pf);
   ScanArgs sc{};
   sc.nb = nbs;
@@ -1386,7 +1412,7 @@ static void launch_dyn_gemm(gpmdm_pf* pf, hipStream_t s) {
   gpmdm_model* m = pf->m;
   const int C = m->C, d = m->d;
   const long long nl = pf->nloc;
-  const std::vector<GpImage>& dset = m->dyn_set(pf->wide_dyn());
+  const std::vector<GpImage>& dset = m->dyn_set(pf->dyn_wide_frame);
   // Diagnostic (GPMDM_DYN_EXACT_GRID=1): read the leader tile counts back (a host sync)
   // and launch exactly the non-empty tiles instead of the device-unknown upper bound --
   // measures what the empty workgroups of the bound cost.  Not the production schedule.
@@ -1448,7 +1474,7 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
   }
   const long long nl = pf->nloc;
   if (nl > 0) {
-    const std::vector<GpImage>& dset = m->dyn_set(pf->wide_dyn());
+    const std::vector<GpImage>& dset = m->dyn_set(pf->dyn_wide_frame);
     if (!pf->gemm_ahead) launch_dyn_gemm(pf, s);   // (replay: launched by the switch already)
     pf->gemm_ahead = false;
     hipEvent_t t0;
@@ -1566,8 +1592,8 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     oa.qpart = pf->qobs;
     oa.ld_q = nl;
     oa.spart = pf->sobs;
-    oa.jm0 = (oi.n_rows + oi.coff) / oi.geo.nb();   // first block with mean columns
-    oa.n_j = oi.n_j;
+    oa.jm0 = oi.jm0();                   // first part with mean columns
+    oa.n_j = oi.n_pblocks();
     oa.sum_log_il2 = m->sum_log_il2;
     oa.z = zsrc;
     oa.Pf = pf->Pf;

@@ -142,10 +142,10 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   // group conflict; a lane-replicated table removes the conflicts and costs more in
   // address arithmetic than they cost, tile_bench)
   __shared__ double tab[64];
-  __shared__ double qred[NW][PT];
+  __shared__ double qred[(NW == 4 && NTW == 8) ? 2 : 1][NW][PT];   // per partial (epilogue)
   constexpr bool PLDS = (FLAGS & kTileCoordLDS) != 0;
   __shared__ double PA[PLDS ? PT : 1][PLDS ? DI + 1 : 1];
-  __shared__ double sred[NW][PT];
+  __shared__ double sred[(NW == 4 && NTW == 8) ? 2 : 1][NW][PT];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -427,10 +427,30 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
 
   // ---- epilogue --------------------------------------------------------------------
   // C/D layout of v_mfma_f64_16x16x4_f64: lane l, reg r -> row (l>>4) + 4r, col l&15.
-  const bool has_r = J * NB - coff < n_rows;
-  const bool has_m = (J + 1) * NB - coff > n_rows;            // block holds mean columns
+  // Read-out partials: one per block, or -- the 4-wave shapes with 8 column tiles per wave
+  // (32 x 512 and its 16-row form) -- one per 256-column half, each reduced exactly as the
+  // 16 x 256 shape reduces the block holding the same columns (wave w's tiles w, w + 4, ...
+  // of the half in order; lanes by xor 1, 2, 4, 8; waves in order) and stored at that
+  // block's index: the 32 x 512 and 16 x 256 images give bitwise the same outputs.
+  constexpr int NH = (NW == 4 && NTW == 8) ? 2 : 1;
+  constexpr int NTH = NTW / NH;
+  constexpr int HB = NB / NH;                                  // columns per partial
+  const int pcoff = NH == 2 ? col_offset(n_cols, HB) : coff;   // the partial blocks' front padding
+  int pj[NH];
+  bool hr[NH], hm[NH];
+  bool any_r = false, any_m = false;
+#pragma unroll
+  for (int h = 0; h < NH; ++h) {
+    const int c0 = J * NB + HB * h - coff;                     // first real column of the part
+    const bool real = c0 + HB > 0;                             // (a split block's first half
+    pj[h] = real ? (c0 + pcoff) / HB : 0;                      //  may be front padding only)
+    hr[h] = real && c0 < n_rows;
+    hm[h] = real && c0 + HB > n_rows;                          // holds mean columns
+    any_r = any_r || hr[h];
+    any_m = any_m || hm[h];
+  }
   const bool fused = prm.spart != nullptr;
-  if (has_m) {
+  if (any_m) {
     if (!fused) {
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
@@ -452,50 +472,53 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       // particles share one filter (always, for a single filter) reads z_j once per column.
       const int Pf = (int)prm.Pf;
       const int f0 = pos0 / Pf, f1 = (min(pos0 + PT, pos_end) - 1) / Pf;   // wave-uniform
-      double ss[MT][4];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int h = 0; h < NH; ++h) {                          // one part at a time (registers)
+        double ss[MT][4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ss[mt][r] = 0.0;
+        for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) {
-        const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
-        if (jm >= 0 && jm < n_m) {
-          const double lam = prm.lam2[jm];
-          if (f0 == f1) {
-            const double zj = prm.z[(long long)f0 * n_m + jm];
+          for (int r = 0; r < 4; ++r) ss[mt][r] = 0.0;
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+        for (int nt = h * NTH; nt < (h + 1) * NTH; ++nt) {
+          const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
+          if (jm >= 0 && jm < n_m) {
+            const double lam = prm.lam2[jm];
+            if (f0 == f1) {
+              const double zj = prm.z[(long long)f0 * n_m + jm];
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const double t = zj - acc[mt][nt][r];
-                ss[mt][r] = fma(t * t, lam, ss[mt][r]);
-              }
-          } else {
+              for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-            for (int mt = 0; mt < MT; ++mt)
+                for (int r = 0; r < 4; ++r) {
+                  const double t = zj - acc[mt][nt][r];
+                  ss[mt][r] = fma(t * t, lam, ss[mt][r]);
+                }
+            } else {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                int p = pos0 + mt * 16 + lk + 4 * r;
-                p = p < pos_end ? p : pos0;
-                const double zz = prm.z[(long long)(p / Pf) * n_m + jm];
-                const double t = zz - acc[mt][nt][r];
-                ss[mt][r] = fma(t * t, lam, ss[mt][r]);
-              }
+              for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  int p = pos0 + mt * 16 + lk + 4 * r;
+                  p = p < pos_end ? p : pos0;
+                  const double zz = prm.z[(long long)(p / Pf) * n_m + jm];
+                  const double t = zz - acc[mt][nt][r];
+                  ss[mt][r] = fma(t * t, lam, ss[mt][r]);
+                }
+            }
           }
         }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            double v = ss[mt][r];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            if (li == 0) sred[h][w][mt * 16 + lk + 4 * r] = v;
+          }
       }
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          double v = ss[mt][r];
-          v += __shfl_xor(v, 1);
-          v += __shfl_xor(v, 2);
-          v += __shfl_xor(v, 4);
-          v += __shfl_xor(v, 8);
-          if (li == 0) sred[w][mt * 16 + lk + 4 * r] = v;
-        }
     }
     // mean columns do not enter the quadratic form
 #pragma unroll
@@ -507,46 +530,53 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       }
     }
   }
-  if (has_r) {
-    // Sum of squares over the block's R columns.  Front-padding columns (col < 0) have
+  if (any_r) {
+    // Sum of squares over the part's R columns.  Front-padding columns (col < 0) have
     // B = 0, so V = 0 there: no mask (mean columns were zeroed above).
-    double qs[MT][4];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double v = 0.0;
-#pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) v = fma(acc[mt][nt][r], acc[mt][nt][r], v);
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        qs[mt][r] = v;
-      }
-    if (li == 0) {
+    for (int h = 0; h < NH; ++h) {
+      if (!hr[h]) continue;
+      double qs[MT][4];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) qred[w][mt * 16 + lk + 4 * r] = qs[mt][r];
+        for (int r = 0; r < 4; ++r) {
+          double v = 0.0;
+#pragma unroll
+          for (int nt = h * NTH; nt < (h + 1) * NTH; ++nt) v = fma(acc[mt][nt][r], acc[mt][nt][r], v);
+          v += __shfl_xor(v, 1);
+          v += __shfl_xor(v, 2);
+          v += __shfl_xor(v, 4);
+          v += __shfl_xor(v, 8);
+          qs[mt][r] = v;
+        }
+      if (li == 0) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) qred[h][w][mt * 16 + lk + 4 * r] = qs[mt][r];
+      }
     }
   }
-  if (has_r || (has_m && fused)) {
+  if (any_r || (any_m && fused)) {
     __syncthreads();
     if (tid < PT) {
       const int p = pos0 + tid;
       if (p < pos_end) {
-        if (has_r) {
-          double q = 0.0;
 #pragma unroll
-          for (int ww = 0; ww < NW; ++ww) q += qred[ww][tid];
-          prm.qpart[(long long)J * prm.ld_q + out_base + p] = q;
-        }
-        if (has_m && fused) {
-          double sm = 0.0;
+        for (int h = 0; h < NH; ++h) {
+          if (hr[h]) {
+            double q = 0.0;
 #pragma unroll
-          for (int ww = 0; ww < NW; ++ww) sm += sred[ww][tid];
-          prm.spart[(long long)J * prm.ld_q + out_base + p] = sm;
+            for (int ww = 0; ww < NW; ++ww) q += qred[h][ww][tid];
+            prm.qpart[(long long)pj[h] * prm.ld_q + out_base + p] = q;
+          }
+          if (hm[h] && fused) {
+            double sm = 0.0;
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) sm += sred[h][ww][tid];
+            prm.spart[(long long)pj[h] * prm.ld_q + out_base + p] = sm;
+          }
         }
       }
     }
@@ -561,7 +591,9 @@ void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
   // model): particle coordinates from LDS (VAR bit 17) -- in VGPRs they push the
   // 2-workgroup register budget into spills (config-5 shape, d = 16: 850 ms per launch vs
   // 1037 ms; the default 64 x 512 shape: 760 ms; profiles/r02/ablations/tb9, tb10)
-  constexpr int kCoordVar = DI > 12 ? kTileCoordLDS : 0;
+  // (d = 11, 12: the split-partial epilogue tipped the 256-VGPR budget into spills in the K
+  // loop; LDS coordinates free 2 d VGPRs and keep the results bitwise)
+  constexpr int kCoordVar = DI > 10 ? kTileCoordLDS : 0;
   if (dyn) {
     // A/B shapes for the dynamics GPs (GPMDM_DYN_GEO / GPMDM_DYNW_GEO, capi.hip; d <= 8):
     // 32 x 1024 (8 waves), 16 x 512, 16 x 1024 (4 waves x 16 column tiles)

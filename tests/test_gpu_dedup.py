@@ -4,9 +4,10 @@ Offspring of one resampling ancestor hold bit-identical states, so the dynamics 
 (gpmdm.py:1032-1068) is evaluated once per distinct (ancestor, new class) key.  The bar is
 bitwise identity with the undeduplicated path (every particle evaluated, as the
 reference's _propogate_dynamics does, gpmdm_pf.py:153-168) for states, classes,
-log-likelihoods and resample indices, frame after frame (both filters on the same
-dynamics tile shape: the default picks wide tiles without de-duplication, which differ
-only in summation order -- test_wide_dynamics_tiles_vs_narrow).
+log-likelihoods and resample indices, frame after frame (for d <= 12 the default's wide
+tiles without de-duplication are bitwise the narrow ones -- test_wide_dynamics_tiles_vs_narrow;
+for d > 12 the 64 x 512 wide image differs from the narrow one in summation order, so the
+identity tests pin both filters to one shape).
 """
 import numpy as np
 import pytest
@@ -106,8 +107,9 @@ def test_dedup_bank(m2):
 def test_wide_dynamics_tiles_vs_narrow(m2, fx_config2):
     """dedup=False runs the dynamics GP on the wide (observation-GP-shaped) tile image by
     default: one resynced step from the same particles and draws as the narrow tiles and as
-    the oracle -- states within 1e-12 of the narrow path (summation order only), everything
-    against the oracle at the parity tolerances."""
+    the oracle -- bitwise the narrow path (the 32 x 512 kernel reduces each 256-column half
+    of its blocks in the 16 x 256 order, gp_tile.h), everything against the oracle at the
+    parity tolerances."""
     from conftest import assert_step_matches, oracle_model
     from gpmdm_amd import GPMDM_PF
     from oracle import gpmdm_oracle as O
@@ -128,8 +130,8 @@ def test_wide_dynamics_tiles_vs_narrow(m2, fx_config2):
         pf.update_with_draws(Y[31], E, nrm, u)
         out[tiles] = (pf.export_state(), pf.class_probabilities().numpy(), pf.current_state_mean().numpy())
     a, b = out["narrow"][0], out["wide"][0]
-    same = a["resample_idx"] == b["resample_idx"]
-    assert int((~same).sum()) <= 2
-    assert np.max(np.abs(a["states"][same] - b["states"][same])) <= 1e-12 * np.max(np.abs(a["states"]))
+    for key in ("states", "classes", "ll", "w", "resample_idx"):
+        assert np.array_equal(a[key], b[key]), key
+    assert np.array_equal(out["narrow"][1], out["wide"][1]) and np.array_equal(out["narrow"][2], out["wide"][2])
     r = O.step(om, T, st0["states"], st0["classes"], Y[31], E, nrm, u)
     assert_step_matches(b, r, out["wide"][1], out["wide"][2], u, what="wide")

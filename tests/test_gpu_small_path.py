@@ -5,7 +5,8 @@ path (GPMDM_NO_SMALL_PATH=1), the observation GP's 16-row tiles (capi.hip obs_ru
 are bitwise its 32-row tiles, and a small replay filter's class counts computed on the host
 (no mid-frame sync) are the device's (GPMDM_NO_HOST_COUNTS=1), and a Philox filter whose
 next switch the resample launches ahead (pre-switch) is bitwise one that switches in the next
-update (GPMDM_NO_PRESWITCH=1), with predict / dynamics_rows / export between frames: replay and Philox draws, multinomial and systematic
+update (GPMDM_NO_PRESWITCH=1), and de-duplicated dynamics passes on the wide image
+(GPMDM_DYN_WIDE_ROWS=0), with predict / dynamics_rows / export between frames: replay and Philox draws, multinomial and systematic
 resampling, with and without ancestor de-duplication, a bank of filters, several frames.
 The environment switches are read once per process, so each configuration runs in its own
 child process (one at a time)."""
@@ -89,12 +90,16 @@ def test_small_path_is_bitwise_the_multi_kernel_path(tmp_path):
     devcounts = _run(tmp_path, "devcounts", {"GPMDM_NO_HOST_COUNTS": "1"})
     # Philox filters' next switch launched by the resample (pre-switch) or by the next update
     nopre = _run(tmp_path, "nopre", {"GPMDM_NO_PRESWITCH": "1"})
-    assert fused.keys() == multi.keys() == tiles16.keys() == devcounts.keys() == nopre.keys()
+    # de-duplicated dynamics passes on the wide 32 x 512 image every frame instead of the
+    # narrow 16 x 256 one (capi.hip dyn_frame_wide: the two are bitwise the same at d <= 12)
+    widedyn = _run(tmp_path, "widedyn", {"GPMDM_DYN_WIDE_ROWS": "0"})
+    assert fused.keys() == multi.keys() == tiles16.keys() == devcounts.keys() == nopre.keys() == widedyn.keys()
     for k in fused:
         assert np.array_equal(fused[k], multi[k]), k
         assert np.array_equal(fused[k], tiles16[k]), k
         assert np.array_equal(fused[k], devcounts[k]), k
         assert np.array_equal(fused[k], nopre[k]), k
+        assert np.array_equal(fused[k], widedyn[k]), k
 
 
 def test_deferred_likelihood_is_flushed_for_an_early_reader():
@@ -162,9 +167,9 @@ np.savez(sys.argv[1], **out)
 @pytest.mark.timeout(600)
 def test_small_observation_image_matches_the_default_image(tmp_path):
     """Small models and filters run the observation GP over a 16 x 256 image (capi.hip
-    obs_pick): its column blocks partition the sums differently, so the filter agrees with
-    the 32 x 512 image to rounding (not bit for bit) -- same classes and resampling
-    indices, states and read-outs to 1e-9 -- on the config-1 model (N = 500)."""
+    obs_pick); the 32 x 512 kernel reduces each 256-column half of its blocks into its own
+    partial in the 16 x 256 order (gp_tile.h), so the filter is bitwise the same on either
+    image -- every export and read-out -- on the config-1 model (N = 500)."""
     def run(tag, env_extra):
         env = dict(os.environ, **env_extra)
         path = tmp_path / f"{tag}.npz"
@@ -176,9 +181,4 @@ def test_small_observation_image_matches_the_default_image(tmp_path):
     default = run("image32", {"GPMDM_OBS_IMAGE16": "0"})
     assert small.keys() == default.keys()
     for k in small:
-        if k.endswith(("classes", "resample_idx")):
-            assert np.array_equal(small[k], default[k]), k
-        elif k.endswith("_ll"):
-            np.testing.assert_allclose(small[k], default[k], rtol=1e-9, atol=1e-9, err_msg=k)
-        else:
-            np.testing.assert_allclose(small[k], default[k], rtol=1e-9, atol=1e-12, err_msg=k)
+        assert np.array_equal(small[k], default[k]), k
