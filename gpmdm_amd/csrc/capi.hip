@@ -111,6 +111,7 @@ constexpr long long kHostCountsMaxP = 1024;
 // dynamics GPs) in MFMA-fragment order -- layout and packing in host_image.h.
 struct GpImage {
   int n_rows = 0, n_m = 0, n_j = 0, coff = 0;
+  bool dyn = false;       // a dynamics GP's image (linear-kernel rows H)
   TileGeo geo = kGeo64x256;
   double* Xrec = nullptr; // row_cap(n_rows) x (d + 1) row records (host_image.h)
   double* Hf = nullptr;   // dynamics only
@@ -132,11 +133,11 @@ struct GpImage {
     s.coff = coff;
     return s;
   }
-  // Read-out partials (gp_tile.h epilogue): one per column block, or for the 4-wave shapes
-  // with 8 column tiles per wave (32 x 512) one per 256-column part, indexed as the 16 x 256
-  // image's blocks (front padding col_offset(n_cols, 256)) -- so both images' partials are
-  // the same numbers in the same slots.
-  bool split() const { return geo.nw == 4 && geo.ntw == 8; }
+  // Read-out partials (gp_tile.h epilogue): one per column block, or for the dynamics GP's
+  // wide shape (4 waves x 8 column tiles: 32 x 512) one per 256-column part, indexed as the
+  // 16 x 256 image's blocks (front padding col_offset(n_cols, 256)) -- so the narrow and wide
+  // dynamics images' partials are the same numbers in the same slots.
+  bool split() const { return dyn && geo.nw == 4 && geo.ntw == 8; }
   int pnb() const { return split() ? geo.nb() / 2 : geo.nb(); }
   int pcoff() const { return split() ? col_offset(n_rows + n_m, pnb()) : coff; }
   int n_parts() const { return (int)cdiv(n_rows + pcoff(), pnb()); }              // parts holding R columns
@@ -156,6 +157,7 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
                 const double* lin_c2, const double* R, const double* M, TileGeo geo) {
   const ImagePacker pk(n_rows, d, n_m, X, ls, lin_c2, R, M, geo);
   g.geo = geo;
+  g.dyn = lin_c2 != nullptr;
   g.n_rows = n_rows;
   g.n_m = n_m;
   g.coff = pk.coff;
@@ -228,9 +230,12 @@ static void model_release(gpmdm_model* m) {
 // The observation launch's image and shape for filters of P particles each (all ranks;
 // a bank: per filter) whose shard holds n rows.
 // * Small models (N <= kSmallObsN, d <= 12) and filters (P <= kSmallObsP): the 16 x 256
-//   image (model.obs_small).  The default 32 x 512 image reduces each 256-column half of
-//   its blocks into its own partial in the 16 x 256 order (gp_tile.h epilogue), so the two
-//   give bitwise the same results (tests/test_gpu_small_path.py).
+//   image (model.obs_small).  Its column blocks differ from the default image's, so the
+//   per-block partial sums combine in another order: results agree to rounding, not bit
+//   for bit, and the choice depends on the per-filter P only (every rank of a sharded
+//   filter, and a bank and its filters run alone, make the same one).  (Splitting the
+//   default image's partials as the dynamics images do would make them bitwise, at 0.5% of
+//   the d = 3 observation launch: gp_tile.h.)
 //   GPMDM_OBS_IMAGE16=0 does not build the image.
 // * Otherwise, with fewer 32-row tiles than one per CU per column block, 16-row tiles over
 //   the same 32 x 512 image (the image's fragment layout depends on the waves and column
@@ -1202,7 +1207,7 @@ constexpr int kDynMt2Rows = 1 << 30, kDynMt4Rows = 1 << 30;
 // one -- only where the two give bitwise the same results (the 32 x 512 wide image reduces
 // each 256-column half in the 16 x 256 order: d <= 12), so the choice, made per rank from
 // its last read frame's rows, never changes a result.  GPMDM_DYN_WIDE_ROWS overrides (A/B).
-constexpr int kDynWideRows = 1 << 30;
+constexpr int kDynWideRows = 32768;   // ~equal at 25k rows, wide 5% ahead at 100k (profiles/r04/dyn)
 
 static bool dyn_frame_wide(const gpmdm_pf* pf) {
   if (pf->dyn_tiles != GPMDM_DYN_TILES_AUTO || !pf->dedup) return pf->wide_dyn();

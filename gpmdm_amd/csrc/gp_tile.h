@@ -142,10 +142,12 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   // group conflict; a lane-replicated table removes the conflicts and costs more in
   // address arithmetic than they cost, tile_bench)
   __shared__ double tab[64];
-  __shared__ double qred[(NW == 4 && NTW == 8) ? 2 : 1][NW][PT];   // per partial (epilogue)
+  // read-out partials per block, or per 256-column half for the wide dynamics shape (epilogue)
+  constexpr int NHS = (DYN && NW == 4 && NTW == 8) ? 2 : 1;
+  __shared__ double qred[NHS * NW][PT];
   constexpr bool PLDS = (FLAGS & kTileCoordLDS) != 0;
   __shared__ double PA[PLDS ? PT : 1][PLDS ? DI + 1 : 1];
-  __shared__ double sred[(NW == 4 && NTW == 8) ? 2 : 1][NW][PT];
+  __shared__ double sred[NHS * NW][PT];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -426,77 +428,64 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   }
 
   // ---- epilogue --------------------------------------------------------------------
-  // C/D layout of v_mfma_f64_16x16x4_f64: lane l, reg r -> row (l>>4) + 4r, col l&15.
-  // Read-out partials: one per block, or -- the 4-wave shapes with 8 column tiles per wave
-  // (32 x 512 and its 16-row form) -- one per 256-column half, each reduced exactly as the
-  // 16 x 256 shape reduces the block holding the same columns (wave w's tiles w, w + 4, ...
-  // of the half in order; lanes by xor 1, 2, 4, 8; waves in order) and stored at that
-  // block's index: the 32 x 512 and 16 x 256 images give bitwise the same outputs.
-  constexpr int NH = (NW == 4 && NTW == 8) ? 2 : 1;
-  constexpr int NTH = NTW / NH;
-  constexpr int HB = NB / NH;                                  // columns per partial
-  const int pcoff = NH == 2 ? col_offset(n_cols, HB) : coff;   // the partial blocks' front padding
-  int pj[NH];
-  bool hr[NH], hm[NH];
-  bool any_r = false, any_m = false;
-#pragma unroll
-  for (int h = 0; h < NH; ++h) {
-    const int c0 = J * NB + HB * h - coff;                     // first real column of the part
-    const bool real = c0 + HB > 0;                             // (a split block's first half
-    pj[h] = real ? (c0 + pcoff) / HB : 0;                      //  may be front padding only)
-    hr[h] = real && c0 < n_rows;
-    hm[h] = real && c0 + HB > n_rows;                          // holds mean columns
-    any_r = any_r || hr[h];
-    any_m = any_m || hm[h];
-  }
-  const bool fused = prm.spart != nullptr;
-  if (any_m) {
-    if (!fused) {
-#pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) {
-        const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
-        if (jm >= 0 && jm < n_m) {
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int p = pos0 + mt * 16 + lk + 4 * r;
-              if (p < pos_end)
-                prm.mu[(long long)(out_base + p) * prm.ld_mu + jm] = acc[mt][nt][r];
-            }
+  // Read-out partials.  The dynamics GP's wide shape (4 waves x 8 column tiles: 32 x 512 and
+  // its 16-row form) reduces each 256-column half of a block into its own partial in the
+  // 16 x 256 shape's order, so the narrow and wide dynamics images give bitwise the same
+  // outputs (tests/test_gpu_small_path.py, test_gpu_dedup.py); every other shape writes one
+  // partial per block.  (The observation GP keeps one partial per block: the split moved
+  // the d = 3 observation tile's register allocation and cost 0.5% of its launch time,
+  // profiles/r04/split_epilogue_ab.txt.)
+  constexpr int NH = NHS;
+  if constexpr (NH == 1) {
+    // C/D layout of v_mfma_f64_16x16x4_f64: lane l, reg r -> row (l>>4) + 4r, col l&15.
+    const bool has_r = J * NB - coff < n_rows;
+    const bool has_m = (J + 1) * NB - coff > n_rows;            // block holds mean columns
+    const bool fused = prm.spart != nullptr;
+    if (has_m) {
+      if (!fused) {
+  #pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
+          const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
+          if (jm >= 0 && jm < n_m) {
+  #pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int p = pos0 + mt * 16 + lk + 4 * r;
+                if (p < pos_end)
+                  prm.mu[(long long)(out_base + p) * prm.ld_mu + jm] = acc[mt][nt][r];
+              }
+          }
         }
-      }
-    } else {
-      // sum_j (z_j - mu_j)^2 lam2_j over this block's mean columns (gpmdm_pf.py:188-192 with
-      // var_j = vc / lam2_j factored out; k_obs_ll finishes the likelihood).  A tile whose
-      // particles share one filter (always, for a single filter) reads z_j once per column.
-      const int Pf = (int)prm.Pf;
-      const int f0 = pos0 / Pf, f1 = (min(pos0 + PT, pos_end) - 1) / Pf;   // wave-uniform
-#pragma unroll
-      for (int h = 0; h < NH; ++h) {                          // one part at a time (registers)
+      } else {
+        // sum_j (z_j - mu_j)^2 lam2_j over this block's mean columns (gpmdm_pf.py:188-192 with
+        // var_j = vc / lam2_j factored out; k_obs_ll finishes the likelihood).  A tile whose
+        // particles share one filter (always, for a single filter) reads z_j once per column.
+        const int Pf = (int)prm.Pf;
+        const int f0 = pos0 / Pf, f1 = (min(pos0 + PT, pos_end) - 1) / Pf;   // wave-uniform
         double ss[MT][4];
-#pragma unroll
+  #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
+  #pragma unroll
           for (int r = 0; r < 4; ++r) ss[mt][r] = 0.0;
-#pragma unroll
-        for (int nt = h * NTH; nt < (h + 1) * NTH; ++nt) {
+  #pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
           const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
           if (jm >= 0 && jm < n_m) {
             const double lam = prm.lam2[jm];
             if (f0 == f1) {
               const double zj = prm.z[(long long)f0 * n_m + jm];
-#pragma unroll
+  #pragma unroll
               for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
+  #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                   const double t = zj - acc[mt][nt][r];
                   ss[mt][r] = fma(t * t, lam, ss[mt][r]);
                 }
             } else {
-#pragma unroll
+  #pragma unroll
               for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
+  #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                   int p = pos0 + mt * 16 + lk + 4 * r;
                   p = p < pos_end ? p : pos0;
@@ -507,43 +496,39 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
             }
           }
         }
-#pragma unroll
+  #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
+  #pragma unroll
           for (int r = 0; r < 4; ++r) {
             double v = ss[mt][r];
             v += __shfl_xor(v, 1);
             v += __shfl_xor(v, 2);
             v += __shfl_xor(v, 4);
             v += __shfl_xor(v, 8);
-            if (li == 0) sred[h][w][mt * 16 + lk + 4 * r] = v;
+            if (li == 0) sred[w][mt * 16 + lk + 4 * r] = v;
           }
       }
-    }
-    // mean columns do not enter the quadratic form
-#pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-      const int col = J * NB + 16 * (NW * nt + w) + li - coff;
-      if (col >= n_rows) {
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = (d4){0.0, 0.0, 0.0, 0.0};
+      // mean columns do not enter the quadratic form
+  #pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int col = J * NB + 16 * (NW * nt + w) + li - coff;
+        if (col >= n_rows) {
+  #pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = (d4){0.0, 0.0, 0.0, 0.0};
+        }
       }
     }
-  }
-  if (any_r) {
-    // Sum of squares over the part's R columns.  Front-padding columns (col < 0) have
-    // B = 0, so V = 0 there: no mask (mean columns were zeroed above).
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      if (!hr[h]) continue;
+    if (has_r) {
+      // Sum of squares over the block's R columns.  Front-padding columns (col < 0) have
+      // B = 0, so V = 0 there: no mask (mean columns were zeroed above).
       double qs[MT][4];
-#pragma unroll
+  #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
+  #pragma unroll
         for (int r = 0; r < 4; ++r) {
           double v = 0.0;
-#pragma unroll
-          for (int nt = h * NTH; nt < (h + 1) * NTH; ++nt) v = fma(acc[mt][nt][r], acc[mt][nt][r], v);
+  #pragma unroll
+          for (int nt = 0; nt < NTW; ++nt) v = fma(acc[mt][nt][r], acc[mt][nt][r], v);
           v += __shfl_xor(v, 1);
           v += __shfl_xor(v, 2);
           v += __shfl_xor(v, 4);
@@ -551,31 +536,183 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
           qs[mt][r] = v;
         }
       if (li == 0) {
-#pragma unroll
+  #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) qred[h][w][mt * 16 + lk + 4 * r] = qs[mt][r];
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) qred[w][mt * 16 + lk + 4 * r] = qs[mt][r];
       }
     }
-  }
-  if (any_r || (any_m && fused)) {
-    __syncthreads();
-    if (tid < PT) {
-      const int p = pos0 + tid;
-      if (p < pos_end) {
-#pragma unroll
-        for (int h = 0; h < NH; ++h) {
-          if (hr[h]) {
+    if (has_r || (has_m && fused)) {
+      __syncthreads();
+      if (tid < PT) {
+        const int p = pos0 + tid;
+        if (p < pos_end) {
+          if (has_r) {
             double q = 0.0;
-#pragma unroll
-            for (int ww = 0; ww < NW; ++ww) q += qred[h][ww][tid];
-            prm.qpart[(long long)pj[h] * prm.ld_q + out_base + p] = q;
+  #pragma unroll
+            for (int ww = 0; ww < NW; ++ww) q += qred[ww][tid];
+            prm.qpart[(long long)J * prm.ld_q + out_base + p] = q;
           }
-          if (hm[h] && fused) {
+          if (has_m && fused) {
             double sm = 0.0;
-#pragma unroll
-            for (int ww = 0; ww < NW; ++ww) sm += sred[h][ww][tid];
-            prm.spart[(long long)pj[h] * prm.ld_q + out_base + p] = sm;
+  #pragma unroll
+            for (int ww = 0; ww < NW; ++ww) sm += sred[ww][tid];
+            prm.spart[(long long)J * prm.ld_q + out_base + p] = sm;
+          }
+        }
+      }
+    }
+  } else {
+    // C/D layout of v_mfma_f64_16x16x4_f64: lane l, reg r -> row (l>>4) + 4r, col l&15.
+    // Read-out partials: one per block, or -- the 4-wave shapes with 8 column tiles per wave
+    // (32 x 512 and its 16-row form) -- one per 256-column half, each reduced exactly as the
+    // 16 x 256 shape reduces the block holding the same columns (wave w's tiles w, w + 4, ...
+    // of the half in order; lanes by xor 1, 2, 4, 8; waves in order) and stored at that
+    // block's index: the 32 x 512 and 16 x 256 images give bitwise the same outputs.
+    constexpr int NTH = NTW / NH;
+    constexpr int HB = NB / NH;                                  // columns per partial
+    const int pcoff = NH == 2 ? col_offset(n_cols, HB) : coff;   // the partial blocks' front padding
+    int pj[NH];
+    bool hr[NH], hm[NH];
+    bool any_r = false, any_m = false;
+  #pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      const int c0 = J * NB + HB * h - coff;                     // first real column of the part
+      const bool real = c0 + HB > 0;                             // (a split block's first half
+      pj[h] = real ? (c0 + pcoff) / HB : 0;                      //  may be front padding only)
+      hr[h] = real && c0 < n_rows;
+      hm[h] = real && c0 + HB > n_rows;                          // holds mean columns
+      any_r = any_r || hr[h];
+      any_m = any_m || hm[h];
+    }
+    const bool fused = prm.spart != nullptr;
+    if (any_m) {
+      if (!fused) {
+  #pragma unroll
+        for (int nt = 0; nt < NTW; ++nt) {
+          const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
+          if (jm >= 0 && jm < n_m) {
+  #pragma unroll
+            for (int mt = 0; mt < MT; ++mt)
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int p = pos0 + mt * 16 + lk + 4 * r;
+                if (p < pos_end)
+                  prm.mu[(long long)(out_base + p) * prm.ld_mu + jm] = acc[mt][nt][r];
+              }
+          }
+        }
+      } else {
+        // sum_j (z_j - mu_j)^2 lam2_j over this block's mean columns (gpmdm_pf.py:188-192 with
+        // var_j = vc / lam2_j factored out; k_obs_ll finishes the likelihood).  A tile whose
+        // particles share one filter (always, for a single filter) reads z_j once per column.
+        const int Pf = (int)prm.Pf;
+        const int f0 = pos0 / Pf, f1 = (min(pos0 + PT, pos_end) - 1) / Pf;   // wave-uniform
+  #pragma unroll
+        for (int h = 0; h < NH; ++h) {                          // one part at a time (registers)
+          double ss[MT][4];
+  #pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) ss[mt][r] = 0.0;
+  #pragma unroll
+          for (int nt = h * NTH; nt < (h + 1) * NTH; ++nt) {
+            const int jm = J * NB + 16 * (NW * nt + w) + li - coff - n_rows;
+            if (jm >= 0 && jm < n_m) {
+              const double lam = prm.lam2[jm];
+              if (f0 == f1) {
+                const double zj = prm.z[(long long)f0 * n_m + jm];
+  #pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+  #pragma unroll
+                  for (int r = 0; r < 4; ++r) {
+                    const double t = zj - acc[mt][nt][r];
+                    ss[mt][r] = fma(t * t, lam, ss[mt][r]);
+                  }
+              } else {
+  #pragma unroll
+                for (int mt = 0; mt < MT; ++mt)
+  #pragma unroll
+                  for (int r = 0; r < 4; ++r) {
+                    int p = pos0 + mt * 16 + lk + 4 * r;
+                    p = p < pos_end ? p : pos0;
+                    const double zz = prm.z[(long long)(p / Pf) * n_m + jm];
+                    const double t = zz - acc[mt][nt][r];
+                    ss[mt][r] = fma(t * t, lam, ss[mt][r]);
+                  }
+              }
+            }
+          }
+  #pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              double v = ss[mt][r];
+              v += __shfl_xor(v, 1);
+              v += __shfl_xor(v, 2);
+              v += __shfl_xor(v, 4);
+              v += __shfl_xor(v, 8);
+              if (li == 0) sred[h * NW + w][mt * 16 + lk + 4 * r] = v;
+            }
+        }
+      }
+      // mean columns do not enter the quadratic form
+  #pragma unroll
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int col = J * NB + 16 * (NW * nt + w) + li - coff;
+        if (col >= n_rows) {
+  #pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[mt][nt] = (d4){0.0, 0.0, 0.0, 0.0};
+        }
+      }
+    }
+    if (any_r) {
+      // Sum of squares over the part's R columns.  Front-padding columns (col < 0) have
+      // B = 0, so V = 0 there: no mask (mean columns were zeroed above).
+  #pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        if (!hr[h]) continue;
+        double qs[MT][4];
+  #pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            double v = 0.0;
+  #pragma unroll
+            for (int nt = h * NTH; nt < (h + 1) * NTH; ++nt) v = fma(acc[mt][nt][r], acc[mt][nt][r], v);
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            v += __shfl_xor(v, 8);
+            qs[mt][r] = v;
+          }
+        if (li == 0) {
+  #pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+  #pragma unroll
+            for (int r = 0; r < 4; ++r) qred[h * NW + w][mt * 16 + lk + 4 * r] = qs[mt][r];
+        }
+      }
+    }
+    if (any_r || (any_m && fused)) {
+      __syncthreads();
+      if (tid < PT) {
+        const int p = pos0 + tid;
+        if (p < pos_end) {
+  #pragma unroll
+          for (int h = 0; h < NH; ++h) {
+            if (hr[h]) {
+              double q = 0.0;
+  #pragma unroll
+              for (int ww = 0; ww < NW; ++ww) q += qred[h * NW + ww][tid];
+              prm.qpart[(long long)pj[h] * prm.ld_q + out_base + p] = q;
+            }
+            if (hm[h] && fused) {
+              double sm = 0.0;
+  #pragma unroll
+              for (int ww = 0; ww < NW; ++ww) sm += sred[h * NW + ww][tid];
+              prm.spart[(long long)pj[h] * prm.ld_q + out_base + p] = sm;
+            }
           }
         }
       }
@@ -591,9 +728,7 @@ void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
   // model): particle coordinates from LDS (VAR bit 17) -- in VGPRs they push the
   // 2-workgroup register budget into spills (config-5 shape, d = 16: 850 ms per launch vs
   // 1037 ms; the default 64 x 512 shape: 760 ms; profiles/r02/ablations/tb9, tb10)
-  // (d = 11, 12: the split-partial epilogue tipped the 256-VGPR budget into spills in the K
-  // loop; LDS coordinates free 2 d VGPRs and keep the results bitwise)
-  constexpr int kCoordVar = DI > 10 ? kTileCoordLDS : 0;
+  constexpr int kCoordVar = DI > 12 ? kTileCoordLDS : 0;
   if (dyn) {
     // A/B shapes for the dynamics GPs (GPMDM_DYN_GEO / GPMDM_DYNW_GEO, capi.hip; d <= 8):
     // 32 x 1024 (8 waves), 16 x 512, 16 x 1024 (4 waves x 16 column tiles)

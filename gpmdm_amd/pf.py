@@ -40,8 +40,8 @@ every per-frame computation runs in the HIP library.  Extra keyword options:
   itself (``gpmdm_pf_set_comm``: both all-gathers on a library-owned stream, the first
   overlapping the observation GP), the native hosts' path -- no torch.distributed.
 * ``dyn_tiles`` (``'auto'``): tile shape of the dynamics-GP pass (``gpmdm_pf_set_dyn_tiles``):
-  narrow tiles for de-duplicated rows, wide ones when every particle is evaluated; the
-  shapes differ only in floating-point summation order.
+  narrow tiles for de-duplicated rows, wide ones when every particle is evaluated; for
+  d <= 12 the two are bitwise identical, above it they differ in summation order only.
 
 Reference quirks kept for parity: log variance counted twice in the
 log-likelihood, float32 ``ln 2pi``, non-recursive weights, read-outs pairing

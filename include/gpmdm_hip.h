@@ -289,9 +289,12 @@ int gpmdm_pf_dyn_rows(gpmdm_pf_t pf, int64_t* rows, void* stream);
 
 /* Tile shape of the dynamics-GP pass.  AUTO (default): narrow 16x256 tiles for the few
  * de-duplicated rows (short K loops), the observation GP's wide shape when every particle
- * is evaluated (dedup off: a throughput problem).  NARROW / WIDE force one; the two differ
- * only in floating-point summation order (the de-duplication test forces NARROW on both
- * filters to check bitwise identity).  Not between switch and propagate. */
+ * is evaluated (dedup off: a throughput problem).  NARROW / WIDE force one.  For d <= 12 the
+ * two are bitwise identical (the 32x512 wide tile reduces each 256-column half in the 16x256
+ * order), and AUTO may run a de-duplicated pass on the wide image when a rank's last read
+ * frame had many rows; above d = 12 the 64x512 wide shape differs in floating-point
+ * summation order (the de-duplication tests pin one shape).  Not between switch and
+ * propagate. */
 #define GPMDM_DYN_TILES_AUTO 0
 #define GPMDM_DYN_TILES_NARROW 1
 #define GPMDM_DYN_TILES_WIDE 2

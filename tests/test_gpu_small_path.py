@@ -167,9 +167,9 @@ np.savez(sys.argv[1], **out)
 @pytest.mark.timeout(600)
 def test_small_observation_image_matches_the_default_image(tmp_path):
     """Small models and filters run the observation GP over a 16 x 256 image (capi.hip
-    obs_pick); the 32 x 512 kernel reduces each 256-column half of its blocks into its own
-    partial in the 16 x 256 order (gp_tile.h), so the filter is bitwise the same on either
-    image -- every export and read-out -- on the config-1 model (N = 500)."""
+    obs_pick): its column blocks partition the sums differently, so the filter agrees with
+    the 32 x 512 image to rounding (not bit for bit) -- same classes and resampling
+    indices, states and read-outs to 1e-9 -- on the config-1 model (N = 500)."""
     def run(tag, env_extra):
         env = dict(os.environ, **env_extra)
         path = tmp_path / f"{tag}.npz"
@@ -181,4 +181,9 @@ def test_small_observation_image_matches_the_default_image(tmp_path):
     default = run("image32", {"GPMDM_OBS_IMAGE16": "0"})
     assert small.keys() == default.keys()
     for k in small:
-        assert np.array_equal(small[k], default[k]), k
+        if k.endswith(("classes", "resample_idx")):
+            assert np.array_equal(small[k], default[k]), k
+        elif k.endswith("_ll"):
+            np.testing.assert_allclose(small[k], default[k], rtol=1e-9, atol=1e-9, err_msg=k)
+        else:
+            np.testing.assert_allclose(small[k], default[k], rtol=1e-9, atol=1e-12, err_msg=k)
