@@ -58,6 +58,7 @@ _SIGS = {
     "gpmdm_pf_draw_buffers": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), POINTER(c_void_p)]),
     "gpmdm_pf_draws_free": (c_int, [c_void_p, c_int]),
     "gpmdm_pf_switch": (c_int, [c_void_p, _dp, _i64p, c_void_p]),
+    "gpmdm_pf_preswitch": (c_int, [c_void_p, _dp, c_void_p]),
     "gpmdm_pf_propagate": (c_int, [c_void_p, _dp, _dp, c_void_p]),
     "gpmdm_pf_propagate_dynamics": (c_int, [c_void_p, _dp, c_void_p]),
     "gpmdm_pf_weigh": (c_int, [c_void_p, _dp, c_void_p]),
@@ -93,6 +94,7 @@ _SIGS = {
     "gpmdm_rng_walk_create": (c_int, [c_void_p, c_int64, POINTER(c_void_p)]),
     "gpmdm_rng_walk_reset": (c_int, [c_void_p, c_void_p, c_int64]),
     "gpmdm_rng_walk_state": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "gpmdm_rng_walk_states": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "gpmdm_rng_walk_destroy": (c_int, [c_void_p]),
     "gpmdm_last_error": (c_char_p, []),
     "gpmdm_version": (c_char_p, []),

@@ -61,9 +61,36 @@ def build_c_host(force: bool = False, verbose: bool = False) -> Path:
     return C_HOST
 
 
+REPLAY_SRC = CSRC / "replay_draws.cpp"
+REPLAY_LIB = PKG / "libgpmdm_replay.so"
+
+
+def build_replay(force: bool = False, verbose: bool = False) -> Path:
+    """The replay draws' chunk runner (csrc/replay_draws.cpp): host C++ against libtorch_cpu
+    (torch's own CPU samplers), g++ with torch's headers and C++ ABI, rpath to torch/lib."""
+    import torch
+    tdir = Path(torch.__file__).resolve().parent
+    if not force and REPLAY_LIB.exists() and REPLAY_LIB.stat().st_mtime >= REPLAY_SRC.stat().st_mtime:
+        return REPLAY_LIB
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    tmp = REPLAY_LIB.with_suffix(".so.tmp")
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+           f"-I{tdir / 'include'}", f"-I{tdir / 'include' / 'torch' / 'csrc' / 'api' / 'include'}",
+           str(REPLAY_SRC), "-o", str(tmp), f"-L{tdir / 'lib'}", "-ltorch_cpu", "-lc10",
+           f"-Wl,-rpath,{tdir / 'lib'}"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, REPLAY_LIB)
+    return REPLAY_LIB
+
+
 def build(force: bool = False, verbose: bool = False) -> Path:
     lib = _build_lib(force, verbose)
     build_c_host(force, verbose)
+    build_replay(force, verbose)
     return lib
 
 

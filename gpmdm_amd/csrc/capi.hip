@@ -442,6 +442,12 @@ struct gpmdm_pf {
   bool preswitched = false;           // launched, not yet consumed by gpmdm_pf_switch
   hipEvent_t sw_ev = nullptr;         // after the pre-switch
   hipStream_t sw_stream = nullptr;
+  // Replay filters pre-switch on the caller's request (gpmdm_pf_preswitch: the next frame's
+  // Exp(1) draws are the caller's, drawn ahead on the host): the switch, its class counts into
+  // mapped memory (cnt_pin, cnt_done after them) and the dynamics-GP tiles, all behind the
+  // read-out.  gpmdm_pf_switch consumes it when handed the same E pointer.
+  const double* pre_E = nullptr;
+  bool pre_counts = false;            // the pre-switch's counts land in cnt_pin (cnt_done)
   hipEvent_t ro_ev = nullptr;         // after the last read-out (gpmdm_pf_read waits on it)
   bool ro_ev_ok = false;
   int* rows_last() const { return small + 504; }   // rows of the last dynamics pass
@@ -1068,6 +1074,7 @@ static int drop_preswitch(gpmdm_pf* pf, hipStream_t s, bool host_wait) {
     HIPCHK(hipStreamWaitEvent(s, pf->sw_ev, 0));
   pf->preswitched = false;
   pf->switched = false;
+  pf->gemm_ahead = pf->pre_counts = false;   // (a replay pre-switch's tiles are redone too)
   return GPMDM_OK;
 }
 
@@ -1230,7 +1237,10 @@ static TileGeo dyn_frame_geo(const gpmdm_pf* pf) {
   return TileGeo{g.nw, mt, g.ntw};
 }
 
-static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipStream_t s, bool order_ahead = false) {
+// counts_ahead (replay pre-switch): the class counts into mapped memory with cnt_done after
+// them, and the dynamics-GP tiles launched behind, without waiting.
+static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipStream_t s, bool order_ahead = false,
+                     bool counts_ahead = false) {
   gpmdm_model* m = pf->m;
   const int C = m->C;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
@@ -1324,7 +1334,7 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
     la.slot = pf->slot;
     la.owner_reset = pf->owner;        // restores the preset for the next election
   }
-  sc.counts_host = class_counts ? pf->cnt_dev : nullptr;   // the counts straight to the host
+  sc.counts_host = (class_counts || counts_ahead) ? pf->cnt_dev : nullptr;   // the counts straight to the host
   // the counts on the host (cls_pin): no wait for this switch
   // (GPMDM_NO_HOST_COUNTS=1: the device counts and the synchronisation, for A/B tests)
   static const bool no_host_counts = std::getenv("GPMDM_NO_HOST_COUNTS") != nullptr;
@@ -1363,7 +1373,15 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
   pf->mark_end(s, GPMDM_STAGE_SWITCH, t0);
   HIPCHK(hipGetLastError());
   if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(0, s));
-  if (host_counts) {
+  if (counts_ahead) {
+    HIPCHK(hipEventRecord(pf->cnt_done, s));
+    if (pf->nloc > 0) {
+      launch_dyn_gemm(pf, s);
+      HIPCHK(hipGetLastError());
+      pf->gemm_ahead = true;
+    }
+    pf->pre_counts = true;
+  } else if (host_counts) {
     HIPCHK(hipEventRecord(pf->cnt_ev, s));
     pf->cnt_check = true;
     for (int c = 0; c < C; ++c) class_counts[c] = pf->cnt_expect[c];
@@ -1396,18 +1414,46 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   if (!pf->initialised) return fail(GPMDM_E_STATE, "particle filter not initialised");
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipSetDevice(pf->m->device));
-  if (pf->preswitched) {               // launched by the last resample: consume it
+  if (pf->preswitched && pf->rng_mode == GPMDM_RNG_REPLAY && E != pf->pre_E)
+    TRY(drop_preswitch(pf, s, false));   // other draws than the pre-switch's: switch again
+  if (pf->preswitched) {               // launched by the last resample / gpmdm_pf_preswitch: consume it
     if (s != pf->sw_stream) HIPCHK(hipStreamWaitEvent(s, pf->sw_ev, 0));
     pf->preswitched = false;
-    if (class_counts) {
+    if (class_counts && pf->pre_counts) {
+      HIPCHK(hipEventSynchronize(pf->cnt_done));   // the counts, not the tiles behind them
+      for (int c = 0; c < pf->m->C; ++c) class_counts[c] = pf->cnt_pin[c];
+    } else if (class_counts) {
       int tmp[kMaxClasses];
       HIPCHK(hipMemcpyAsync(tmp, pf->counts(), sizeof(int) * pf->m->C, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       for (int c = 0; c < pf->m->C; ++c) class_counts[c] = tmp[c];
     }
+    pf->pre_counts = false;
     return GPMDM_OK;
   }
   return do_switch(pf, E, class_counts, s);
+}
+
+int gpmdm_pf_preswitch(gpmdm_pf_t pf, const double* E, void* stream) {
+  CHECK(pf, "null handle");
+  if (!pf->initialised) return fail(GPMDM_E_STATE, "particle filter not initialised");
+  if ((pf->switched && !pf->preswitched) || pf->dyn_done || pf->propagated)
+    return fail(GPMDM_E_STATE, "preswitch inside a step");
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(pf->m->device));
+  if (pf->rng_mode == GPMDM_RNG_PHILOX) {
+    if (pf->preswitched) return GPMDM_OK;   // (the resample's)
+    TRY(do_switch(pf, nullptr, nullptr, s));
+  } else {
+    CHECK(E, "replay mode needs the Exp(1) switch draws");
+    TRY(drop_preswitch(pf, s, false));   // an earlier pre-switch's draws are replaced
+    TRY(do_switch(pf, E, nullptr, s, false, pf->cnt_done != nullptr));
+    pf->pre_E = E;
+  }
+  HIPCHK(hipEventRecord(pf->sw_ev, s));
+  pf->sw_stream = s;
+  pf->preswitched = true;
+  return GPMDM_OK;
 }
 
 // The dynamics-GP tile launches of this rank's rows (per class, segments of at most kMaxSeg

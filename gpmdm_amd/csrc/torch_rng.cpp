@@ -152,6 +152,14 @@ int gpmdm_rng_walk_state(gpmdm_rng_walk_t w, int64_t draws, const uint8_t* cache
   return GPMDM_OK;
 }
 
+// gpmdm_rng_walk_state at n offsets, one state after the other in out (n x 5056 bytes).
+int gpmdm_rng_walk_states(gpmdm_rng_walk_t w, int64_t n, const int64_t* draws, const uint8_t* cache_from,
+                          uint8_t* out) {
+  CHECK(w && out && draws && n >= 0, "bad argument");
+  for (int64_t k = 0; k < n; ++k) TRY(gpmdm_rng_walk_state(w, draws[k], cache_from, out + k * GPMDM_TORCH_GEN_STATE_BYTES));
+  return GPMDM_OK;
+}
+
 int gpmdm_rng_walk_destroy(gpmdm_rng_walk_t w) {
   delete w;
   return GPMDM_OK;

@@ -51,6 +51,7 @@ post-resample classes/states with pre-resample weights, ``ll + log_w`` in the po
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -104,6 +105,7 @@ class GPMDM_PF:
             raise ValueError("resample must be 'multinomial' or 'systematic'")
         self._rng = rng
         self._draws = None                      # replay.FrameDraws (rng='torch'), made on first use
+        self._pre_sw = False                    # a replay pre-switch with the draws made ahead is pending
         self._resample_mode = resample
         self._group = process_group
         self._exchange_fn = exchange
@@ -298,6 +300,10 @@ class GPMDM_PF:
             dr, counts = self._draws, self._counts
             pE, pC, pN, pU = self._draw_ptr
             dr.switch()
+            if self._pre_sw and not dr.last_hit:
+                # the caller drew from the generator since the pre-switch: its E is stale
+                _lib.check(lib.gpmdm_pf_preswitch(h, pE, s), "preswitch")
+            self._pre_sw = False
             _lib.check(lib.gpmdm_pf_switch(h, pE, pC, s), "switch")
             for hp, sp in self._all()[1:]:      # devices=: every rank switches all P (replay)
                 _lib.check(lib.gpmdm_pf_switch(hp, pE, None, sp), "switch")
@@ -305,6 +311,11 @@ class GPMDM_PF:
             self._propagate(z, dr.N, s, pN)
             dr.resample()
             self._each("gpmdm_pf_resample", pU, what="resample")
+            if self._replay_preswitch() and dr.ahead_ready():
+                # the next frame's E is drawn ahead (it needs no device result): its switch and
+                # dynamics tiles go behind this read-out (gpmdm_pf_preswitch)
+                _lib.check(lib.gpmdm_pf_preswitch(h, pE, s), "preswitch")
+                self._pre_sw = True
         else:
             self._each("gpmdm_pf_switch", None, None, what="switch")
             self._propagate(z, None, s)
@@ -312,6 +323,12 @@ class GPMDM_PF:
         self._readout = None
 
     step = update    # north-star name (BASELINE.json): one filter step
+
+    def _replay_preswitch(self) -> bool:
+        """Replay filters whose draws are made ahead (ParallelFrameDraws), on one handle and
+        one rank, launch the next switch between frames (GPMDM_NO_PRESWITCH=1: not, A/B)."""
+        return (isinstance(self._draws, replay.ParallelFrameDraws) and not self._peers and self._world == 1
+                and not os.environ.get("GPMDM_NO_PRESWITCH"))
 
     def update_with_draws(self, z, exp_draws, normals, uniforms):
         """One update with explicit random draws in the reference's order (replay: see

@@ -152,6 +152,15 @@ class _Walk:
         self._lib.check(self._lib.load().gpmdm_rng_walk_state(self._h, int(draws), cf, out.data_ptr()), "rng walk")
         return out
 
+    def states(self, draws: np.ndarray, cache_from: Optional[np.ndarray] = None) -> np.ndarray:
+        """The states at every offset of ``draws`` (int64), one row each (n x STATE_BYTES)."""
+        draws = np.ascontiguousarray(draws, dtype=np.int64)
+        out = np.empty((draws.size, STATE_BYTES), dtype=np.uint8)
+        cf = None if cache_from is None else cache_from.ctypes.data
+        self._lib.check(self._lib.load().gpmdm_rng_walk_states(self._h, draws.size, draws.ctypes.data, cf,
+                                                               out.ctypes.data), "rng walk")
+        return out
+
     def __del__(self):
         try:
             if self._h:
@@ -159,6 +168,38 @@ class _Walk:
                 self._h = None
         except Exception:
             pass
+
+
+_EXPONENTIAL, _NORMAL, _UNIFORM = 0, 1, 2
+_OPS = {_EXPONENTIAL: lambda x, g: x.exponential_(1, generator=g),
+        _NORMAL: lambda x, g: x.normal_(0, 1, generator=g),
+        _UNIFORM: lambda x, g: x.uniform_(0, 1, generator=g)}
+
+
+class _Native:
+    """libgpmdm_replay.so (csrc/replay_draws.cpp, built by gpmdm_amd/build.py): all chunks of
+    a draw run by torch's samplers on its intra-op pool in one call, the GIL released.
+    ``None`` when the library is absent or GPMDM_REPLAY_PY_CHUNKS is set (the chunks then
+    run on a Python thread pool: the same samplers and values, ~15 us more per chunk)."""
+    _lib = None
+    _tried = False
+
+    @classmethod
+    def load(cls):
+        import ctypes
+        import os
+        from pathlib import Path
+        if not cls._tried:
+            cls._tried = True
+            path = Path(__file__).resolve().parent / "libgpmdm_replay.so"
+            if path.exists() and not os.environ.get("GPMDM_REPLAY_PY_CHUNKS"):
+                lib = ctypes.CDLL(str(path))
+                lib.gpmdm_replay_draw_chunks.restype = ctypes.c_int
+                lib.gpmdm_replay_draw_chunks.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                         ctypes.c_void_p, ctypes.c_int64]
+                lib.gpmdm_replay_last_error.restype = ctypes.c_char_p
+                cls._lib = lib
+        return cls._lib
 
 
 class ParallelFrameDraws:
@@ -188,16 +229,22 @@ class ParallelFrameDraws:
     reference's whatever the caller does between frames."""
 
     def __init__(self, P: int, C: int, d: int, n_uniform: int, threads: Optional[int] = None,
-                 chunk: int = 8192, buffers=None, wait_free=None):
+                 chunk: Optional[int] = None, buffers=None, wait_free=None, native: Optional[bool] = None):
         """``buffers``: (E, N, U) float64 numpy arrays to draw into (e.g. the library's
         pinned staging buffers, gpmdm_pf_draw_buffers), else own ones; ``wait_free(k)``
-        (k = 0 E, 1 N, 2 U) returns once buffer k may be rewritten (gpmdm_pf_draws_free)."""
+        (k = 0 E, 1 N, 2 U) returns once buffer k may be rewritten (gpmdm_pf_draws_free).
+        ``chunk``: the least values per chunk (default 1024 with the native runner, 8192 on
+        the Python pool).  ``native``: run the chunks through libgpmdm_replay.so (True; an
+        error if it is absent), on the Python pool (False), or the former when present."""
         from concurrent.futures import ThreadPoolExecutor
         self.P, self.C, self.d, self.nu = int(P), int(C), int(d), int(n_uniform)
         self.threads = threads or host_threads()
-        self._pool = ThreadPoolExecutor(max_workers=self.threads)
+        self._native = _Native.load() if native is not False else None
+        if native and self._native is None:
+            raise RuntimeError("libgpmdm_replay.so is not built (python -m gpmdm_amd.build)")
+        self._pool = None if self._native is not None else ThreadPoolExecutor(max_workers=self.threads)
         self._bg = ThreadPoolExecutor(max_workers=1)
-        self._chunk = int(chunk)
+        self._chunk = int(chunk or (1024 if self._native is not None else 8192))
         if buffers is None:
             buffers = (np.empty((P, C)), np.empty((P, d)), np.empty((self.nu,)))
         self.E, self.N, self.U = (np.asarray(b, dtype=np.float64) for b in buffers)
@@ -214,6 +261,7 @@ class ParallelFrameDraws:
         self._pending = None            # background future (the next frame's walk, E, first normals)
         self.prefetch_hits = 0
         self.prefetch_misses = 0
+        self.last_hit = False           # the last begin() used the draws made ahead
         self.record = False             # keep copies of the frame's draws (last_E/N/U; tests): E
                                         # and N are refilled ahead for the next frame
 
@@ -222,10 +270,22 @@ class ParallelFrameDraws:
     def _frame_draws(self) -> int:
         return self.P * self.C + self.P * self.d + 16 * self.C + self.nu
 
-    def _run(self, tasks):
-        """Run the chunks: all but the first on the pool, the first on this thread."""
-        if not tasks:
+    def _draw(self, kind: int, flat: torch.Tensor, walk: _Walk, cache: np.ndarray, spans):
+        """Run the chunks ``spans`` = [(a, b, draw offset)] of one sampler: flat[a:b] drawn
+        from the walk's state at that offset (normal caches of ``cache``), in parallel."""
+        if not spans:
             return
+        offs = np.array([o for _, _, o in spans], dtype=np.int64)
+        states = walk.states(offs, cache)
+        if self._native is not None:
+            bounds = np.array([(a, b) for a, b, _ in spans], dtype=np.int64)
+            if self._native.gpmdm_replay_draw_chunks(kind, flat.data_ptr(), bounds.ctypes.data, states.ctypes.data,
+                                                     len(spans)) != 0:
+                raise RuntimeError("replay draws: " + self._native.gpmdm_replay_last_error().decode())
+            return
+        op = _OPS[kind]
+        st = [torch.from_numpy(states[k].copy()) for k in range(len(spans))]   # (set_state of a row view faults)
+        tasks = [lambda a=a, b=b, k=k: op(flat[a:b], self._gen(st[k])) for k, (a, b, _) in enumerate(spans)]
         futs = [self._pool.submit(f) for f in tasks[1:]]
         tasks[0]()
         for f in futs:
@@ -237,16 +297,18 @@ class ParallelFrameDraws:
         g.set_state(state)
         return g
 
-    def _normal_tasks(self, walk: _Walk, cache: np.ndarray, seg: torch.Tensor, pos: int, tasks: list):
-        """Chunks of one class's normal_ (n = seg.numel() >= 16 values from draw ``pos``)."""
-        n = seg.numel()
+    def _normal_spans(self, off: int, n: int, pos: int, spans: list):
+        """Chunks of one class's normal_ (n >= 16 values at flat[off:], from draw ``pos``)."""
         step = max(16 * -(-self._chunk // 16), 16 * -(-n // (16 * self.threads)))
         a = 0
         while a < n:
             b = n if n - a < step + 16 else a + step   # the last chunk: >= 16 values, the tail
-            st = walk.state(pos + a, cache)
-            tasks.append(lambda a=a, b=b, st=st, seg=seg: seg[a:b].normal_(0, 1, generator=self._gen(st)))
+            spans.append((off + a, off + b, pos + a))
             a = b
+
+    def _plain_spans(self, n: int, pos: int):
+        step = max(self._chunk, -(-n // self.threads))
+        return [(a, min(n, a + step), pos + a) for a in range(0, n, step)]
 
     def _ahead(self, walk: _Walk, state: np.ndarray):
         """The frame's draws that need no device result: E, and the first class's normals
@@ -255,17 +317,20 @@ class ParallelFrameDraws:
         self._wait_free(0)
         self._wait_free(1)
         flat = self._E.view(-1)
-        n, step = flat.numel(), max(self._chunk, -(-flat.numel() // self.threads))
-        tasks = []
-        for a in range(0, n, step):
-            b = min(n, a + step)
-            st = walk.state(a, state)
-            tasks.append(lambda a=a, b=b, st=st: flat[a:b].exponential_(1, generator=self._gen(st)))
+        self._draw(_EXPONENTIAL, flat, walk, state, self._plain_spans(flat.numel(), 0))
         spec = self.P * self.d >= 16
         if spec:
-            self._normal_tasks(walk, state, self._N.view(-1), self.P * self.C, tasks)
-        self._run(tasks)
+            spans = []
+            self._normal_spans(0, self.P * self.d, self.P * self.C, spans)
+            self._draw(_NORMAL, self._N.view(-1), walk, state, spans)
         return walk, state, spec
+
+    def ahead_ready(self) -> bool:
+        """Wait for the next frame's draws ahead (if any are being made); True if there are."""
+        if self._pending is None:
+            return False
+        self._pending.result()
+        return True
 
     def begin(self) -> np.ndarray:
         """The frame's Exp(1) switch draws (P x C), from the global generator's state."""
@@ -274,7 +339,8 @@ class ParallelFrameDraws:
         if self._pending is not None:
             got = self._pending.result()
             self._pending = None
-        if got is not None and self._expect is not None and torch.equal(cur, self._expect):
+        self.last_hit = got is not None and self._expect is not None and torch.equal(cur, self._expect)
+        if self.last_hit:
             self._walk, self._cache, self._spec = got
             self.prefetch_hits += 1
         else:
@@ -292,7 +358,7 @@ class ParallelFrameDraws:
         """Per-class standard normals (sum_c P_c) x d in class order."""
         walk, d = self._walk, self.d
         flat = self._N.view(-1)
-        tasks, row, first = [], 0, True
+        spans, row, first = [], 0, True
         if int(sum(int(c) for c in counts)) != self.P:
             raise ValueError(f"class counts sum to {sum(counts)}, not {self.P}")
         for p_c in counts:
@@ -300,27 +366,26 @@ class ParallelFrameDraws:
             if p_c == 0:
                 continue
             n = p_c * d
-            seg = flat[row * d:(row + p_c) * d]
+            off = row * d
             if n < 16:                  # torch's serial path: pairs and the normal cache
-                self._run(tasks)        # (the chunks before it do not depend on it: order kept simple)
-                tasks = []
+                self._draw(_NORMAL, flat, walk, self._cache, spans)   # (the chunks before it
+                spans = []                                            # do not depend on it)
                 g = self._gen(walk.state(self._pos, self._cache))
-                seg.normal_(0, 1, generator=g)
+                flat[off:off + n].normal_(0, 1, generator=g)
                 after = g.get_state().numpy()
                 self._cache = self._cache.copy()
                 self._cache[_CACHE] = after[_CACHE]
                 self._pos += _consumed(after, walk, self._pos)
             elif first and self._spec:  # drawn ahead; only a tail's last 16 are drawn again
                 if n % 16:
-                    st = walk.state(self._pos + n, self._cache)
-                    tasks.append(lambda st=st, seg=seg, n=n: seg[n - 16:n].normal_(0, 1, generator=self._gen(st)))
+                    spans.append((off + n - 16, off + n, self._pos + n))
                 self._pos += n + (16 if n % 16 else 0)
             else:
-                self._normal_tasks(walk, self._cache, seg, self._pos, tasks)
+                self._normal_spans(off, n, self._pos, spans)
                 self._pos += n + (16 if n % 16 else 0)
             first = False
             row += p_c
-        self._run(tasks)
+        self._draw(_NORMAL, flat, walk, self._cache, spans)
         if self.record:
             self.last_N = self.N.copy()
         return self.N
@@ -330,13 +395,7 @@ class ParallelFrameDraws:
         frame would leave it, and the next frame's draws ahead start in the background."""
         walk, n = self._walk, self.nu
         self._wait_free(2)
-        step = max(self._chunk, -(-n // self.threads))
-        tasks = []
-        for a in range(0, n, step):
-            b = min(n, a + step)
-            st = walk.state(self._pos + a, self._cache)
-            tasks.append(lambda a=a, b=b, st=st: self._U[a:b].uniform_(0, 1, generator=self._gen(st)))
-        self._run(tasks)
+        self._draw(_UNIFORM, self._U, walk, self._cache, self._plain_spans(n, self._pos))
         if self.record:
             self.last_U = self.U.copy()
         self._pos += n
@@ -351,7 +410,8 @@ class ParallelFrameDraws:
         if self._pending is not None:
             self._pending.result()
             self._pending = None
-        self._pool.shutdown(wait=True)
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
         self._bg.shutdown(wait=True)
 
 

@@ -162,9 +162,24 @@ int gpmdm_pf_draws_free(gpmdm_pf_t pf, int which);
  * device's counts are checked at the next switch), others copy them back synchronously.
  * Philox filters: gpmdm_pf_resample already launched the next frame's switch behind its
  * read-out (its draws need no host input), and this call then only consumes it (the
- * caller's stream waits on it if it is another stream); the call order is still required. */
+ * caller's stream waits on it if it is another stream); the call order is still required.
+ * A replay filter consumes a pending gpmdm_pf_preswitch when exp_draws is the pointer the
+ * pre-switch was given (its counts come from mapped memory once the switch kernels are
+ * done, not after the dynamics tiles behind them); another pointer drops it and switches. */
 int gpmdm_pf_switch(gpmdm_pf_t pf, const double* exp_draws, int64_t* class_counts,
                     void* stream);
+
+/* The next frame's switch launched now, between frames -- behind the last read-out, while
+ * the host is still busy -- instead of in gpmdm_pf_switch.  Replay filters: exp_draws is the
+ * next frame's P x C Exp(1) draws (a host draws them ahead: they depend on no device
+ * result); the switch, its class counts (into mapped memory) and the dynamics-GP tiles are
+ * launched on `stream`, and the next gpmdm_pf_switch with the same exp_draws pointer
+ * consumes them.  The caller promises that the array's contents do not change in between;
+ * if they do (its generator moved), it calls gpmdm_pf_preswitch again, which drops the
+ * earlier pre-switch.  Philox filters: what gpmdm_pf_resample already does (no-op if
+ * pending).  Any call that drops a pre-switch (import, predict, set_*) drops this one: the
+ * next gpmdm_pf_switch then switches from scratch.  Not inside a step. */
+int gpmdm_pf_preswitch(gpmdm_pf_t pf, const double* exp_draws, void* stream);
 
 /* _propogate_dynamics + _update_weights' likelihoods for this rank's particles
  * (gpmdm_pf.py:153-192).  z: D host.  normals: (sum_c P_c) x d host in the reference's
@@ -376,6 +391,9 @@ int gpmdm_rng_walk_create(const uint8_t* state, int64_t n_draws, gpmdm_rng_walk_
 /* restart a walk at another state (its buffer is reused when large enough) */
 int gpmdm_rng_walk_reset(gpmdm_rng_walk_t walk, const uint8_t* state, int64_t n_draws);
 int gpmdm_rng_walk_state(gpmdm_rng_walk_t walk, int64_t draws, const uint8_t* cache_from, uint8_t* out_state);
+/* the states at n offsets draws[0..n), written one after the other (n x 5056 bytes) */
+int gpmdm_rng_walk_states(gpmdm_rng_walk_t walk, int64_t n, const int64_t* draws, const uint8_t* cache_from,
+                          uint8_t* out_states);
 int gpmdm_rng_walk_destroy(gpmdm_rng_walk_t walk);
 
 /* Message of the last failed call on this thread ("" if none). */

@@ -83,3 +83,61 @@ def test_parallel_replay_step_vs_oracle(model):
     assert np.array_equal(counts, pf._counts)             # the device's counts are the oracle's
     assert_step_matches(post, r, pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), dr.last_U,
                         what="replay P=100k")
+
+
+def test_replay_preswitch_consumed_replaced_or_dropped(model, monkeypatch):
+    """gpmdm_pf_preswitch (replay filters with the draws made ahead): the next switch consumes
+    it when handed the same E pointer; a second pre-switch replaces it; another E pointer
+    drops it (the switch starts from scratch); predict / export between frames drop it --
+    every way bitwise the filter that never pre-switches (GPMDM_NO_PRESWITCH=1)."""
+    from gpmdm_amd import GPMDM_PF, _lib
+    f, m, T = model
+    Y = m.get_Y()
+    lib = _lib.load()
+
+    def run(mode):
+        torch.manual_seed(29)
+        pf = GPMDM_PF(m, T, 20000)
+        outs = []
+        for k in range(6):
+            z = np.ascontiguousarray(np.asarray(Y[80 + 5 * k], dtype=np.float64) + 0.01)
+            if mode == "poke" and k == 4:
+                # this frame by hand, with a copy of the E the pre-switch was given
+                h, s = pf._h, pf._stream()
+                dr = pf._draws
+                pE, pC, pN, pU = pf._draw_ptr
+                dr.switch()
+                E2 = dr.E.copy()
+                _lib.check(lib.gpmdm_pf_switch(h, _lib.dptr(E2), pC, s), "switch")
+                dr.dynamics(pf._counts)
+                pf._propagate(z, dr.N, s, pN)
+                dr.resample()
+                _lib.check(lib.gpmdm_pf_resample(h, pU, s), "resample")
+                pf._readout = None
+                pf._pre_sw = False
+            else:
+                pf.update(z)
+            outs.append((pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), pf._counts.copy()))
+            if mode == "poke":
+                if k == 0:                 # replaced by a second pre-switch of the same draws
+                    _lib.check(lib.gpmdm_pf_preswitch(pf._h, pf._draw_ptr[0], pf._stream()), "preswitch")
+                elif k == 1:
+                    outs.append((pf.predict().numpy(),))
+                elif k == 2:
+                    outs.append((pf.export_state()["states"],))
+            elif mode == "nopre" and k in (1, 2):
+                outs.append((pf.predict().numpy(),) if k == 1 else (pf.export_state()["states"],))
+        assert pf._draws.prefetch_hits >= 4
+        st = pf.export_state()
+        return outs, st, torch.get_rng_state().clone()
+
+    a = run("poke")
+    monkeypatch.setenv("GPMDM_NO_PRESWITCH", "1")
+    b = run("nopre")
+    assert len(a[0]) == len(b[0])
+    for k, (x, y) in enumerate(zip(a[0], b[0])):
+        for u, v in zip(x, y):
+            assert np.array_equal(u, v), k
+    for key in ("states", "classes", "ll", "w", "resample_idx"):
+        assert np.array_equal(a[1][key], b[1][key]), key
+    assert torch.equal(a[2], b[2])

@@ -31,7 +31,19 @@ def test_walk_states_are_torch_states():
     assert s0.numel() == STATE_BYTES
 
 
-def _frames(P, C, d, counts_list, interleave, threads):
+def test_walk_states_batch_is_walk_state():
+    torch.manual_seed(4)
+    s0 = torch.get_rng_state().numpy().copy()
+    w = _Walk().reset(s0, 3000)
+    offs = np.array([0, 5, 311, 312, 2999, 7], dtype=np.int64)
+    cache = s0.copy()
+    cache[5016:] = 7
+    got = w.states(offs, cache)
+    for k, o in enumerate(offs):
+        assert np.array_equal(got[k], w.state(int(o), cache).numpy()), o
+
+
+def _frames(P, C, d, counts_list, interleave, threads, native=None):
     torch.manual_seed(5)
     ref = FrameDraws(P, C, d, P)
     outs = []
@@ -41,7 +53,7 @@ def _frames(P, C, d, counts_list, interleave, threads):
         if interleave and k == 1:
             torch.randn(7)
     torch.manual_seed(5)
-    par = ParallelFrameDraws(P, C, d, P, threads=threads)
+    par = ParallelFrameDraws(P, C, d, P, threads=threads, native=native)
     par.record = True
     for k, counts in enumerate(counts_list):
         par.begin()
@@ -65,13 +77,17 @@ def _frames(P, C, d, counts_list, interleave, threads):
     (50001, 2, 3, [[25001, 25000], [50001, 0], [5, 49996], [0, 50001]]),
 ])
 @pytest.mark.parametrize("interleave", [False, True])
-def test_parallel_draws_are_the_serial_draws(P, C, d, counts_list, interleave):
-    hits, misses = _frames(P, C, d, counts_list, interleave, threads=4)
+@pytest.mark.parametrize("native", [True, False], ids=["native", "pythonpool"])
+def test_parallel_draws_are_the_serial_draws(P, C, d, counts_list, interleave, native):
+    """The chunks run by libgpmdm_replay.so (csrc/replay_draws.cpp: torch's samplers on its
+    intra-op pool) and on the Python thread pool."""
+    hits, misses = _frames(P, C, d, counts_list, interleave, threads=4, native=native)
     assert misses == (2 if interleave else 1)    # the first frame, and the frame after a caller's draw
     assert hits == len(counts_list) - misses
 
 
 def test_library_declares_the_walk():
     lib = _lib.load()
-    for name in ("gpmdm_rng_walk_create", "gpmdm_rng_walk_reset", "gpmdm_rng_walk_state", "gpmdm_rng_walk_destroy"):
+    for name in ("gpmdm_rng_walk_create", "gpmdm_rng_walk_reset", "gpmdm_rng_walk_state", "gpmdm_rng_walk_states",
+                 "gpmdm_rng_walk_destroy"):
         assert hasattr(lib, name)
