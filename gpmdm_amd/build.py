@@ -70,11 +70,12 @@ def build_replay(force: bool = False, verbose: bool = False) -> Path:
     (torch's own CPU samplers), g++ with torch's headers and C++ ABI, rpath to torch/lib."""
     import torch
     tdir = Path(torch.__file__).resolve().parent
-    if not force and REPLAY_LIB.exists() and REPLAY_LIB.stat().st_mtime >= REPLAY_SRC.stat().st_mtime:
+    if not force and REPLAY_LIB.exists() and REPLAY_LIB.stat().st_mtime >= max(REPLAY_SRC.stat().st_mtime,
+                                                                            Path(__file__).stat().st_mtime):
         return REPLAY_LIB
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     tmp = REPLAY_LIB.with_suffix(".so.tmp")
-    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-pthread", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
            f"-I{tdir / 'include'}", f"-I{tdir / 'include' / 'torch' / 'csrc' / 'api' / 'include'}",
            str(REPLAY_SRC), "-o", str(tmp), f"-L{tdir / 'lib'}", "-ltorch_cpu", "-lc10",
            f"-Wl,-rpath,{tdir / 'lib'}"]

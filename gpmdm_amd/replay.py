@@ -178,7 +178,7 @@ _OPS = {_EXPONENTIAL: lambda x, g: x.exponential_(1, generator=g),
 
 class _Native:
     """libgpmdm_replay.so (csrc/replay_draws.cpp, built by gpmdm_amd/build.py): all chunks of
-    a draw run by torch's samplers on its intra-op pool in one call, the GIL released.
+    a draw run by torch's samplers on a native thread pool in one call, the GIL released.
     ``None`` when the library is absent or GPMDM_REPLAY_PY_CHUNKS is set (the chunks then
     run on a Python thread pool: the same samplers and values, ~15 us more per chunk)."""
     _lib = None
@@ -196,7 +196,7 @@ class _Native:
                 lib = ctypes.CDLL(str(path))
                 lib.gpmdm_replay_draw_chunks.restype = ctypes.c_int
                 lib.gpmdm_replay_draw_chunks.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
-                                                         ctypes.c_void_p, ctypes.c_int64]
+                                                         ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
                 lib.gpmdm_replay_last_error.restype = ctypes.c_char_p
                 cls._lib = lib
         return cls._lib
@@ -233,7 +233,7 @@ class ParallelFrameDraws:
         """``buffers``: (E, N, U) float64 numpy arrays to draw into (e.g. the library's
         pinned staging buffers, gpmdm_pf_draw_buffers), else own ones; ``wait_free(k)``
         (k = 0 E, 1 N, 2 U) returns once buffer k may be rewritten (gpmdm_pf_draws_free).
-        ``chunk``: the least values per chunk (default 1024 with the native runner, 8192 on
+        ``chunk``: the least values per chunk (default 2048 with the native runner, 8192 on
         the Python pool).  ``native``: run the chunks through libgpmdm_replay.so (True; an
         error if it is absent), on the Python pool (False), or the former when present."""
         from concurrent.futures import ThreadPoolExecutor
@@ -244,7 +244,7 @@ class ParallelFrameDraws:
             raise RuntimeError("libgpmdm_replay.so is not built (python -m gpmdm_amd.build)")
         self._pool = None if self._native is not None else ThreadPoolExecutor(max_workers=self.threads)
         self._bg = ThreadPoolExecutor(max_workers=1)
-        self._chunk = int(chunk or (1024 if self._native is not None else 8192))
+        self._chunk = int(chunk or (2048 if self._native is not None else 8192))
         if buffers is None:
             buffers = (np.empty((P, C)), np.empty((P, d)), np.empty((self.nu,)))
         self.E, self.N, self.U = (np.asarray(b, dtype=np.float64) for b in buffers)
@@ -280,7 +280,7 @@ class ParallelFrameDraws:
         if self._native is not None:
             bounds = np.array([(a, b) for a, b, _ in spans], dtype=np.int64)
             if self._native.gpmdm_replay_draw_chunks(kind, flat.data_ptr(), bounds.ctypes.data, states.ctypes.data,
-                                                     len(spans)) != 0:
+                                                     len(spans), self.threads) != 0:
                 raise RuntimeError("replay draws: " + self._native.gpmdm_replay_last_error().decode())
             return
         op = _OPS[kind]

@@ -80,7 +80,7 @@ def _frames(P, C, d, counts_list, interleave, threads, native=None):
 @pytest.mark.parametrize("native", [True, False], ids=["native", "pythonpool"])
 def test_parallel_draws_are_the_serial_draws(P, C, d, counts_list, interleave, native):
     """The chunks run by libgpmdm_replay.so (csrc/replay_draws.cpp: torch's samplers on its
-    intra-op pool) and on the Python thread pool."""
+    native thread pool) and on the Python thread pool."""
     hits, misses = _frames(P, C, d, counts_list, interleave, threads=4, native=native)
     assert misses == (2 if interleave else 1)    # the first frame, and the frame after a caller's draw
     assert hits == len(counts_list) - misses
