@@ -59,6 +59,7 @@ _SIGS = {
     "gpmdm_pf_draws_free": (c_int, [c_void_p, c_int]),
     "gpmdm_pf_switch": (c_int, [c_void_p, _dp, _i64p, c_void_p]),
     "gpmdm_pf_preswitch": (c_int, [c_void_p, _dp, c_void_p]),
+    "gpmdm_pf_stage_normals": (c_int, [c_void_p, _dp, c_int64, c_int64, c_void_p]),
     "gpmdm_pf_propagate": (c_int, [c_void_p, _dp, _dp, c_void_p]),
     "gpmdm_pf_propagate_dynamics": (c_int, [c_void_p, _dp, c_void_p]),
     "gpmdm_pf_weigh": (c_int, [c_void_p, _dp, c_void_p]),

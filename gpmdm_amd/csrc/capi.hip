@@ -448,6 +448,19 @@ struct gpmdm_pf {
   // read-out.  gpmdm_pf_switch consumes it when handed the same E pointer.
   const double* pre_E = nullptr;
   bool pre_counts = false;            // the pre-switch's counts land in cnt_pin (cnt_done)
+  // Replay normals copied to the device ahead of the propagate that reads them
+  // (gpmdm_pf_stage_normals): the value ranges staged from nstage_ptr since the last propagate
+  const double* nstage_ptr = nullptr;
+  std::vector<std::pair<long long, long long>> nstaged;
+  bool normals_staged(const double* p, long long n) const {   // does the union cover [0, n)?
+    if (p != nstage_ptr) return false;
+    long long reach = 0;
+    for (const auto& r : nstaged) {     // sorted by start
+      if (r.first > reach) return false;
+      reach = std::max(reach, r.second);
+    }
+    return reach >= n;
+  }
   hipEvent_t ro_ev = nullptr;         // after the last read-out (gpmdm_pf_read waits on it)
   bool ro_ev_ok = false;
   int* rows_last() const { return small + 504; }   // rows of the last dynamics pass
@@ -1434,6 +1447,28 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   return do_switch(pf, E, class_counts, s);
 }
 
+int gpmdm_pf_stage_normals(gpmdm_pf_t pf, const double* normals, int64_t begin, int64_t end, void* stream) {
+  CHECK(pf, "null handle");
+  if (pf->rng_mode != GPMDM_RNG_REPLAY) return fail(GPMDM_E_STATE, "staged normals are replay draws");
+  const long long n = (long long)pf->P * pf->m->d;
+  CHECK(normals && begin >= 0 && begin <= end && end <= n, "bad normals range");
+  if (begin == end || sizeof(double) * (size_t)n <= gpmdm_pf::kZeroCopyBytes) return GPMDM_OK;   // (small: read in place)
+  hipStream_t s = (hipStream_t)stream;
+  HIPCHK(hipSetDevice(pf->m->device));
+  HIPCHK(hipEventSynchronize(pf->rep_ev[1]));   // the staging buffer's previous readers have run
+  const size_t bytes = sizeof(double) * (size_t)(end - begin);
+  if (normals != pf->rep_pin[1]) std::memcpy(pf->rep_pin[1] + begin, normals + begin, bytes);
+  HIPCHK(hipMemcpyAsync(pf->normals + begin, pf->rep_pin[1] + begin, bytes, hipMemcpyHostToDevice, s));
+  HIPCHK(pf->draws_used(1, s));
+  if (pf->nstage_ptr != normals) {
+    pf->nstage_ptr = normals;
+    pf->nstaged.clear();
+  }
+  pf->nstaged.emplace_back((long long)begin, (long long)end);
+  std::sort(pf->nstaged.begin(), pf->nstaged.end());
+  return GPMDM_OK;
+}
+
 int gpmdm_pf_preswitch(gpmdm_pf_t pf, const double* E, void* stream) {
   CHECK(pf, "null handle");
   if (!pf->initialised) return fail(GPMDM_E_STATE, "particle filter not initialised");
@@ -1521,7 +1556,12 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
   const int C = m->C, d = m->d;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
     CHECK(normals, "replay mode needs the dynamics normals");
-    HIPCHK(pf->upload_draws(1, pf->normals, normals, (size_t)pf->P * d, s));
+    if (pf->normals_staged(normals, (long long)pf->P * d))
+      pf->rep_src[1] = pf->normals;    // every value already copied (gpmdm_pf_stage_normals)
+    else
+      HIPCHK(pf->upload_draws(1, pf->normals, normals, (size_t)pf->P * d, s));
+    pf->nstage_ptr = nullptr;
+    pf->nstaged.clear();
   }
   const long long nl = pf->nloc;
   if (nl > 0) {

@@ -106,6 +106,7 @@ class GPMDM_PF:
         self._rng = rng
         self._draws = None                      # replay.FrameDraws (rng='torch'), made on first use
         self._pre_sw = False                    # a replay pre-switch with the draws made ahead is pending
+        self._n_staged = False                  # ... and the normals drawn ahead are on the device
         self._resample_mode = resample
         self._group = process_group
         self._exchange_fn = exchange
@@ -308,14 +309,22 @@ class GPMDM_PF:
             for hp, sp in self._all()[1:]:      # devices=: every rank switches all P (replay)
                 _lib.check(lib.gpmdm_pf_switch(hp, pE, None, sp), "switch")
             dr.dynamics(counts)
+            if self._n_staged:
+                # the first class's normals drawn ahead went to the device behind the last
+                # read-out; copy what dynamics() drew (everything if the ahead draw was stale)
+                v = dr.ahead_valid if dr.last_hit else 0
+                _lib.check(lib.gpmdm_pf_stage_normals(h, pN, v, P * d, s), "stage normals")
+                self._n_staged = False
             self._propagate(z, dr.N, s, pN)
             dr.resample()
             self._each("gpmdm_pf_resample", pU, what="resample")
             if self._replay_preswitch() and dr.ahead_ready():
-                # the next frame's E is drawn ahead (it needs no device result): its switch and
-                # dynamics tiles go behind this read-out (gpmdm_pf_preswitch)
+                # the next frame's E and first-class normals are drawn ahead (they need no
+                # device result): its switch and dynamics tiles go behind this read-out
+                # (gpmdm_pf_preswitch), and the normals to the device (gpmdm_pf_stage_normals)
                 _lib.check(lib.gpmdm_pf_preswitch(h, pE, s), "preswitch")
-                self._pre_sw = True
+                _lib.check(lib.gpmdm_pf_stage_normals(h, pN, 0, P * d, s), "stage normals")
+                self._pre_sw = self._n_staged = True
         else:
             self._each("gpmdm_pf_switch", None, None, what="switch")
             self._propagate(z, None, s)

@@ -262,6 +262,7 @@ class ParallelFrameDraws:
         self.prefetch_hits = 0
         self.prefetch_misses = 0
         self.last_hit = False           # the last begin() used the draws made ahead
+        self.ahead_valid = 0            # leading values of N the last dynamics() kept from the ahead draw
         self.record = False             # keep copies of the frame's draws (last_E/N/U; tests): E
                                         # and N are refilled ahead for the next frame
 
@@ -359,6 +360,7 @@ class ParallelFrameDraws:
         walk, d = self._walk, self.d
         flat = self._N.view(-1)
         spans, row, first = [], 0, True
+        self.ahead_valid = 0
         if int(sum(int(c) for c in counts)) != self.P:
             raise ValueError(f"class counts sum to {sum(counts)}, not {self.P}")
         for p_c in counts:
@@ -379,6 +381,7 @@ class ParallelFrameDraws:
             elif first and self._spec:  # drawn ahead; only a tail's last 16 are drawn again
                 if n % 16:
                     spans.append((off + n - 16, off + n, self._pos + n))
+                self.ahead_valid = n - 16 if n % 16 else n
                 self._pos += n + (16 if n % 16 else 0)
             else:
                 self._normal_spans(off, n, self._pos, spans)

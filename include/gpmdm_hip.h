@@ -181,6 +181,15 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* exp_draws, int64_t* class_count
  * next gpmdm_pf_switch then switches from scratch.  Not inside a step. */
 int gpmdm_pf_preswitch(gpmdm_pf_t pf, const double* exp_draws, void* stream);
 
+/* Replay filters: copy values [begin, end) of the next propagate's normals ((sum_c P_c) x d,
+ * flattened) to the device now, on `stream` (the propagate must run on the same stream).
+ * The next gpmdm_pf_propagate(_dynamics) handed the same `normals` pointer copies nothing if
+ * the ranges staged since the last propagate cover every value, else all of them.  A host
+ * that knows part of the normals early (the first class's, drawn ahead) stages that part
+ * behind the read-out and the rest once drawn; values changed after staging must be staged
+ * again.  Small filters (<= 32 KB of normals, read in place) ignore it. */
+int gpmdm_pf_stage_normals(gpmdm_pf_t pf, const double* normals, int64_t begin, int64_t end, void* stream);
+
 /* _propogate_dynamics + _update_weights' likelihoods for this rank's particles
  * (gpmdm_pf.py:153-192).  z: D host.  normals: (sum_c P_c) x d host in the reference's
  * per-class order (replay) or NULL (philox).  A single-shard filter of <= 1024 particles

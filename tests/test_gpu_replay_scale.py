@@ -88,8 +88,10 @@ def test_parallel_replay_step_vs_oracle(model):
 def test_replay_preswitch_consumed_replaced_or_dropped(model, monkeypatch):
     """gpmdm_pf_preswitch (replay filters with the draws made ahead): the next switch consumes
     it when handed the same E pointer; a second pre-switch replaces it; another E pointer
-    drops it (the switch starts from scratch); predict / export between frames drop it --
-    every way bitwise the filter that never pre-switches (GPMDM_NO_PRESWITCH=1)."""
+    drops it (the switch starts from scratch); predict / export between frames drop it; the
+    normals staged ahead (gpmdm_pf_stage_normals) are used only for the pointer they were
+    staged from -- every way bitwise the filter that never pre-switches or stages
+    (GPMDM_NO_PRESWITCH=1)."""
     from gpmdm_amd import GPMDM_PF, _lib
     f, m, T = model
     Y = m.get_Y()
@@ -110,7 +112,9 @@ def test_replay_preswitch_consumed_replaced_or_dropped(model, monkeypatch):
                 E2 = dr.E.copy()
                 _lib.check(lib.gpmdm_pf_switch(h, _lib.dptr(E2), pC, s), "switch")
                 dr.dynamics(pf._counts)
-                pf._propagate(z, dr.N, s, pN)
+                N2 = dr.N.copy()               # another normals pointer: the staged copy is not used
+                pf._propagate(z, N2, s, _lib.dptr(N2))
+                pf._n_staged = False
                 dr.resample()
                 _lib.check(lib.gpmdm_pf_resample(h, pU, s), "resample")
                 pf._readout = None

@@ -73,3 +73,16 @@ for native, chunk in ((False, 8192), (True, 4096), (True, 2048), (True, 1024), (
     print(f"{'native' if native else 'python pool'} chunk {chunk}: " +
           ", ".join(f"{key} {np.median(v[5:]) * 1e6:.1f} us" for key, v in ts.items()) +
           f" (median; counts {counts.tolist()})")
+
+# the pieces of one dynamics() call: walk states, the native call, its per-chunk floor
+nat = replay._Native.load()
+if nat is not None:
+    import ctypes  # noqa: E402
+    flat = torch.empty(400_000, dtype=torch.float64)
+    offs = np.arange(17, dtype=np.int64) * 1904 + 200_000
+    print(f"walk.states x17: {tm(lambda: w.states(offs, s)):.1f} us")
+    st17 = w.states(offs, s)
+    for n_ch, per in ((1, 1904), (16, 1904), (16, 64), (1, 64)):
+        bounds = np.array([(k * per, (k + 1) * per) for k in range(n_ch)], dtype=np.int64)
+        print(f"native normal_ {n_ch} chunks x {per}: "
+              f"{tm(lambda: nat.gpmdm_replay_draw_chunks(1, flat.data_ptr(), bounds.ctypes.data, st17.ctypes.data, n_ch, nthr)):.1f} us")
