@@ -448,6 +448,8 @@ struct gpmdm_pf {
   // read-out.  gpmdm_pf_switch consumes it when handed the same E pointer.
   const double* pre_E = nullptr;
   bool pre_counts = false;            // the pre-switch's counts land in cnt_pin (cnt_done)
+  hipStream_t up_stream = nullptr;    // its Exp(1) draws go up on this stream, beside the frame
+  hipEvent_t up_ev = nullptr;         // still running on the caller's (the switch waits on it)
   // Replay normals copied to the device ahead of the propagate that reads them
   // (gpmdm_pf_stage_normals): the value ranges staged from nstage_ptr since the last propagate
   const double* nstage_ptr = nullptr;
@@ -498,6 +500,7 @@ struct gpmdm_pf {
 
   ~gpmdm_pf() {
     if (sw_ev) (void)hipEventSynchronize(sw_ev);   // a pre-switch may still use the buffers
+    if (up_stream) (void)hipStreamSynchronize(up_stream);
     release_comm();
     double* ds[] = {T, X, X_prop, ll, qdyn, mudyn, qobs, sobs, z, E, normals, U,
                     e, local, blocksum, blockoffw, total, cum, partials, readout,
@@ -523,6 +526,8 @@ struct gpmdm_pf {
     if (sw_ev) (void)hipEventDestroy(sw_ev);
     if (ro_ev) (void)hipEventDestroy(ro_ev);
     if (cnt_done) (void)hipEventDestroy(cnt_done);
+    if (up_ev) (void)hipEventDestroy(up_ev);
+    if (up_stream) (void)hipStreamDestroy(up_stream);
     if (ro_pin) (void)hipHostFree(ro_pin);
     for (int k = 0; k < 2; ++k) {
       if (zpin[k]) (void)hipHostFree(zpin[k]);
@@ -1253,10 +1258,10 @@ static TileGeo dyn_frame_geo(const gpmdm_pf* pf) {
 // counts_ahead (replay pre-switch): the class counts into mapped memory with cnt_done after
 // them, and the dynamics-GP tiles launched behind, without waiting.
 static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipStream_t s, bool order_ahead = false,
-                     bool counts_ahead = false) {
+                     bool counts_ahead = false, bool e_uploaded = false) {
   gpmdm_model* m = pf->m;
   const int C = m->C;
-  if (pf->rng_mode == GPMDM_RNG_REPLAY) {
+  if (pf->rng_mode == GPMDM_RNG_REPLAY && !e_uploaded) {
     CHECK(E, "replay mode needs the Exp(1) switch draws");
     HIPCHK(pf->upload_draws(0, pf->E, E, (size_t)pf->P * C, s));
   }
@@ -1482,7 +1487,16 @@ int gpmdm_pf_preswitch(gpmdm_pf_t pf, const double* E, void* stream) {
   } else {
     CHECK(E, "replay mode needs the Exp(1) switch draws");
     TRY(drop_preswitch(pf, s, false));   // an earlier pre-switch's draws are replaced
-    TRY(do_switch(pf, E, nullptr, s, false, pf->cnt_done != nullptr));
+    if (!pf->up_stream) {
+      HIPCHK(hipStreamCreateWithFlags(&pf->up_stream, hipStreamNonBlocking));
+      HIPCHK(hipEventCreateWithFlags(&pf->up_ev, hipEventDisableTiming));
+    }
+    // the draws go up beside the frame still running on `stream` (upload_draws first waits
+    // for the last switch, the device copy's only reader); the switch waits for them
+    HIPCHK(pf->upload_draws(0, pf->E, E, (size_t)pf->P * pf->m->C, pf->up_stream));
+    HIPCHK(hipEventRecord(pf->up_ev, pf->up_stream));
+    HIPCHK(hipStreamWaitEvent(s, pf->up_ev, 0));
+    TRY(do_switch(pf, E, nullptr, s, false, pf->cnt_done != nullptr, true));
     pf->pre_E = E;
   }
   HIPCHK(hipEventRecord(pf->sw_ev, s));

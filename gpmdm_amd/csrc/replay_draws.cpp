@@ -21,6 +21,7 @@
 #include <c10/core/InferenceMode.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
@@ -59,7 +60,9 @@ void run_chunk(int kind, double* dst, int64_t a, int64_t b, const uint8_t* state
 
 // Worker threads that sleep between runs; the caller works on its run too.  One run at a
 // time (run_mu); a worker joins a run only while it is current, and the caller waits for
-// every worker that joined to leave before the run (on its stack) goes away.
+// every worker that joined to leave before the run (on its stack) goes away.  warm(us) wakes
+// the workers to poll for a run until the deadline (a frame's normals follow its switch by
+// ~0.1 ms: woken then, the workers are running when the draw comes), then they sleep again.
 class Pool {
  public:
   explicit Pool(int workers) {
@@ -72,13 +75,21 @@ class Pool {
     {
       std::lock_guard<std::mutex> lk(mu_);
       cur_ = &r;
-      ++gen_;
+      gen_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
     work(r);
     std::unique_lock<std::mutex> lk(mu_);
     cur_ = nullptr;                     // no worker joins from here on
     done_.wait(lk, [&] { return r.active == 0; });
+  }
+  void warm(int64_t us) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      warm_until_.store(now_ns() + us * 1000, std::memory_order_relaxed);
+      ++wgen_;
+    }
+    cv_.notify_all();
   }
 
  private:
@@ -88,17 +99,26 @@ class Pool {
     std::atomic<int64_t> next{0};
     int active = 0;                     // workers inside (guarded by mu_)
   };
+  static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
   static void work(Run& r) {
     for (int64_t k = r.next.fetch_add(1); k < r.n; k = r.next.fetch_add(1)) (*r.fn)(k);
   }
   void loop() {
-    uint64_t seen = 0;
+    uint64_t seen = 0, wseen = 0;
     for (;;) {
+      // warm: poll for the next run until the deadline, then block
+      while (gen_.load(std::memory_order_acquire) == seen && now_ns() < warm_until_.load(std::memory_order_relaxed))
+        __builtin_ia32_pause();
       Run* r;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return cur_ != nullptr && gen_ != seen; });
-        seen = gen_;
+        cv_.wait(lk, [&] { return (cur_ != nullptr && gen_.load() != seen) || wgen_ != wseen; });
+        wseen = wgen_;
+        if (cur_ == nullptr || gen_.load() == seen) continue;   // woken to warm up: poll
+        seen = gen_.load();
         r = cur_;
         ++r->active;
       }
@@ -113,7 +133,9 @@ class Pool {
   std::mutex run_mu_, mu_;
   std::condition_variable cv_, done_;
   Run* cur_ = nullptr;
-  uint64_t gen_ = 0;
+  std::atomic<uint64_t> gen_{0};
+  uint64_t wgen_ = 0;
+  std::atomic<int64_t> warm_until_{0};
 };
 
 Pool* pool_for(int threads) {
@@ -168,6 +190,18 @@ int gpmdm_replay_draw_chunks(int kind, double* dst, const int64_t* bounds, const
   }
   if (failed.load()) {
     g_err = first_err;
+    return -1;
+  }
+  return 0;
+}
+
+// Wake the pool of `threads` threads to poll for work for the next `us` microseconds.
+int gpmdm_replay_warm(int threads, int64_t us) {
+  if (threads < 2 || us < 0 || us > 100000) return 0;
+  try {
+    pool_for(threads)->warm(us);
+  } catch (const std::exception& e) {
+    g_err = e.what();
     return -1;
   }
   return 0;

@@ -198,6 +198,8 @@ class _Native:
                 lib.gpmdm_replay_draw_chunks.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                                          ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
                 lib.gpmdm_replay_last_error.restype = ctypes.c_char_p
+                lib.gpmdm_replay_warm.restype = ctypes.c_int
+                lib.gpmdm_replay_warm.argtypes = [ctypes.c_int, ctypes.c_int64]
                 cls._lib = lib
         return cls._lib
 
@@ -335,6 +337,8 @@ class ParallelFrameDraws:
 
     def begin(self) -> np.ndarray:
         """The frame's Exp(1) switch draws (P x C), from the global generator's state."""
+        if self._native is not None:    # the pool polls until the frame's normals (dynamics())
+            self._native.gpmdm_replay_warm(self.threads, 400)
         cur = torch.get_rng_state()
         got = None
         if self._pending is not None:
