@@ -450,6 +450,14 @@ struct gpmdm_pf {
   bool pre_counts = false;            // the pre-switch's counts land in cnt_pin (cnt_done)
   hipStream_t up_stream = nullptr;    // its Exp(1) draws go up on this stream, beside the frame
   hipEvent_t up_ev = nullptr;         // still running on the caller's (the switch waits on it)
+  hipEvent_t ndev_ev = nullptr;       // after the last dynamics finish (the device normals' reader)
+  hipError_t make_up_stream() {
+    if (up_stream) return hipSuccess;
+    hipError_t e = hipStreamCreateWithFlags(&up_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&up_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ndev_ev, hipEventDisableTiming);
+    return e;
+  }
   // Replay normals copied to the device ahead of the propagate that reads them
   // (gpmdm_pf_stage_normals): the value ranges staged from nstage_ptr since the last propagate
   const double* nstage_ptr = nullptr;
@@ -527,6 +535,7 @@ struct gpmdm_pf {
     if (ro_ev) (void)hipEventDestroy(ro_ev);
     if (cnt_done) (void)hipEventDestroy(cnt_done);
     if (up_ev) (void)hipEventDestroy(up_ev);
+    if (ndev_ev) (void)hipEventDestroy(ndev_ev);
     if (up_stream) (void)hipStreamDestroy(up_stream);
     if (ro_pin) (void)hipHostFree(ro_pin);
     for (int k = 0; k < 2; ++k) {
@@ -1460,11 +1469,19 @@ int gpmdm_pf_stage_normals(gpmdm_pf_t pf, const double* normals, int64_t begin, 
   if (begin == end || sizeof(double) * (size_t)n <= gpmdm_pf::kZeroCopyBytes) return GPMDM_OK;   // (small: read in place)
   hipStream_t s = (hipStream_t)stream;
   HIPCHK(hipSetDevice(pf->m->device));
-  HIPCHK(hipEventSynchronize(pf->rep_ev[1]));   // the staging buffer's previous readers have run
   const size_t bytes = sizeof(double) * (size_t)(end - begin);
-  if (normals != pf->rep_pin[1]) std::memcpy(pf->rep_pin[1] + begin, normals + begin, bytes);
-  HIPCHK(hipMemcpyAsync(pf->normals + begin, pf->rep_pin[1] + begin, bytes, hipMemcpyHostToDevice, s));
-  HIPCHK(pf->draws_used(1, s));
+  if (normals != pf->rep_pin[1]) {    // into the staging buffer once its previous readers have run
+    HIPCHK(hipEventSynchronize(pf->rep_ev[1]));
+    std::memcpy(pf->rep_pin[1] + begin, normals + begin, bytes);
+  }
+  HIPCHK(pf->make_up_stream());
+  // on the side stream, after the device copy's last reader (ndev_ev: the last dynamics
+  // finish), so a copy staged between frames runs beside the frame still on `stream`
+  HIPCHK(hipStreamWaitEvent(pf->up_stream, pf->ndev_ev, 0));
+  HIPCHK(hipMemcpyAsync(pf->normals + begin, pf->rep_pin[1] + begin, bytes, hipMemcpyHostToDevice, pf->up_stream));
+  HIPCHK(hipEventRecord(pf->up_ev, pf->up_stream));
+  HIPCHK(hipStreamWaitEvent(s, pf->up_ev, 0));
+  HIPCHK(pf->draws_used(1, pf->up_stream));   // the staging buffer's reader: the copy
   if (pf->nstage_ptr != normals) {
     pf->nstage_ptr = normals;
     pf->nstaged.clear();
@@ -1487,10 +1504,7 @@ int gpmdm_pf_preswitch(gpmdm_pf_t pf, const double* E, void* stream) {
   } else {
     CHECK(E, "replay mode needs the Exp(1) switch draws");
     TRY(drop_preswitch(pf, s, false));   // an earlier pre-switch's draws are replaced
-    if (!pf->up_stream) {
-      HIPCHK(hipStreamCreateWithFlags(&pf->up_stream, hipStreamNonBlocking));
-      HIPCHK(hipEventCreateWithFlags(&pf->up_ev, hipEventDisableTiming));
-    }
+    HIPCHK(pf->make_up_stream());
     // the draws go up beside the frame still running on `stream` (upload_draws first waits
     // for the last switch, the device copy's only reader); the switch waits for them
     HIPCHK(pf->upload_draws(0, pf->E, E, (size_t)pf->P * pf->m->C, pf->up_stream));
@@ -1634,7 +1648,10 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
     HIPCHK(hipMemsetAsync(pf->rows_last(), 0, sizeof(int), s));
   }
   HIPCHK(hipGetLastError());
-  if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(1, s));
+  if (pf->rng_mode == GPMDM_RNG_REPLAY) {
+    HIPCHK(pf->draws_used(1, s));
+    if (pf->ndev_ev) HIPCHK(hipEventRecord(pf->ndev_ev, s));
+  }
   pf->dyn_done = true;
   pf->switched = false;
   return GPMDM_OK;
@@ -2092,7 +2109,17 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   const bool sys = pf->resample_mode == GPMDM_RESAMPLE_SYSTEMATIC;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
     CHECK(uniforms, "replay mode needs the resampling uniforms");
-    HIPCHK(pf->upload_draws(2, pf->U, uniforms, sys ? 1 : (size_t)pf->P, s));
+    if (pf->up_stream) {
+      // (a filter that pre-switches) beside the observation GP still running on `stream`:
+      // host-to-device copies share one engine in submission order, so a copy queued on
+      // `stream` behind the GP would hold the next frame's draws (queued on up_stream after
+      // it) back until the GP ends.  upload_draws first waits for the last resample.
+      HIPCHK(pf->upload_draws(2, pf->U, uniforms, sys ? 1 : (size_t)pf->P, pf->up_stream));
+      HIPCHK(hipEventRecord(pf->up_ev, pf->up_stream));
+      HIPCHK(hipStreamWaitEvent(s, pf->up_ev, 0));
+    } else {
+      HIPCHK(pf->upload_draws(2, pf->U, uniforms, sys ? 1 : (size_t)pf->P, s));
+    }
   }
   hipEvent_t t0;
   pf->mark_begin(s, GPMDM_STAGE_RESAMPLE, t0);
