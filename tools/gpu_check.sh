@@ -8,7 +8,7 @@ out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
 kargs=(); [ -n "$kexpr" ] && kargs=(-k "$kexpr")
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread "${kargs[@]}" > $out/pytest.log 2>&1 \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${kargs[@]}" > $out/pytest.log 2>&1 \
   || { echo "pytest failed rc=$?"; tail -40 $out/pytest.log; exit 1; }
 tail -3 $out/pytest.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 \
