@@ -145,3 +145,52 @@ def test_replay_preswitch_consumed_replaced_or_dropped(model, monkeypatch):
     for key in ("states", "classes", "ll", "w", "resample_idx"):
         assert np.array_equal(a[1][key], b[1][key]), key
     assert torch.equal(a[2], b[2])
+
+
+def test_preswitch_and_staging_contract(model):
+    """gpmdm_pf_preswitch / gpmdm_pf_stage_normals: a Philox filter's explicit pre-switch is
+    the one its resample launched (no-op, bitwise); inside a step both calls are refused;
+    a bad normals range is a ValueError; a Philox filter has no normals to stage."""
+    from gpmdm_amd import GPMDM_PF, _lib
+    f, m, T = model
+    Y = m.get_Y()
+    lib = _lib.load()
+    outs = []
+    for poke in (False, True):
+        torch.manual_seed(31)
+        pf = GPMDM_PF(m, T, 5000, rng="philox", seed=3)
+        for k in range(3):
+            pf.update(np.asarray(Y[40 + k], dtype=np.float64) + 0.01)
+            if poke:
+                _lib.check(lib.gpmdm_pf_preswitch(pf._h, None, pf._stream()), "preswitch")
+        outs.append((pf.class_probabilities().numpy(), pf.export_state()["states"]))
+        with pytest.raises(RuntimeError):
+            _lib.check(lib.gpmdm_pf_stage_normals(pf._h, None, 0, 1, pf._stream()), "stage")
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    torch.manual_seed(32)
+    pf = GPMDM_PF(m, T, 20000)
+    z = np.ascontiguousarray(np.asarray(Y[50], dtype=np.float64) + 0.01)
+    pf.update(z)
+    pN = pf._draw_ptr[2]
+    with pytest.raises(ValueError):
+        _lib.check(lib.gpmdm_pf_stage_normals(pf._h, pN, 0, 20000 * m.d + 1, pf._stream()), "stage")
+    with pytest.raises(ValueError):
+        _lib.check(lib.gpmdm_pf_stage_normals(pf._h, pN, 5, 4, pf._stream()), "stage")
+    # inside a step: after the switch, before the propagate
+    s = pf._stream()
+    dr = pf._draws
+    dr.switch()
+    if pf._pre_sw and not dr.last_hit:
+        _lib.check(lib.gpmdm_pf_preswitch(pf._h, pf._draw_ptr[0], s), "preswitch")
+    _lib.check(lib.gpmdm_pf_switch(pf._h, pf._draw_ptr[0], pf._draw_ptr[1], s), "switch")
+    with pytest.raises(RuntimeError):
+        _lib.check(lib.gpmdm_pf_preswitch(pf._h, pf._draw_ptr[0], s), "preswitch")
+    # the step completes as usual
+    dr.dynamics(pf._counts)
+    N2 = dr.N.copy()                       # (not the staged pointer: copied in full)
+    pf._propagate(z, N2, s, _lib.dptr(N2))
+    dr.resample()
+    _lib.check(lib.gpmdm_pf_resample(pf._h, pf._draw_ptr[3], s), "resample")
+    pf._readout = None
+    pf._pre_sw = pf._n_staged = False
+    assert np.isfinite(pf.class_probabilities().numpy()).all()

@@ -91,3 +91,31 @@ def test_library_declares_the_walk():
     for name in ("gpmdm_rng_walk_create", "gpmdm_rng_walk_reset", "gpmdm_rng_walk_state", "gpmdm_rng_walk_states",
                  "gpmdm_rng_walk_destroy"):
         assert hasattr(lib, name)
+
+
+def test_native_runner_exports_and_rejects_bad_arguments():
+    """libgpmdm_replay.so (built by gpmdm_amd.build): its entry points, and argument checks
+    that return an error instead of drawing (no GPU)."""
+    import ctypes
+    from gpmdm_amd.replay import _Native
+    lib = _Native.load()
+    if lib is None:
+        pytest.skip("GPMDM_REPLAY_PY_CHUNKS set or the runner is not built")
+    for name in ("gpmdm_replay_draw_chunks", "gpmdm_replay_warm", "gpmdm_replay_last_error"):
+        assert hasattr(lib, name)
+    buf = np.zeros(64)
+    states = np.zeros((1, STATE_BYTES), dtype=np.uint8)
+    bad = np.array([10, 5], dtype=np.int64)                     # end before begin
+    assert lib.gpmdm_replay_draw_chunks(1, buf.ctypes.data, bad.ctypes.data, states.ctypes.data, 1, 2) == -1
+    assert b"bounds" in lib.gpmdm_replay_last_error()
+    ok = np.array([0, 64], dtype=np.int64)
+    assert lib.gpmdm_replay_draw_chunks(7, buf.ctypes.data, ok.ctypes.data, states.ctypes.data, 1, 2) == -1   # kind
+    assert lib.gpmdm_replay_warm(4, 100) == 0
+    assert lib.gpmdm_replay_warm(4, -1) == 0                    # ignored
+    # a real draw from torch's state: the values of a generator in that state
+    torch.manual_seed(8)
+    st = torch.get_rng_state().numpy().copy()[None, :]
+    assert lib.gpmdm_replay_draw_chunks(2, buf.ctypes.data, ok.ctypes.data, st.ctypes.data, 1, 1) == 0
+    g = torch.Generator()
+    g.set_state(torch.from_numpy(st[0].copy()))
+    assert np.array_equal(buf, torch.empty(64, dtype=torch.float64).uniform_(0, 1, generator=g).numpy())
