@@ -21,7 +21,7 @@ zs = data.observation_stream(80, seed=1)
 torch.manual_seed(11)
 pf = GPMDM_PF(model, T, P)
 lib, h = _lib.load(), pf._h
-phases = {k: [] for k in ("begin", "switch", "normals", "propagate", "uniforms", "resample", "read")}
+phases = {k: [] for k in ("begin", "switch", "normals", "propagate", "uniforms", "resample+preswitch", "read")}
 for k in range(40):
     z = np.ascontiguousarray(zs[k], dtype=np.float64)
     s = pf._stream()
@@ -30,13 +30,20 @@ for k in range(40):
         pf.update(z)
         pf.class_probabilities()
         continue
+    # GPMDM_PF.update's replay branch, phase by phase (pre-switch and staged normals included)
     dr, counts = pf._draws, pf._counts
     pE, pC, pN, pU = pf._draw_ptr
     dr.switch()
+    if pf._pre_sw and not dr.last_hit:
+        _lib.check(lib.gpmdm_pf_preswitch(h, pE, s))
+    pf._pre_sw = False
     t1 = time.perf_counter()
     _lib.check(lib.gpmdm_pf_switch(h, pE, pC, s))
     t2 = time.perf_counter()
     dr.dynamics(counts)
+    if pf._n_staged:
+        _lib.check(lib.gpmdm_pf_stage_normals(h, pN, dr.ahead_valid if dr.last_hit else 0, P * pf.latent_dim, s))
+        pf._n_staged = False
     t3 = time.perf_counter()
     pf._propagate(z, dr.N, s, pN)
     t4 = time.perf_counter()
@@ -44,6 +51,10 @@ for k in range(40):
     t5 = time.perf_counter()
     _lib.check(lib.gpmdm_pf_resample(h, pU, s))
     pf._readout = None
+    if pf._replay_preswitch() and dr.ahead_ready():
+        _lib.check(lib.gpmdm_pf_preswitch(h, pE, s))
+        _lib.check(lib.gpmdm_pf_stage_normals(h, pN, 0, P * pf.latent_dim, s))
+        pf._pre_sw = pf._n_staged = True
     t6 = time.perf_counter()
     pf.class_probabilities()
     t7 = time.perf_counter()
