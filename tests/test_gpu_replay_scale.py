@@ -194,3 +194,31 @@ def test_preswitch_and_staging_contract(model):
     pf._readout = None
     pf._pre_sw = pf._n_staged = False
     assert np.isfinite(pf.class_probabilities().numpy()).all()
+
+
+@pytest.mark.parametrize("resample,dedup", [("systematic", True), ("multinomial", False)])
+def test_replay_preswitch_other_modes(model, monkeypatch, resample, dedup):
+    """The replay pre-switch and staged normals with systematic resampling (one uniform per
+    frame) and without ancestor de-duplication (every particle a dynamics row): bitwise the
+    filter that switches in each update (GPMDM_NO_PRESWITCH=1)."""
+    from gpmdm_amd import GPMDM_PF
+    f, m, T = model
+    Y = m.get_Y()
+
+    def run():
+        torch.manual_seed(37)
+        pf = GPMDM_PF(m, T, 20000, resample=resample, dedup=dedup)
+        outs = []
+        for k in range(4):
+            pf.update(np.asarray(Y[90 + 4 * k], dtype=np.float64) + 0.01)
+            outs.append((pf.class_probabilities().numpy(), pf.current_state_mean().numpy()))
+        return outs, pf.export_state(), torch.get_rng_state().clone()
+
+    a = run()
+    monkeypatch.setenv("GPMDM_NO_PRESWITCH", "1")
+    b = run()
+    for x, y in zip(a[0], b[0]):
+        assert np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1])
+    for key in ("states", "classes", "ll", "w", "resample_idx"):
+        assert np.array_equal(a[1][key], b[1][key]), key
+    assert torch.equal(a[2], b[2])
