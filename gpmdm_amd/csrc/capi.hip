@@ -383,7 +383,12 @@ struct gpmdm_pf {
   double* ro_pin = nullptr;
   double* ro_dev = nullptr;
   int* cnt_dev = nullptr;
-  hipEvent_t zev[2] = {nullptr, nullptr};
+  hipEvent_t zev[2] = {nullptr, nullptr};   // (unused: see zslot_free)
+  // A z slot is written again two frames after its frame used it; its readers (k_dyn_finish,
+  // the observation tiles, the likelihood finish) precede that frame's read-out, and the
+  // resample of the frame in between has recorded ro_ev by then (the call order is enforced),
+  // so ro_ev guards both slots -- no event record of its own between two kernels.
+  hipError_t zslot_free() { return ro_ev_ok ? hipEventSynchronize(ro_ev) : hipSuccess; }
   int zslot = 0;
   bool z_staged = false;              // zpin[zslot] holds the frame's z, k_dyn_finish copies it
   double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *sobs = nullptr;
@@ -440,7 +445,10 @@ struct gpmdm_pf {
   // turns it off (A/B).
   bool preswitch = true;
   bool preswitched = false;           // launched, not yet consumed by gpmdm_pf_switch
-  hipEvent_t sw_ev = nullptr;         // after the pre-switch
+  // after the pre-switch: recorded on sw_stream only when another stream or the host must
+  // wait for it (an event record between two kernels idles the GPU ~6 us; on the stream
+  // itself the order already holds), so it covers whatever followed the pre-switch there too
+  hipEvent_t sw_ev = nullptr;
   hipStream_t sw_stream = nullptr;
   // Replay filters pre-switch on the caller's request (gpmdm_pf_preswitch: the next frame's
   // Exp(1) draws are the caller's, drawn ahead on the host): the switch, its class counts into
@@ -507,7 +515,7 @@ struct gpmdm_pf {
   const int* own_order() const { return own_valid ? own : nullptr; }
 
   ~gpmdm_pf() {
-    if (sw_ev) (void)hipEventSynchronize(sw_ev);   // a pre-switch may still use the buffers
+    if (preswitched) (void)hipDeviceSynchronize();   // a pre-switch may still use the buffers
     if (up_stream) (void)hipStreamSynchronize(up_stream);
     release_comm();
     double* ds[] = {T, X, X_prop, ll, qdyn, mudyn, qobs, sobs, z, E, normals, U,
@@ -1095,6 +1103,7 @@ static int flush_ll(gpmdm_pf* pf, hipStream_t s) {
 // the next gpmdm_pf_switch launches the switch again (same draws: the same tables).
 static int drop_preswitch(gpmdm_pf* pf, hipStream_t s, bool host_wait) {
   if (!pf->preswitched) return GPMDM_OK;
+  if (host_wait || s != pf->sw_stream) HIPCHK(hipEventRecord(pf->sw_ev, pf->sw_stream));   // (see sw_ev)
   if (host_wait)
     HIPCHK(hipEventSynchronize(pf->sw_ev));
   else if (s != pf->sw_stream)
@@ -1444,7 +1453,10 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
   if (pf->preswitched && pf->rng_mode == GPMDM_RNG_REPLAY && E != pf->pre_E)
     TRY(drop_preswitch(pf, s, false));   // other draws than the pre-switch's: switch again
   if (pf->preswitched) {               // launched by the last resample / gpmdm_pf_preswitch: consume it
-    if (s != pf->sw_stream) HIPCHK(hipStreamWaitEvent(s, pf->sw_ev, 0));
+    if (s != pf->sw_stream) {
+      HIPCHK(hipEventRecord(pf->sw_ev, pf->sw_stream));
+      HIPCHK(hipStreamWaitEvent(s, pf->sw_ev, 0));
+    }
     pf->preswitched = false;
     if (class_counts && pf->pre_counts) {
       HIPCHK(hipEventSynchronize(pf->cnt_done));   // the counts, not the tiles behind them
@@ -1513,7 +1525,6 @@ int gpmdm_pf_preswitch(gpmdm_pf_t pf, const double* E, void* stream) {
     TRY(do_switch(pf, E, nullptr, s, false, pf->cnt_done != nullptr, true));
     pf->pre_E = E;
   }
-  HIPCHK(hipEventRecord(pf->sw_ev, s));
   pf->sw_stream = s;
   pf->preswitched = true;
   return GPMDM_OK;
@@ -1672,7 +1683,7 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     pf->z_staged = false;
     pf->zslot ^= 1;
   } else {
-    HIPCHK(hipEventSynchronize(pf->zev[zk]));     // the slot's previous readers have run
+    HIPCHK(pf->zslot_free());
     std::memcpy(pf->zpin[zk], zh, sizeof(double) * D * pf->F);
     if (zmap)
       zsrc = pf->zdev[zk];
@@ -1739,7 +1750,6 @@ static int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     }
     pf->mark_end(s, GPMDM_STAGE_OBS_FINISH, t0);
   }
-  HIPCHK(hipEventRecord(pf->zev[zk], s));
   HIPCHK(hipGetLastError());
   pf->propagated = true;
   pf->dyn_done = false;
@@ -1826,7 +1836,7 @@ int gpmdm_pf_propagate(gpmdm_pf_t pf, const double* zh, const double* normals, v
   const int D = pf->m->D;
   const bool zstage = pf->nloc > 4096 && pf->nloc >= (long long)D * pf->F;
   if (zstage) {
-    HIPCHK(hipEventSynchronize(pf->zev[pf->zslot]));   // the slot's previous readers have run
+    HIPCHK(pf->zslot_free());
     std::memcpy(pf->zpin[pf->zslot], zh, sizeof(double) * D * pf->F);
   }
   const int rc = propagate_dynamics(pf, normals, (hipStream_t)stream, zstage);
@@ -2182,7 +2192,6 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   if (pf->preswitch) {                 // the next frame's switch, behind the read-out
     static const bool no_ahead = std::getenv("GPMDM_NO_ORDER_AHEAD") != nullptr;   // A/B
     TRY(do_switch(pf, nullptr, nullptr, s, pf->order_wanted() && !no_ahead));
-    HIPCHK(hipEventRecord(pf->sw_ev, s));
     pf->sw_stream = s;
     pf->preswitched = true;
   }

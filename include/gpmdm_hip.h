@@ -264,7 +264,9 @@ int gpmdm_pf_propagate_multi(gpmdm_pf_t* pfs, int n, const double* z, const doub
  * 302-312).  uniforms: P host (replay, multinomial), 1 host (replay, systematic) or NULL.
  * Philox filters then launch the next frame's switch on the same stream (see
  * gpmdm_pf_switch); gpmdm_pf_predict, gpmdm_pf_init and the gpmdm_pf_set_* calls drop it,
- * and the next gpmdm_pf_switch launches it again (the same draws, the same result). */
+ * and the next gpmdm_pf_switch launches it again (the same draws, the same result).  The
+ * stream must stay valid until that next switch or drop (a call that waits for the
+ * pre-switch from another stream or the host records its event on this stream then). */
 int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream);
 
 /* update(z) in one call  (gpmdm_pf.py:117-135): switch + propagate + resample.
