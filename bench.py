@@ -786,10 +786,12 @@ def main():
     pf.stage_times()                # drop warm-up records
     # The roofline kernel's launches are timed live with HIP events (two per timed launch)
     # on every `sample`-th frame of the timed region: each record is a host API call on the
-    # frame's critical path (~11 us; measured at the notebook's 0.13 ms frames), so the
-    # sample keeps that cost out of ms_per_step while the average launch time still comes
-    # from launches inside the timed loop.
-    sample = 8 if args.config == 1 else 4
+    # frame's critical path (~11 us; measured at the notebook's 0.13 ms frames) and idles the
+    # GPU between the kernels around it (a sampled headline frame runs ~40 us longer:
+    # profiles/r04/events_ab/), so the sample keeps that cost out of ms_per_step while the
+    # average launch time still comes from launches inside the timed loop (>= 31 of 500 at
+    # configs 2 / 4; configs 3 / 5 time 20 frames of 0.15-0.8 s launches, every 4th).
+    sample = {1: 8, 3: 4, 5: 4}.get(args.config, 16)
     pf.enable_timing(True, stages=("obs_gemm",))   # the roofline kernel only
     pf.enable_timing(False)
     lib_, h_ = _lib.load(), pf._h
