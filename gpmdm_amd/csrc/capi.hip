@@ -469,6 +469,7 @@ struct gpmdm_pf {
   // Replay normals copied to the device ahead of the propagate that reads them
   // (gpmdm_pf_stage_normals): the value ranges staged from nstage_ptr since the last propagate
   const double* nstage_ptr = nullptr;
+  bool n_staged_frame = false;        // this frame's normals came fully staged
   std::vector<std::pair<long long, long long>> nstaged;
   bool normals_staged(const double* p, long long n) const {   // does the union cover [0, n)?
     if (p != nstage_ptr) return false;
@@ -1595,7 +1596,8 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
   const int C = m->C, d = m->d;
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
     CHECK(normals, "replay mode needs the dynamics normals");
-    if (pf->normals_staged(normals, (long long)pf->P * d))
+    pf->n_staged_frame = pf->normals_staged(normals, (long long)pf->P * d);
+    if (pf->n_staged_frame)
       pf->rep_src[1] = pf->normals;    // every value already copied (gpmdm_pf_stage_normals)
     else
       HIPCHK(pf->upload_draws(1, pf->normals, normals, (size_t)pf->P * d, s));
@@ -1660,7 +1662,10 @@ static int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s
   }
   HIPCHK(hipGetLastError());
   if (pf->rng_mode == GPMDM_RNG_REPLAY) {
-    HIPCHK(pf->draws_used(1, s));
+    // the staging buffer's readers: the side-stream copies when staged (they recorded
+    // rep_ev[1] themselves), else the copy / the in-place reads above (one record fewer
+    // between the dynamics finish and the observation GP when staged)
+    if (!pf->n_staged_frame) HIPCHK(pf->draws_used(1, s));
     if (pf->ndev_ev) HIPCHK(hipEventRecord(pf->ndev_ev, s));
   }
   pf->dyn_done = true;
