@@ -1,12 +1,14 @@
 // C ABI of libgpmdm_hip.so (include/gpmdm_hip.h): model and particle-filter handles,
 // device memory layout, and the per-frame launch sequence.
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <dlfcn.h>
@@ -388,7 +390,36 @@ struct gpmdm_pf {
   // the observation tiles, the likelihood finish) precede that frame's read-out, and the
   // resample of the frame in between has recorded ro_ev by then (the call order is enforced),
   // so ro_ev guards both slots -- no event record of its own between two kernels.
-  hipError_t zslot_free() { return ro_ev_ok ? hipEventSynchronize(ro_ev) : hipSuccess; }
+  hipError_t zslot_free() {
+    if (seq_pin) return wait_readout(ro_seq);
+    return ro_ev_ok ? hipEventSynchronize(ro_ev) : hipSuccess;
+  }
+  // Single filters whose read-out lands in mapped memory also get its sequence number there
+  // (the read-out kernels publish it after the values: publish_readout), and the host waits on
+  // that instead of on an event recorded behind the read-out -- such a record idles the GPU
+  // ~6 us before the next frame's switch.  GPMDM_RO_EVENT=1 keeps the event (A/B).
+  long long* seq_pin = nullptr;
+  long long* seq_dev = nullptr;
+  long long ro_seq = 0;               // the last read-out's number (0: none launched)
+  hipError_t wait_readout(long long target) const {
+    const volatile long long* p = seq_pin;
+    if (*p >= target) return hipSuccess;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 1;; ++it) {
+      if (*p >= target) return hipSuccess;
+      if ((it & 255) == 0) {
+        std::this_thread::yield();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
+          // not published: whatever the device is doing, finish it and look once more
+          const hipError_t e = hipDeviceSynchronize();
+          if (e != hipSuccess) return e;
+          return *p >= target ? hipSuccess : hipErrorUnknown;
+        }
+      } else {
+        __builtin_ia32_pause();
+      }
+    }
+  }
   int zslot = 0;
   bool z_staged = false;              // zpin[zslot] holds the frame's z, k_dyn_finish copies it
   double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *sobs = nullptr;
@@ -547,6 +578,7 @@ struct gpmdm_pf {
     if (ndev_ev) (void)hipEventDestroy(ndev_ev);
     if (up_stream) (void)hipStreamDestroy(up_stream);
     if (ro_pin) (void)hipHostFree(ro_pin);
+    if (seq_pin) (void)hipHostFree(seq_pin);
     for (int k = 0; k < 2; ++k) {
       if (zpin[k]) (void)hipHostFree(zpin[k]);
       if (zev[k]) (void)hipEventDestroy(zev[k]);
@@ -930,6 +962,17 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
       return fail(GPMDM_E_NOMEM, "mapped read-out buffer");
     }
     pf->ro_dev = (double*)rv;
+    void* sv = nullptr;
+    if (F == 1 && std::getenv("GPMDM_RO_EVENT") == nullptr) {
+      if (hipHostMalloc((void**)&pf->seq_pin, sizeof(long long), hipHostMallocMapped | hipHostMallocCoherent) !=
+              hipSuccess ||
+          hipHostGetDevicePointer(&sv, pf->seq_pin, 0) != hipSuccess) {
+        delete pf;
+        return fail(GPMDM_E_NOMEM, "mapped read-out number");
+      }
+      *pf->seq_pin = 0;
+      pf->seq_dev = (long long*)sv;
+    }
   }
   {
     void* rv = nullptr;
@@ -1162,6 +1205,7 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   HIPCHK(hipEventRecord(pf->ro_ev, nullptr));
   HIPCHK(hipDeviceSynchronize());
   pf->ro_ev_ok = true;
+  if (pf->seq_pin) pf->ro_seq = *(volatile long long*)pf->seq_pin;   // (synchronised: nothing to wait for)
   pf->initialised = true;
   pf->own_valid = false;               // no ancestors yet: identity ownership
   pf->rows_st = pf->rows_ll = nullptr;
@@ -1236,6 +1280,7 @@ int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes,
   HIPCHK(hipEventRecord(pf->ro_ev, nullptr));
   HIPCHK(hipDeviceSynchronize());
   pf->ro_ev_ok = true;
+  if (pf->seq_pin) pf->ro_seq = *(volatile long long*)pf->seq_pin;   // (synchronised: nothing to wait for)
   pf->initialised = true;
   pf->switched = pf->propagated = pf->dyn_done = pf->gemm_ahead = false;
   return GPMDM_OK;
@@ -2139,6 +2184,10 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   hipEvent_t t0;
   pf->mark_begin(s, GPMDM_STAGE_RESAMPLE, t0);
   ResampleArgs ra = resample_args(pf);
+  if (pf->seq_pin) {                   // the read-out's number, published after it
+    ra.seq_host = pf->seq_dev;
+    ra.seq = ++pf->ro_seq;
+  }
   ra.U = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->rep_src[2] : nullptr;
   NormArgs na = norm_args(pf);
   const bool small = small_resample_ok(na, ra);
@@ -2190,8 +2239,10 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   pf->own_next_frame = -1;
   pf->mark_end(s, GPMDM_STAGE_RESAMPLE, t0);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(pf->ro_ev, s));
-  pf->ro_ev_ok = true;
+  if (!pf->seq_pin) {                  // (else the read-out kernel publishes its number)
+    HIPCHK(hipEventRecord(pf->ro_ev, s));
+    pf->ro_ev_ok = true;
+  }
   pf->frame += 1;
   pf->propagated = false;
   if (pf->preswitch) {                 // the next frame's switch, behind the read-out
@@ -2226,6 +2277,8 @@ int gpmdm_pf_read(gpmdm_pf_t pf, double* post, double* mean, double* lik, void* 
     HIPCHK(hipMemcpyAsync(pf->rpin, pf->readout, sizeof(double) * pf->F * nr, hipMemcpyDeviceToHost, s));
     src = pf->rpin;
     HIPCHK(hipStreamSynchronize(s));
+  } else if (pf->seq_pin) {
+    HIPCHK(pf->wait_readout(pf->ro_seq));     // not the stream: a pre-switch may follow
   } else if (pf->ro_ev_ok) {
     HIPCHK(hipEventSynchronize(pf->ro_ev));   // not the stream: a pre-switch may follow
   } else {

@@ -225,6 +225,8 @@ struct ResampleArgs {
   double* partials;               // F x nb x (C + 1 + d)
   double* readout;                // per filter: C posterior, d mean, 1 likelihood sum
   double* readout_host;           // the same into mapped host memory (small filters), or nullptr
+  long long* seq_host;            // mapped: `seq` published after readout_host (or nullptr)
+  long long seq;
   int* cls_host;                  // post-resample classes into mapped host memory (k_small_resample,
                                   // single replay filters: the next switch's counts on the host), or nullptr
   int* guide;                     // F x (GB + 3): guide[b] = first i with cum[i] >= b / GB

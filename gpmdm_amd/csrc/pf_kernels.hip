@@ -1072,6 +1072,17 @@ __global__ __launch_bounds__(kB) void k_rows_ll(RowsLLArgs a) {
   }
 }
 
+// The read-out is in mapped host memory: publish its sequence number after it, so the host
+// that sees the number sees the values (every storing thread's system-scope fence precedes
+// the barrier, the number's store follows it) -- gpmdm_pf_read then waits on host memory,
+// and no event record sits between the read-out and the next frame's switch.
+__device__ inline void publish_readout(const ResampleArgs& a, long long f, int tid) {
+  if (!a.seq_host) return;              // (uniform over the workgroup)
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0) *(volatile long long*)(a.seq_host + f) = a.seq;
+}
+
 __global__ __launch_bounds__(1024) void k_readout(ResampleArgs a) {
   __shared__ double red[8][16];
   __shared__ double tot[kMaxReadout];
@@ -1120,6 +1131,7 @@ __global__ __launch_bounds__(1024) void k_readout(ResampleArgs a) {
     readout[tid] = v;
     if (a.readout_host) a.readout_host[f * nro + tid] = v;
   }
+  publish_readout(a, f, tid);
 }
 
 
@@ -1334,6 +1346,7 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
     readout[tid] = v;
     if (a.readout_host) a.readout_host[f * nro + tid] = v;
   }
+  publish_readout(a, f, tid);
 }
 
 // ---------------------------------------------------------------------------------
