@@ -1174,7 +1174,8 @@ static int drop_preswitch(gpmdm_pf* pf, hipStream_t s, bool host_wait) {
 // operations); a difference is reported as an error, never used.
 static int check_counts(gpmdm_pf* pf) {
   if (!pf->cnt_check) return GPMDM_OK;
-  HIPCHK(hipEventSynchronize(pf->cnt_ev));   // done: it precedes the resample already waited for
+  // done: it precedes the resample already waited for (whose read-out number follows it)
+  HIPCHK(pf->seq_pin ? pf->wait_readout(pf->ro_seq) : hipEventSynchronize(pf->cnt_ev));
   pf->cnt_check = false;
   for (int c = 0; c < pf->m->C; ++c)
     if (pf->cnt_pin[c] != pf->cnt_expect[c])
@@ -1435,7 +1436,8 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
       class_counts && pf->rng_mode == GPMDM_RNG_REPLAY && pf->cls_host_ok && !sl && !no_host_counts;
   if (host_counts) {
     if (pf->cls_ev_pending) {          // the resample that wrote cls_pin (normally done: read)
-      HIPCHK(hipEventSynchronize(pf->cls_ev));
+      // (k_small_resample writes cls_pin before the read-out number it publishes)
+      HIPCHK(pf->seq_pin ? pf->wait_readout(pf->ro_seq) : hipEventSynchronize(pf->cls_ev));
       pf->cls_ev_pending = false;
     }
     TRY(check_counts(pf));
@@ -1475,7 +1477,7 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
     }
     pf->pre_counts = true;
   } else if (host_counts) {
-    HIPCHK(hipEventRecord(pf->cnt_ev, s));
+    if (!pf->seq_pin) HIPCHK(hipEventRecord(pf->cnt_ev, s));
     pf->cnt_check = true;
     for (int c = 0; c < C; ++c) class_counts[c] = pf->cnt_expect[c];
   } else if (class_counts) {
@@ -2227,7 +2229,7 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   pf->bmax_ready = false;
   pf->cls_host_ok = cls_host;
   if (cls_host) {
-    HIPCHK(hipEventRecord(pf->cls_ev, s));
+    if (!pf->seq_pin) HIPCHK(hipEventRecord(pf->cls_ev, s));
     pf->cls_ev_pending = true;
   }
   pf->ll_pending = false;

@@ -1,5 +1,5 @@
 set -o pipefail
-out=gpurun_out/r04_zc; mkdir -p $out
+out=${OUT:-gpurun_out/r04_zc}; mkdir -p $out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $out/pytest.log 2>&1; tail -2 $out/pytest.log
 grep -q " passed" $out/pytest.log && ! grep -q "failed" $out/pytest.log || exit 1
 for r in 1 2 3; do
