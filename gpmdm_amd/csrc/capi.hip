@@ -403,26 +403,32 @@ struct gpmdm_pf {
     if (seq_pin) return wait_readout(ro_seq);
     return ro_ev_ok ? hipEventSynchronize(ro_ev) : hipSuccess;
   }
-  // Single filters whose read-out lands in mapped memory also get its sequence number there
-  // (the read-out kernels publish it after the values: publish_readout), and the host waits on
-  // that instead of on an event recorded behind the read-out -- such a record idles the GPU
-  // ~6 us before the next frame's switch.  GPMDM_RO_EVENT=1 keeps the event (A/B).
+  // Filters whose read-outs land in mapped memory (one number per filter of a bank) also get
+  // their sequence numbers there (the read-out kernels publish them after the values:
+  // publish_readout), and the host waits on them instead of on an event recorded behind the
+  // read-out -- such a record idles the GPU ~6 us before the next frame's switch.
+  // GPMDM_RO_EVENT=1 keeps the event (A/B).
   long long* seq_pin = nullptr;
   long long* seq_dev = nullptr;
   long long ro_seq = 0;               // the last read-out's number (0: none launched)
-  hipError_t wait_readout(long long target) const {
+  long long seq_min() const {          // the oldest filter's published number (one per filter)
     const volatile long long* p = seq_pin;
-    if (*p >= target) return hipSuccess;
+    long long v = p[0];
+    for (long long f = 1; f < F; ++f) v = p[f] < v ? p[f] : v;
+    return v;
+  }
+  hipError_t wait_readout(long long target) const {
+    if (seq_min() >= target) return hipSuccess;
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 1;; ++it) {
-      if (*p >= target) return hipSuccess;
+      if (seq_min() >= target) return hipSuccess;
       if ((it & 255) == 0) {
         std::this_thread::yield();
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
           // not published: whatever the device is doing, finish it and look once more
           const hipError_t e = hipDeviceSynchronize();
           if (e != hipSuccess) return e;
-          return *p >= target ? hipSuccess : hipErrorUnknown;
+          return seq_min() >= target ? hipSuccess : hipErrorUnknown;
         }
       } else {
         __builtin_ia32_pause();
@@ -972,14 +978,14 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
     }
     pf->ro_dev = (double*)rv;
     void* sv = nullptr;
-    if (F == 1 && std::getenv("GPMDM_RO_EVENT") == nullptr) {
-      if (hipHostMalloc((void**)&pf->seq_pin, sizeof(long long), hipHostMallocMapped | hipHostMallocCoherent) !=
+    if (std::getenv("GPMDM_RO_EVENT") == nullptr) {
+      if (hipHostMalloc((void**)&pf->seq_pin, sizeof(long long) * F, hipHostMallocMapped | hipHostMallocCoherent) !=
               hipSuccess ||
           hipHostGetDevicePointer(&sv, pf->seq_pin, 0) != hipSuccess) {
         delete pf;
         return fail(GPMDM_E_NOMEM, "mapped read-out number");
       }
-      *pf->seq_pin = 0;
+      for (long long f = 0; f < F; ++f) pf->seq_pin[f] = 0;
       pf->seq_dev = (long long*)sv;
     }
   }
@@ -1217,7 +1223,7 @@ int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   HIPCHK(hipEventRecord(pf->ro_ev, nullptr));
   HIPCHK(hipDeviceSynchronize());
   pf->ro_ev_ok = true;
-  if (pf->seq_pin) pf->ro_seq = *(volatile long long*)pf->seq_pin;   // (synchronised: nothing to wait for)
+  if (pf->seq_pin) pf->ro_seq = pf->seq_min();   // (synchronised: nothing to wait for)
   pf->initialised = true;
   pf->own_valid = false;               // no ancestors yet: identity ownership
   pf->rows_st = pf->rows_ll = nullptr;
@@ -1292,7 +1298,7 @@ int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes,
   HIPCHK(hipEventRecord(pf->ro_ev, nullptr));
   HIPCHK(hipDeviceSynchronize());
   pf->ro_ev_ok = true;
-  if (pf->seq_pin) pf->ro_seq = *(volatile long long*)pf->seq_pin;   // (synchronised: nothing to wait for)
+  if (pf->seq_pin) pf->ro_seq = pf->seq_min();   // (synchronised: nothing to wait for)
   pf->initialised = true;
   pf->switched = pf->propagated = pf->dyn_done = pf->gemm_ahead = false;
   return GPMDM_OK;
