@@ -1076,9 +1076,11 @@ __global__ __launch_bounds__(kB) void k_rows_ll(RowsLLArgs a) {
 // that sees the number sees the values (every storing thread's system-scope fence precedes
 // the barrier, the number's store follows it) -- gpmdm_pf_read then waits on host memory,
 // and no event record sits between the read-out and the next frame's switch.
-__device__ inline void publish_readout(const ResampleArgs& a, long long f, int tid) {
+// `stored`: this thread wrote host memory in this kernel (only those need the system-scope
+// fence, whose L2 write-back costs ~3 us a wave).
+__device__ inline void publish_readout(const ResampleArgs& a, long long f, int tid, bool stored) {
   if (!a.seq_host) return;              // (uniform over the workgroup)
-  __threadfence_system();
+  if (stored) __threadfence_system();
   __syncthreads();
   if (tid == 0) *(volatile long long*)(a.seq_host + f) = a.seq;
 }
@@ -1131,7 +1133,7 @@ __global__ __launch_bounds__(1024) void k_readout(ResampleArgs a) {
     readout[tid] = v;
     if (a.readout_host) a.readout_host[f * nro + tid] = v;
   }
-  publish_readout(a, f, tid);
+  publish_readout(a, f, tid, tid < nro);
 }
 
 
@@ -1346,7 +1348,7 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
     readout[tid] = v;
     if (a.readout_host) a.readout_host[f * nro + tid] = v;
   }
-  publish_readout(a, f, tid);
+  publish_readout(a, f, tid, true);   // (cls_host: any slot's thread)
 }
 
 // ---------------------------------------------------------------------------------
