@@ -411,30 +411,40 @@ struct gpmdm_pf {
   long long* seq_pin = nullptr;
   long long* seq_dev = nullptr;
   long long ro_seq = 0;               // the last read-out's number (0: none launched)
-  long long seq_min() const {          // the oldest filter's published number (one per filter)
-    const volatile long long* p = seq_pin;
+  long long seq_min() const { return min_mapped(seq_pin, F); }   // (one number per filter)
+  static long long min_mapped(const long long* q, long long n) {
+    const volatile long long* p = q;
     long long v = p[0];
-    for (long long f = 1; f < F; ++f) v = p[f] < v ? p[f] : v;
+    for (long long f = 1; f < n; ++f) v = p[f] < v ? p[f] : v;
     return v;
   }
-  hipError_t wait_readout(long long target) const {
-    if (seq_min() >= target) return hipSuccess;
+  // until every one of the n numbers at p is >= target (a number the device publishes after
+  // the data it guards)
+  static hipError_t wait_mapped(const long long* p, long long n, long long target) {
+    if (min_mapped(p, n) >= target) return hipSuccess;
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 1;; ++it) {
-      if (seq_min() >= target) return hipSuccess;
+      if (min_mapped(p, n) >= target) return hipSuccess;
       if ((it & 255) == 0) {
         std::this_thread::yield();
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
           // not published: whatever the device is doing, finish it and look once more
           const hipError_t e = hipDeviceSynchronize();
           if (e != hipSuccess) return e;
-          return seq_min() >= target ? hipSuccess : hipErrorUnknown;
+          return min_mapped(p, n) >= target ? hipSuccess : hipErrorUnknown;
         }
       } else {
         __builtin_ia32_pause();
       }
     }
   }
+  hipError_t wait_readout(long long target) const { return wait_mapped(seq_pin, F, target); }
+  // the switch's class counts (replay filters): k_scan_counts publishes cseq after writing
+  // them to cnt_pin, so the host's wait for them needs no event record behind the switch
+  long long* cseq_pin = nullptr;
+  long long* cseq_dev = nullptr;
+  long long cseq = 0;
+  bool pre_counts_seq = false;        // the pending pre-switch's counts come with cseq
   int zslot = 0;
   bool z_staged = false;              // zpin[zslot] holds the frame's z, k_dyn_finish copies it
   double *qdyn = nullptr, *mudyn = nullptr, *qobs = nullptr, *sobs = nullptr;
@@ -582,6 +592,7 @@ struct gpmdm_pf {
     for (auto ev : pool) (void)hipEventDestroy(ev);
     if (rpin) (void)hipHostFree(rpin);
     if (cnt_pin) (void)hipHostFree(cnt_pin);
+    if (cseq_pin) (void)hipHostFree(cseq_pin);
     if (rows_pin) (void)hipHostFree(rows_pin);
     if (cls_pin) (void)hipHostFree(cls_pin);
     if (cls_ev) (void)hipEventDestroy(cls_ev);
@@ -1020,6 +1031,16 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
       return fail(GPMDM_E_NOMEM, "pinned class-count buffer");
     }
     pf->cnt_dev = (int*)cv;
+    if (std::getenv("GPMDM_RO_EVENT") == nullptr) {
+      void* qv = nullptr;
+      if (hipHostMalloc((void**)&pf->cseq_pin, sizeof(long long), fl) != hipSuccess ||
+          hipHostGetDevicePointer(&qv, pf->cseq_pin, 0) != hipSuccess) {
+        delete pf;
+        return fail(GPMDM_E_NOMEM, "mapped class-count number");
+      }
+      *pf->cseq_pin = 0;
+      pf->cseq_dev = (long long*)qv;
+    }
     if (F == 1 && n_ranks == 1 && P <= kHostCountsMaxP) {
       void* lv = nullptr;
       if (hipHostMalloc((void**)&pf->cls_pin, sizeof(int) * P, fl) != hipSuccess ||
@@ -1435,6 +1456,10 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
     la.owner_reset = pf->owner;        // restores the preset for the next election
   }
   sc.counts_host = (class_counts || counts_ahead) ? pf->cnt_dev : nullptr;   // the counts straight to the host
+  if (sc.counts_host && pf->cseq_pin) {
+    sc.counts_seq_host = pf->cseq_dev;
+    sc.counts_seq = pf->cseq + 1;
+  }
   // the counts on the host (cls_pin): no wait for this switch
   // (GPMDM_NO_HOST_COUNTS=1: the device counts and the synchronisation, for A/B tests)
   static const bool no_host_counts = std::getenv("GPMDM_NO_HOST_COUNTS") != nullptr;
@@ -1462,6 +1487,9 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
     for (int c = 0; c < C; ++c) pf->cnt_expect[c] = cnt[c];
   }
   const bool small_path = launch_switch_group(sa, sc, ga, sa.owner ? &la : nullptr, !pf->owner_clean, s);
+  // (the one-launch small switch writes the counts without the number: an event then)
+  const bool counts_by_seq = sc.counts_seq_host && !small_path;
+  if (counts_by_seq) pf->cseq = sc.counts_seq;
   if (sa.owner) pf->owner_clean = !small_path;   // the small path presets in-kernel, leaves it dirty
   if (order_ahead) {
     // (pre-switch) the next resample's ownership order: its uniforms are keyed by the
@@ -1475,13 +1503,14 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
   HIPCHK(hipGetLastError());
   if (pf->rng_mode == GPMDM_RNG_REPLAY) HIPCHK(pf->draws_used(0, s));
   if (counts_ahead) {
-    HIPCHK(hipEventRecord(pf->cnt_done, s));
+    if (!counts_by_seq) HIPCHK(hipEventRecord(pf->cnt_done, s));
     if (pf->nloc > 0) {
       launch_dyn_gemm(pf, s);
       HIPCHK(hipGetLastError());
       pf->gemm_ahead = true;
     }
     pf->pre_counts = true;
+    pf->pre_counts_seq = counts_by_seq;
   } else if (host_counts) {
     if (!pf->seq_pin) HIPCHK(hipEventRecord(pf->cnt_ev, s));
     pf->cnt_check = true;
@@ -1496,11 +1525,11 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
     if (pf->cnt_done && pf->nloc > 0) {
       // the dynamics-GP tiles need the switch's tables, not the normals the caller draws
       // from these counts: they run while it draws (propagate launches the finish only)
-      HIPCHK(hipEventRecord(pf->cnt_done, s));
+      if (!counts_by_seq) HIPCHK(hipEventRecord(pf->cnt_done, s));
       launch_dyn_gemm(pf, s);
       HIPCHK(hipGetLastError());
       pf->gemm_ahead = true;
-      HIPCHK(hipEventSynchronize(pf->cnt_done));
+      HIPCHK(counts_by_seq ? gpmdm_pf::wait_mapped(pf->cseq_pin, 1, pf->cseq) : hipEventSynchronize(pf->cnt_done));
     } else {
       HIPCHK(hipStreamSynchronize(s));
     }
@@ -1524,7 +1553,8 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
     }
     pf->preswitched = false;
     if (class_counts && pf->pre_counts) {
-      HIPCHK(hipEventSynchronize(pf->cnt_done));   // the counts, not the tiles behind them
+      // the counts, not the tiles behind them
+      HIPCHK(pf->pre_counts_seq ? gpmdm_pf::wait_mapped(pf->cseq_pin, 1, pf->cseq) : hipEventSynchronize(pf->cnt_done));
       for (int c = 0; c < pf->m->C; ++c) class_counts[c] = pf->cnt_pin[c];
     } else if (class_counts) {
       int tmp[kMaxClasses];

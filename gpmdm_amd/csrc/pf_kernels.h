@@ -65,6 +65,8 @@ struct ScanArgs {
   int* class_start;               // C + 1
   int* counts;                    // C
   int* counts_host;               // C, or nullptr: the counts also into mapped host memory
+  long long* counts_seq_host;     // mapped: `counts_seq` published after counts_host (k_scan_counts)
+  long long counts_seq;
   int* seg_pos_begin;             // C
   int* seg_pos_end;               // C
   int* seg_out_base;              // C

@@ -177,6 +177,10 @@ __device__ __forceinline__ void scan_counts_body(const ScanArgs& a) {
       ts += (e0 - b0 + a.pt - 1) / a.pt;
       cs += tot[c];
     }
+    if (a.counts_seq_host) {            // the host waits on this number, not on an event
+      __threadfence_system();
+      *(volatile long long*)a.counts_seq_host = a.counts_seq;
+    }
     a.class_start[a.C] = cs;
     a.seg_tile_start[a.C] = ts;
   }
