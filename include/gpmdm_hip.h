@@ -276,9 +276,11 @@ int gpmdm_pf_step(gpmdm_pf_t pf, const double* z, const double* exp_draws,
                   const double* normals, const double* uniforms, void* stream);
 
 /* class_probabilities() / current_state_mean() / log_likelihood()
- * (gpmdm_pf.py:224-262, 215-222).  Waits for the last read-out (an event recorded after it,
- * so not for a pre-launched switch behind it), or synchronises `stream` when the read-outs
- * need a copy (banks of more than ~800 filters); any pointer may be NULL. */
+ * (gpmdm_pf.py:224-262, 215-222).  Waits for the last read-out -- the read-out kernels write
+ * it to mapped host memory and then publish a sequence number there, which this call waits
+ * on (GPMDM_RO_EVENT=1: an event recorded after the read-out), so not for a pre-launched
+ * switch behind it -- or synchronises `stream` when the read-outs need a copy (banks of more
+ * than ~800 filters); any pointer may be NULL. */
 int gpmdm_pf_read(gpmdm_pf_t pf, double* posterior, double* mean, double* lik, void* stream);
 
 /* Export the full particle state to host (any pointer may be NULL): states P x d,
