@@ -74,6 +74,14 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "particle-steps/sec (P×timesteps) + achieved HBM GB/s, N=2000 D=62 d=3"
 FP64_MFMA_PEAK_TFLOPS = 78.6          # MI355X spec (dense FP64 matrix); measured 77.1 (profiles/)
+# The reference's only published throughput for this path: P = 100 particles
+# at 12.78 frames/s on the author's laptop CPU (test_gpmdm_pf.ipynb:79, 259-260).  It is the
+# notebook's own configuration, not configs[1]'s N/P; vs_baseline divides by it and says so.
+PUBLISHED_PARTICLE_STEPS = 100 * 12.78
+PUBLISHED_BASIS = ("value / 1.278e3 particle-steps/s: the reference's published frame rate (12.78 FPS x P=100, "
+                   "author's laptop CPU, test_gpmdm_pf.ipynb:259-260; BASELINE.md §1) -- the only published "
+                   "throughput for this path, quoted at the notebook's own model and P, not configs[1]'s; "
+                   "cpu_baseline is the same-box comparison")
 # per-GPU particles: configs 4 and 5 are quoted on 8 GPUs
 P_PER_GPU = {1: 100, 2: 100_000, 3: 100_000, 4: 125_000, 5: 125_000}
 WORKLOAD = None
@@ -555,18 +563,54 @@ def launch(args, argv):
             log("[bench] no GPU visible")
             return 2
         backend = "gloo" if args.rehearse_gloo else "nccl"
+    import tempfile
+    import threading
     port = _free_port()
-    procs = []
+    logdir = Path(os.environ.get("GPMDM_BENCH_LOGDIR") or tempfile.mkdtemp(prefix="gpmdm_bench_"))
+    logdir.mkdir(parents=True, exist_ok=True)
+    procs, pumps = [], []
+    out_chunks = []                     # rank 0's stdout, drained while the workers run
+
+    def pump_stdout(pipe, path):
+        # Every rank's stdout is read as it is written (a pipe holds 64 KiB: a rank that
+        # writes more -- RCCL's own messages go to stdout -- would block until the launcher
+        # read it, i.e. forever).  Rank 0's is kept for its JSON line; every rank's also goes
+        # to its own log file.
+        with open(path, "wb") as f:
+            for chunk in iter(lambda: pipe.read1(65536), b""):
+                f.write(chunk)
+                if path.name == "rank0.stdout":
+                    out_chunks.append(chunk)
+
+    def pump_stderr(pipe, path, r):
+        # each rank's stderr to its own file, and forwarded line by line with a rank prefix
+        with open(path, "wb") as f:
+            for line in iter(pipe.readline, b""):
+                f.write(line)
+                f.flush()
+                try:
+                    sys.stderr.write(f"[rank {r}] " + line.decode(errors="replace"))
+                    sys.stderr.flush()
+                except Exception:   # noqa: BLE001  (a closed parent stderr must not stop the drain)
+                    pass
+
     for r in range(N):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(N), LOCAL_WORLD_SIZE=str(N),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    GPMDM_BENCH_BACKEND=backend, GPMDM_BENCH_LAUNCHER="bench.py")
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")    # dmabuf IPC (RCCL between processes)
-        procs.append(subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve()), *argv], env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+        p = subprocess.Popen([sys.executable, "-u", str(Path(__file__).resolve()), *argv], env=env,
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+        procs.append(p)
+        for target, a in ((pump_stdout, (p.stdout, logdir / f"rank{r}.stdout")),
+                          (pump_stderr, (p.stderr, logdir / f"rank{r}.stderr", r))):
+            t = threading.Thread(target=target, args=a, daemon=True)
+            t.start()
+            pumps.append(t)
+    log(f"[bench] {N} workers, per-rank logs in {logdir}")
     t0 = time.time()
     rc = 0
-    out = b""
+    failed = []
     try:
         live = set(range(N))
         while live:
@@ -575,6 +619,8 @@ def launch(args, argv):
                 if code is None:
                     continue
                 live.discard(r)
+                if code != 0:
+                    failed.append(r)
                 if code != 0 and rc == 0:
                     rc = code if code > 0 else 128 - code
                     log(f"[bench] worker rank {r} exited with status {code}: stopping the launch")
@@ -583,6 +629,7 @@ def launch(args, argv):
             if time.time() - t0 > args.launch_timeout:
                 log(f"[bench] launch exceeded {args.launch_timeout} s: stopping the workers")
                 rc = 124
+                failed.extend(r for r in range(N) if procs[r].poll() is None)
                 break
             time.sleep(0.2)
     finally:
@@ -594,9 +641,18 @@ def launch(args, argv):
                 p.wait(timeout=30)
             except Exception:
                 pass
-        if procs[0].stdout is not None:
-            out = procs[0].stdout.read()
+        for t in pumps:                 # the pipes close with their processes
+            t.join(timeout=30)
+    if rc != 0:
+        for r in sorted(set(failed)):
+            path = logdir / f"rank{r}.stderr"
+            try:
+                tail = path.read_bytes()[-4000:].decode(errors="replace")
+            except OSError:
+                tail = "(no log)"
+            log(f"[bench] ---- rank {r} stderr tail ({path}) ----\n{tail}")
     if rc == 0:
+        out = b"".join(out_chunks)
         lines = [ln for ln in out.decode(errors="replace").splitlines() if ln.startswith("{")]
         if len(lines) != 1:
             log(f"[bench] rank 0 printed {len(lines)} JSON lines, expected 1")
@@ -618,6 +674,16 @@ def plumbing_worker(args):
     dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.collective_timeout))
     if os.environ.get("GPMDM_PLUMBING_FAIL_RANK") == str(rank):   # tests: a worker that dies mid-run
         os._exit(3)
+    # tests: a worker that writes more than a pipe buffer to stdout / stderr before its line
+    # (RCCL's debug and warning output goes to stdout)
+    spam = int(os.environ.get("GPMDM_PLUMBING_SPAM_BYTES", "0"))
+    if spam:
+        row = f"NCCL INFO rank {rank}: " + "x" * 100 + "\n"
+        for _ in range(spam // len(row) + 1):
+            sys.stdout.write(row)
+            sys.stderr.write(row)
+        sys.stdout.flush()
+        sys.stderr.flush()
     try:
         x = np.arange(4096, dtype=np.float64)
         for _ in range(args.warmup):
@@ -893,7 +959,8 @@ def main():
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": None,
+        "vs_baseline": P_total * args.steps / elapsed / PUBLISHED_PARTICLE_STEPS,
+        "vs_baseline_basis": PUBLISHED_BASIS,
         "dtype": "f64",
         "data": "synthetic (SURVEY §8(d) generator; random-phase sinusoid mocap surrogate, PCA latents)",
         "config": {"workload": f"configs[{WORKLOAD['cfg'] - 1}]: N={N} D={D} d={d} C={model.n_classes}, "
@@ -955,12 +1022,19 @@ def main():
         rec["ms_per_frame_without_timing_events"] = {
             "value": untimed_ms, "note": "the next frames of the stream, same loop, no stage events "
                                          "(ms_per_step keeps the roofline kernel's two events per frame)"}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
+        # after every timed pass (the other ranks wait at the barrier below); at N > 1 the
+        # same per-GPU workload, so the N-GPU line carries the CPU baseline beside its value
         try:
             rec["cpu_baseline"] = cpu_baseline(data)
+            if world > 1:
+                rec["cpu_baseline"]["note"] = (f"rank 0's host, after the {world}-rank timed passes; the CPU "
+                                               f"sample is one GPU's share (P={P_local})")
         except Exception as e:  # the baseline is reported, never the target
             log(f"[bench] cpu baseline failed: {e!r}")
             rec["cpu_baseline"] = None
+    if dist is not None:
+        dist.barrier()
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if dist is not None:

@@ -407,20 +407,29 @@ struct gpmdm_pf {
   // their sequence numbers there (the read-out kernels publish them after the values:
   // publish_readout), and the host waits on them instead of on an event recorded behind the
   // read-out -- such a record idles the GPU ~6 us before the next frame's switch.
-  // GPMDM_RO_EVENT=1 keeps the event (A/B).
   long long* seq_pin = nullptr;
   long long* seq_dev = nullptr;
-  long long ro_seq = 0;               // the last read-out's number (0: none launched)
+  // the last read-out's number (0: none launched); atomic because gpmdm_pf_draws_free may
+  // run on a drawing thread while the frame's thread launches the next read-out
+  std::atomic<long long> ro_seq{0};
   long long seq_min() const { return min_mapped(seq_pin, F); }   // (one number per filter)
-  static long long min_mapped(const long long* q, long long n) {
-    const volatile long long* p = q;
-    long long v = p[0];
-    for (long long f = 1; f < n; ++f) v = p[f] < v ? p[f] : v;
+  // The numbers are read with ACQUIRE loads: the device publishes each with a system-scope
+  // release store after the values it guards (publish_seq, pf_kernels.hip), so a caller that
+  // has seen a number >= its target may then read those values with plain loads -- the
+  // acquire keeps the compiler (and the CPU) from moving them above the number's load.
+  static long long min_mapped(const long long* p, long long n) {
+    long long v = __atomic_load_n(p, __ATOMIC_ACQUIRE);
+    for (long long f = 1; f < n; ++f) {
+      const long long x = __atomic_load_n(p + f, __ATOMIC_ACQUIRE);
+      v = x < v ? x : v;
+    }
     return v;
   }
   // until every one of the n numbers at p is >= target (a number the device publishes after
-  // the data it guards)
-  static hipError_t wait_mapped(const long long* p, long long n, long long target) {
+  // the data it guards).  `s`: the stream the publishing kernel was launched on -- if the
+  // number has not appeared after 60 s, that stream is drained and the number looked at once
+  // more (an error, not a hang, if it is still missing).
+  static hipError_t wait_mapped(const long long* p, long long n, long long target, hipStream_t s) {
     if (min_mapped(p, n) >= target) return hipSuccess;
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 1;; ++it) {
@@ -428,8 +437,7 @@ struct gpmdm_pf {
       if ((it & 255) == 0) {
         std::this_thread::yield();
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) {
-          // not published: whatever the device is doing, finish it and look once more
-          const hipError_t e = hipDeviceSynchronize();
+          const hipError_t e = hipStreamSynchronize(s);
           if (e != hipSuccess) return e;
           return min_mapped(p, n) >= target ? hipSuccess : hipErrorUnknown;
         }
@@ -438,7 +446,10 @@ struct gpmdm_pf {
       }
     }
   }
-  hipError_t wait_readout(long long target) const { return wait_mapped(seq_pin, F, target); }
+  hipStream_t ro_stream = nullptr;    // the stream of the last read-out (its number's publisher)
+  hipStream_t cnt_stream = nullptr;   // the stream of the switch whose counts cseq guards
+  hipError_t wait_readout(long long target) const { return wait_mapped(seq_pin, F, target, ro_stream); }
+  hipError_t wait_counts() const { return wait_mapped(cseq_pin, 1, cseq, cnt_stream); }
   // the switch's class counts (replay filters): k_scan_counts publishes cseq after writing
   // them to cnt_pin, so the host's wait for them needs no event record behind the switch
   long long* cseq_pin = nullptr;
@@ -685,29 +696,6 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
     case GPMDM_TILE_64x512: obs_geo = dyn_geo = dynw_geo = kGeo64x512; break;
     case GPMDM_TILE_32x512: obs_geo = kGeo32x512; break;
     default: break;   // rejected by check_model_desc
-  }
-  // A/B override of the dynamics shapes ("nw,mt,ntw"; the extra ones need d <= 8): 16x256
-  // (4,1,4), 16x512 (4,1,8), 16x1024 (4,1,16), 32x256 (4,2,4), 32x512 (4,2,8),
-  // 32x1024 (8,2,8), 64x256 (4,4,4), 64x512 (8,4,4)
-  auto geo_env = [&](const char* name, TileGeo& g) -> bool {
-    const char* v = std::getenv(name);
-    if (!v) return true;
-    TileGeo t{};
-    if (std::sscanf(v, "%d,%d,%d", &t.nw, &t.mt, &t.ntw) != 3) return false;
-    const TileGeo ok[] = {kGeo16x256, {4, 1, 8}, {4, 1, 16}, kGeo32x256, kGeo32x512, {8, 2, 8},
-                          kGeo64x256, kGeo64x512};
-    for (const TileGeo& o : ok) {
-      if (o.nw != t.nw || o.mt != t.mt || o.ntw != t.ntw) continue;
-      const bool ab_only = (t.nw == 8 && t.mt <= 2) || (t.mt == 1 && t.ntw >= 8);   // launch_d: d <= 8
-      if (ab_only && d > 8) return false;
-      g = t;
-      return true;
-    }
-    return false;
-  };
-  if (!geo_env("GPMDM_DYN_GEO", dyn_geo) || !geo_env("GPMDM_DYNW_GEO", dynw_geo)) {
-    delete m;
-    return fail(GPMDM_E_INVALID, "GPMDM_DYN_GEO / GPMDM_DYNW_GEO: not a dynamics tile shape for this d");
   }
   int rc = build_image(m->obs, (int)m->N, d, m->D, desc->X, desc->y_lengthscales, nullptr,
                        desc->obs_R, desc->obs_beta, obs_geo);
@@ -989,16 +977,14 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
     }
     pf->ro_dev = (double*)rv;
     void* sv = nullptr;
-    if (std::getenv("GPMDM_RO_EVENT") == nullptr) {
-      if (hipHostMalloc((void**)&pf->seq_pin, sizeof(long long) * F, hipHostMallocMapped | hipHostMallocCoherent) !=
-              hipSuccess ||
-          hipHostGetDevicePointer(&sv, pf->seq_pin, 0) != hipSuccess) {
-        delete pf;
-        return fail(GPMDM_E_NOMEM, "mapped read-out number");
-      }
-      for (long long f = 0; f < F; ++f) pf->seq_pin[f] = 0;
-      pf->seq_dev = (long long*)sv;
+    if (hipHostMalloc((void**)&pf->seq_pin, sizeof(long long) * F, hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(&sv, pf->seq_pin, 0) != hipSuccess) {
+      delete pf;
+      return fail(GPMDM_E_NOMEM, "mapped read-out number");
     }
+    for (long long f = 0; f < F; ++f) pf->seq_pin[f] = 0;
+    pf->seq_dev = (long long*)sv;
   }
   {
     void* rv = nullptr;
@@ -1031,16 +1017,14 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
       return fail(GPMDM_E_NOMEM, "pinned class-count buffer");
     }
     pf->cnt_dev = (int*)cv;
-    if (std::getenv("GPMDM_RO_EVENT") == nullptr) {
-      void* qv = nullptr;
-      if (hipHostMalloc((void**)&pf->cseq_pin, sizeof(long long), fl) != hipSuccess ||
-          hipHostGetDevicePointer(&qv, pf->cseq_pin, 0) != hipSuccess) {
-        delete pf;
-        return fail(GPMDM_E_NOMEM, "mapped class-count number");
-      }
-      *pf->cseq_pin = 0;
-      pf->cseq_dev = (long long*)qv;
+    void* qv = nullptr;
+    if (hipHostMalloc((void**)&pf->cseq_pin, sizeof(long long), fl) != hipSuccess ||
+        hipHostGetDevicePointer(&qv, pf->cseq_pin, 0) != hipSuccess) {
+      delete pf;
+      return fail(GPMDM_E_NOMEM, "mapped class-count number");
     }
+    *pf->cseq_pin = 0;
+    pf->cseq_dev = (long long*)qv;
     if (F == 1 && n_ranks == 1 && P <= kHostCountsMaxP) {
       void* lv = nullptr;
       if (hipHostMalloc((void**)&pf->cls_pin, sizeof(int) * P, fl) != hipSuccess ||
@@ -1102,8 +1086,13 @@ int gpmdm_pf_draws_free(gpmdm_pf_t pf, int which) {
   CHECK(which >= 0 && which < 3, "which: 0 exp draws, 1 normals, 2 uniforms");
   HIPCHK(hipSetDevice(pf->m->device));
   HIPCHK(hipEventSynchronize(pf->rep_ev[which]));
-  if (pf->seq_pin && pf->rep_dev[which] && pf->rep_src[which] == pf->rep_dev[which])
+  if (pf->seq_pin && pf->rep_dev[which] && pf->rep_src[which] == pf->rep_dev[which]) {
     HIPCHK(pf->wait_readout(pf->ro_seq));   // last read in place: guarded by the read-out number (draws_used)
+    // a replay pre-switch launched after that read-out reads the Exp(1) draws in place too:
+    // its class counts (published after its switch) follow that read
+    if (which == 0 && pf->preswitched && pf->pre_counts)
+      HIPCHK(pf->pre_counts_seq ? pf->wait_counts() : hipEventSynchronize(pf->cnt_done));
+  }
   return GPMDM_OK;
 }
 
@@ -1327,36 +1316,27 @@ int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes,
 
 static void launch_dyn_gemm(gpmdm_pf* pf, hipStream_t s);
 
-// Rows from which the de-duplicated dynamics pass runs 32- / 64-row tiles of the 16 x 256
-// image (per rank, the last read frame's count; tools/dyn_family.sh).  GPMDM_DYN_MT=1|2|4
-// forces a height (A/B).
-constexpr int kDynMt2Rows = 1 << 30, kDynMt4Rows = 1 << 30;
 // Rows from which an AUTO de-duplicated pass runs on the wide image instead of the narrow
 // one -- only where the two give bitwise the same results (the 32 x 512 wide image reduces
 // each 256-column half in the 16 x 256 order: d <= 12), so the choice, made per rank from
-// its last read frame's rows, never changes a result.  GPMDM_DYN_WIDE_ROWS overrides (A/B).
+// its last read frame's rows, never changes a result.  GPMDM_DYN_WIDE_ROWS overrides (tests:
+// test_gpu_small_path.py forces every de-duplicated pass wide and compares bit for bit).
 constexpr int kDynWideRows = 32768;   // ~equal at 25k rows, wide 5% ahead at 100k (profiles/r04/dyn)
 
 static bool dyn_frame_wide(const gpmdm_pf* pf) {
   if (pf->dyn_tiles != GPMDM_DYN_TILES_AUTO || !pf->dedup) return pf->wide_dyn();
   const gpmdm_model* m = pf->m;
-  if (m->dynw.empty() || !m->dynw[0].split() || m->dyn[0].geo.nw != 4 || m->dyn[0].geo.ntw != 4) return false;
+  // (the per-half reduction that makes the images bitwise equal exists for d <= 12 only)
+  if (m->d > 12 || m->dynw.empty() || !m->dynw[0].split() || m->dyn[0].geo.nw != 4 || m->dyn[0].geo.ntw != 4)
+    return false;
   static const char* env = std::getenv("GPMDM_DYN_WIDE_ROWS");
   static const long long thr = env ? std::atoll(env) : kDynWideRows;
   return pf->rows_hint >= thr;
 }
 
-static TileGeo dyn_frame_geo(const gpmdm_pf* pf) {
-  const TileGeo g = pf->m->dyn_set(pf->dyn_wide_frame)[0].geo;
-  if (g.nw != kGeo16x256.nw || g.mt != kGeo16x256.mt || g.ntw != kGeo16x256.ntw) return g;
-  static const char* env = std::getenv("GPMDM_DYN_MT");
-  int mt = 1;
-  if (env && (env[0] == '1' || env[0] == '2' || env[0] == '4'))
-    mt = env[0] - '0';
-  else
-    mt = pf->rows_hint >= kDynMt4Rows ? 4 : (pf->rows_hint >= kDynMt2Rows ? 2 : 1);
-  return TileGeo{g.nw, mt, g.ntw};
-}
+// The frame's dynamics launch shape: the image's own (the 16 x 256 image at 32 or 64 rows per
+// workgroup lost at every row count measured, profiles/r04/dyn, and was removed).
+static TileGeo dyn_frame_geo(const gpmdm_pf* pf) { return pf->m->dyn_set(pf->dyn_wide_frame)[0].geo; }
 
 // counts_ahead (replay pre-switch): the class counts into mapped memory with cnt_done after
 // them, and the dynamics-GP tiles launched behind, without waiting.
@@ -1489,7 +1469,10 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
   const bool small_path = launch_switch_group(sa, sc, ga, sa.owner ? &la : nullptr, !pf->owner_clean, s);
   // (the one-launch small switch writes the counts without the number: an event then)
   const bool counts_by_seq = sc.counts_seq_host && !small_path;
-  if (counts_by_seq) pf->cseq = sc.counts_seq;
+  if (counts_by_seq) {
+    pf->cseq = sc.counts_seq;
+    pf->cnt_stream = s;
+  }
   if (sa.owner) pf->owner_clean = !small_path;   // the small path presets in-kernel, leaves it dirty
   if (order_ahead) {
     // (pre-switch) the next resample's ownership order: its uniforms are keyed by the
@@ -1529,7 +1512,7 @@ static int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipSt
       launch_dyn_gemm(pf, s);
       HIPCHK(hipGetLastError());
       pf->gemm_ahead = true;
-      HIPCHK(counts_by_seq ? gpmdm_pf::wait_mapped(pf->cseq_pin, 1, pf->cseq) : hipEventSynchronize(pf->cnt_done));
+      HIPCHK(counts_by_seq ? pf->wait_counts() : hipEventSynchronize(pf->cnt_done));
     } else {
       HIPCHK(hipStreamSynchronize(s));
     }
@@ -1554,7 +1537,7 @@ int gpmdm_pf_switch(gpmdm_pf_t pf, const double* E, int64_t* class_counts, void*
     pf->preswitched = false;
     if (class_counts && pf->pre_counts) {
       // the counts, not the tiles behind them
-      HIPCHK(pf->pre_counts_seq ? gpmdm_pf::wait_mapped(pf->cseq_pin, 1, pf->cseq) : hipEventSynchronize(pf->cnt_done));
+      HIPCHK(pf->pre_counts_seq ? pf->wait_counts() : hipEventSynchronize(pf->cnt_done));
       for (int c = 0; c < pf->m->C; ++c) class_counts[c] = pf->cnt_pin[c];
     } else if (class_counts) {
       int tmp[kMaxClasses];
@@ -1633,15 +1616,6 @@ static void launch_dyn_gemm(gpmdm_pf* pf, hipStream_t s) {
   const int C = m->C, d = m->d;
   const long long nl = pf->nloc;
   const std::vector<GpImage>& dset = m->dyn_set(pf->dyn_wide_frame);
-  // Diagnostic (GPMDM_DYN_EXACT_GRID=1): read the leader tile counts back (a host sync)
-  // and launch exactly the non-empty tiles instead of the device-unknown upper bound --
-  // measures what the empty workgroups of the bound cost.  Not the production schedule.
-  static const bool exact_grid = std::getenv("GPMDM_DYN_EXACT_GRID") != nullptr;
-  int ltiles[kMaxClasses + 1] = {0};
-  if (exact_grid && pf->dedup) {
-    (void)hipMemcpyAsync(ltiles, pf->lseg_tiles(), sizeof(int) * (C + 1), hipMemcpyDeviceToHost, s);
-    (void)hipStreamSynchronize(s);
-  }
   hipEvent_t t0;
   pf->mark_begin(s, GPMDM_STAGE_DYN_GEMM, t0);
   for (int c0 = 0; c0 < C; c0 += kMaxSeg) {
@@ -1654,8 +1628,10 @@ static void launch_dyn_gemm(gpmdm_pf* pf, hipStream_t s) {
     }
     tp.n_seg = ns;
     tp.geo = pf->dyn_geo_frame;      // tile starts computed on the device in units of pt
+    // an upper bound (the leaders' tile count is known on the device only): the empty
+    // workgroups map last and exit at once (an exact grid read back measured no faster,
+    // DESIGN.md §3 "Dynamics tiles")
     tp.tiles_ub = (int)(cdiv(nl, tp.geo.pt()) + ns);
-    if (exact_grid && pf->dedup) tp.tiles_ub = std::max(ltiles[c0 + ns] - ltiles[c0], 1);
     tp.n_j_max = njm;
     if (pf->dedup) {                  // one row per (ancestor, class) leader
       tp.seg_pos_begin = pf->lseg_begin() + c0;
@@ -2166,10 +2142,8 @@ static int launch_unpack_rows(gpmdm_pf* pf, const double* recv, int part, const 
 
 // Exchanged rows are read in place by the next resample (gpmdm_pf.rows_*) when it runs the
 // multi-kernel path (the one-workgroup small path reads the unpacked arrays).
-// GPMDM_NO_ROWS_IN_PLACE=1 unpacks at once (A/B).
 static bool rows_in_place(gpmdm_pf* pf) {
-  static const bool off = std::getenv("GPMDM_NO_ROWS_IN_PLACE") != nullptr;
-  return !off && pf->F == 1 && !small_resample_ok(norm_args(pf), resample_args(pf));
+  return pf->F == 1 && !small_resample_ok(norm_args(pf), resample_args(pf));
 }
 
 static int unpack_part(gpmdm_pf* pf, const double* recv, int part, hipStream_t s) {
@@ -2236,6 +2210,7 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   if (pf->seq_pin) {                   // the read-out's number, published after it
     ra.seq_host = pf->seq_dev;
     ra.seq = ++pf->ro_seq;
+    pf->ro_stream = s;
   }
   ra.U = pf->rng_mode == GPMDM_RNG_REPLAY ? pf->rep_src[2] : nullptr;
   NormArgs na = norm_args(pf);
@@ -2295,8 +2270,7 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   pf->frame += 1;
   pf->propagated = false;
   if (pf->preswitch) {                 // the next frame's switch, behind the read-out
-    static const bool no_ahead = std::getenv("GPMDM_NO_ORDER_AHEAD") != nullptr;   // A/B
-    TRY(do_switch(pf, nullptr, nullptr, s, pf->order_wanted() && !no_ahead));
+    TRY(do_switch(pf, nullptr, nullptr, s, pf->order_wanted()));
     pf->sw_stream = s;
     pf->preswitched = true;
   }
@@ -2333,7 +2307,7 @@ int gpmdm_pf_read(gpmdm_pf_t pf, double* post, double* mean, double* lik, void* 
   } else {
     HIPCHK(hipStreamSynchronize(s));
   }
-  pf->rows_hint = *(volatile int*)pf->rows_pin;   // its dynamics pass has run (the read-out follows it)
+  pf->rows_hint = __atomic_load_n(pf->rows_pin, __ATOMIC_RELAXED);   // its dynamics pass has run (the read-out follows it)
   for (int f = 0; f < pf->F; ++f) {
     const double* b = src + (size_t)f * nr;
     if (post) std::memcpy(post + (size_t)f * m->C, b, sizeof(double) * m->C);

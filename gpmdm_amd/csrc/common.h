@@ -85,6 +85,15 @@ __device__ __forceinline__ double ord_dec(unsigned long long u) {
   return __longlong_as_double((long long)v);
 }
 
+// Publish a sequence number the host polls in mapped (fine-grained) host memory: a
+// system-scope release store -- everything this thread's program order and the stream's
+// earlier kernels wrote before it is visible to a host that observes the number with an
+// acquire load (capi.hip gpmdm_pf::min_mapped).  A vector store with release semantics (the
+// compiler emits the system-scope fence sequence in front of it); never a volatile plain store.
+__device__ __forceinline__ void publish_seq(long long* p, long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Wave (64-lane) reductions.
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll

@@ -730,28 +730,12 @@ void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
   // 1037 ms; the default 64 x 512 shape: 760 ms; profiles/r02/ablations/tb9, tb10)
   constexpr int kCoordVar = DI > 12 ? kTileCoordLDS : 0;
   if (dyn) {
-    // A/B shapes for the dynamics GPs (GPMDM_DYN_GEO / GPMDM_DYNW_GEO, capi.hip; d <= 8):
-    // 32 x 1024 (8 waves), 16 x 512, 16 x 1024 (4 waves x 16 column tiles)
-    if constexpr (DI <= 8) {
-      if (g.nw == 8 && g.mt == 2) {
-        hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 8, 2, 8>), grid, dim3(512), 0, stream, p);
-        return;
-      }
-      if (g.nw == 4 && g.mt == 1 && g.ntw == 8) {
-        hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 1, 8>), grid, dim3(256), 0, stream, p);
-        return;
-      }
-      if (g.nw == 4 && g.mt == 1 && g.ntw == 16) {
-        hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 1, 16>), grid, dim3(256), 0, stream, p);
-        return;
-      }
-    }
+    // dynamics images: narrow 16 x 256, wide = the observation GP's shape, or a model-wide
+    // tile_shape (64 x 256 / 64 x 512)
     if (g.nw == 8)
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 8>), grid, dim3(512), 0, stream, p);
     else if (g.mt == 2 && g.ntw == 8)
       hipLaunchKernelGGL((k_gp_tile<DI, true, kCoordVar, 4, 2, 8>), grid, dim3(256), 0, stream, p);
-    else if (g.mt == 2)
-      hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 2, 4>), grid, dim3(256), 0, stream, p);
     else if (g.mt == 1)
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 1, 4>), grid, dim3(256), 0, stream, p);
     else

@@ -177,10 +177,8 @@ __device__ __forceinline__ void scan_counts_body(const ScanArgs& a) {
       ts += (e0 - b0 + a.pt - 1) / a.pt;
       cs += tot[c];
     }
-    if (a.counts_seq_host) {            // the host waits on this number, not on an event
-      __threadfence_system();
-      *(volatile long long*)a.counts_seq_host = a.counts_seq;
-    }
+    if (a.counts_seq_host)              // the host waits on this number, not on an event
+      publish_seq(a.counts_seq_host, a.counts_seq);   // (this thread wrote counts_host above)
     a.class_start[a.C] = cs;
     a.seg_tile_start[a.C] = ts;
   }
@@ -1077,16 +1075,24 @@ __global__ __launch_bounds__(kB) void k_rows_ll(RowsLLArgs a) {
 }
 
 // The read-out is in mapped host memory: publish its sequence number after it, so the host
-// that sees the number sees the values (every storing thread's system-scope fence precedes
-// the barrier, the number's store follows it) -- gpmdm_pf_read then waits on host memory,
-// and no event record sits between the read-out and the next frame's switch.
+// that sees the number sees the values -- gpmdm_pf_read then waits on host memory, and no
+// event record sits between the read-out and the next frame's switch.  The protocol
+// (DESIGN.md §1 "Mapped-memory handshake"):
+//  * every other thread that wrote host memory in this kernel issues a system-scope fence
+//    before the workgroup barrier (its stores are performed at system scope first);
+//  * thread 0, after the barrier, publishes the number with a system-scope RELEASE store
+//    (publish_seq): it orders thread 0's own stores, and everything that happens-before it
+//    -- the other threads' fenced stores through the barrier, and every earlier kernel of
+//    the stream (k_dyn_finish's row count) -- before the number;
+//  * the host polls with ACQUIRE loads (gpmdm_pf::min_mapped), so its later plain loads of
+//    the guarded values cannot be hoisted above the number.
 // `stored`: this thread wrote host memory in this kernel (only those need the system-scope
-// fence, whose L2 write-back costs ~3 us a wave).
+// fence, whose L2 write-back costs ~3 us a wave; thread 0's release store includes its own).
 __device__ inline void publish_readout(const ResampleArgs& a, long long f, int tid, bool stored) {
   if (!a.seq_host) return;              // (uniform over the workgroup)
-  if (stored) __threadfence_system();
+  if (stored && tid != 0) __threadfence_system();
   __syncthreads();
-  if (tid == 0) *(volatile long long*)(a.seq_host + f) = a.seq;
+  if (tid == 0) publish_seq(a.seq_host + f, a.seq);
 }
 
 __global__ __launch_bounds__(1024) void k_readout(ResampleArgs a) {

@@ -150,7 +150,10 @@ int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes,
  * Passing these very pointers to gpmdm_pf_switch / gpmdm_pf_propagate / gpmdm_pf_resample
  * skips the copy into staging.  A buffer may be written only when gpmdm_pf_draws_free
  * (which = 0, 1, 2) has returned: it waits until the launches that read the buffer's last
- * contents have run. */
+ * contents have run (a pending replay pre-switch included).  It may be called from another
+ * thread than the one stepping the filter (a host drawing ahead) when the buffer is copied
+ * to the device (a buffer of more than 32 KB); for smaller, in-place buffers call it
+ * from the stepping thread (it reads the pre-switch's bookkeeping). */
 int gpmdm_pf_draw_buffers(gpmdm_pf_t pf, double** exp_draws, double** normals, double** uniforms);
 int gpmdm_pf_draws_free(gpmdm_pf_t pf, int which);
 
