@@ -42,7 +42,7 @@ Prints ONE JSON line (rank 0) with the contract fields plus:
                 per particle; SURVEY §8(d)'s dense 2N^2 + 2ND is reported beside it) / mean
                 launch time from HIP events on the launch stream; traffic = HBM bytes per
                 launch of the same kernel from the committed rocprofv3 PMC passes of this
-                bench command (profiles/r04_pmc_summary.json; its "commit" field names the
+                bench command (profiles/r05_pmc_summary.json; its "commit" field names the
                 build it measured -- the driver's bench run has no profiler attached), or null
   cpu_baseline  the CPU oracle (numpy fp64) on this configuration's own particle count
                 for N <= 2000 (a bounded sample of frames), a 1000-particle sample above;
@@ -149,7 +149,7 @@ def obs_model_bytes(N, D):
 def pmc_traffic(cfg):
     """(HBM bytes per launch of the obs tile kernel, source note) from the committed
     rocprofv3 PMC summary of this bench command (tools/pmc_passes.sh + tools/pmc_summary.py)."""
-    for name in ("r04_pmc_summary.json", "r03_pmc_summary.json", "r02_pmc_summary.json", "pmc_summary.json"):
+    for name in ("r05_pmc_summary.json", "r04_pmc_summary.json", "r03_pmc_summary.json", "r02_pmc_summary.json", "pmc_summary.json"):
         p = ROOT / "profiles" / name
         if not p.exists():
             continue

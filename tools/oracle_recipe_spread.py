@@ -1,0 +1,130 @@
+"""How far apart two correct fp64 evaluations of the filter's weights are at configs[2] / [4].
+
+    python tools/oracle_recipe_spread.py [--config 3] [--P 2000] [--out profiles/r05/oracle_recipe_spread.json]
+
+The large-config parity tests check the GPU's weights against the oracle with the observation
+GP factored by Cholesky solves (OracleModel.precompute("cholesky")), while the reference forms
+the explicit inverse K_y^-1 = U^-1 U^-T (gpmdm.py:1284-1305) and the GPU uses R = U^-1 (the same
+recipe, triangular form).  This script evaluates one filter step's log-likelihoods and weights
+with BOTH oracle recipes on the same particle cloud and reports their spread -- the floor any
+fp64 implementation's weights can be held to against either oracle.  The cloud: the oracle's
+own filter run from the reference's initialisation for two warm-up steps (seeded draws), then
+the third step's propagated states (gpmdm_pf.py:153-204).  CPU only (numpy BLAS threads).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def nrel(a, b):
+    return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / max(np.linalg.norm(np.asarray(b)), 1e-300))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--P", type=int, default=2000)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    from gpmdm_amd import synthetic
+    from oracle import gpmdm_oracle as O
+    c = synthetic.CONFIGS[a.config]
+    data = synthetic.make_sequences(c["C"], c["S"], c["L"], c["D"], c["d"], seed=0)
+    hp = synthetic.default_hyperparameters(c["D"], c["d"], 0.1)
+    # CPU only: the latents by PCA of Y as bench.py's cpu_baseline builds them (the GPU model's
+    # init_X is the same PCA up to sign; the spread does not depend on which)
+    from sklearn.decomposition import PCA
+    Y = np.concatenate([y for cl in data.sequences for y in cl]).astype(np.float64)
+    X = PCA(n_components=c["d"]).fit_transform(Y)
+    kw = dict(X=X, Y=Y, seq_lengths=[[c["L"]] * c["S"]] * c["C"],
+              y_log_lengthscales=np.log(hp["y_lengthscales_init"]), y_log_lambdas=np.log(hp["y_lambdas_init"]),
+              y_log_sigma_n=np.log(0.1), x_log_lengthscales=np.log(hp["x_lengthscales_init"]),
+              x_log_lambdas=np.log(hp["x_lambdas_init"]), x_log_sigma_n=np.log(0.1),
+              x_log_lin_coeff=np.log(hp["x_lin_coeff_init"]))
+    t0 = time.perf_counter()
+    om_c = O.OracleModel(**kw).precompute("cholesky")
+    t_c = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    om_i = O.OracleModel(**kw).precompute("inverse")
+    t_i = time.perf_counter() - t0
+    # a third: K_y perturbed symmetrically at the rounding level (relative 2^-53 per entry),
+    # Cholesky solves -- a backward-stable factorisation of K_y is the exact factorisation of
+    # such a matrix, so this spread is the floor two correct fp64 factorisations sit apart
+    Ky = O.rbf_kernel(X, X, kw["y_log_lengthscales"], kw["y_log_sigma_n"], 0.0, noise=True)
+    prng = np.random.RandomState(77)
+    Dp = prng.uniform(-1.0, 1.0, Ky.shape)
+    Dp = np.triu(Dp) + np.triu(Dp, 1).T
+    Kp = Ky * (1.0 + 2.0 ** -53 * Dp)
+    del Ky, Dp
+    from scipy.linalg import cho_factor, cho_solve
+    om_p = O.OracleModel(**kw).precompute("cholesky")
+    L, _ = cho_factor(Kp, lower=True, overwrite_a=True, check_finite=False)
+    om_p.Ly = np.tril(L)
+    om_p.beta_y = cho_solve((om_p.Ly, True), Y, check_finite=False)
+    del Kp, L
+    C, d, P = c["C"], c["d"], a.P
+    T = synthetic.markov_matrix(C)
+    rng = np.random.RandomState(a.config)
+    parts = [rng.randint(0, om_c.X_for_class(k).shape[0], P // C + (k < P % C)) for k in range(C)]
+    s, cl = O.init_particles(om_c, P, parts)
+    zs = data.observation_stream(4, seed=1)
+    for k in range(2):
+        r = O.step(om_c, T, s, cl, zs[k], rng.exponential(size=(P, C)), rng.randn(P, d), rng.rand(P))
+        s, cl = r.states, r.classes
+    E, nrm, u = rng.exponential(size=(P, C)), rng.randn(P, d), rng.rand(P)
+    rc = O.step(om_c, T, s, cl, zs[2], E, nrm, u)
+    ri = O.step(om_i, T, s, cl, zs[2], E, nrm, u)
+    # the same propagated states through both observation maps (the dynamics GPs are the same recipe)
+    ll_c = O.log_likelihoods(om_c, rc.states_propagated, zs[2])
+    ll_i = O.log_likelihoods(om_i, rc.states_propagated, zs[2])
+    ll_p = O.log_likelihoods(om_p, rc.states_propagated, zs[2])
+    _, w_c = O.normalise(ll_c)
+    _, w_i = O.normalise(ll_i)
+    _, w_p = O.normalise(ll_p)
+    # sensitivity of the weights to the propagated states: the states perturbed at relative
+    # eps (per coordinate, seeded) -- what a dynamics-GP mean that agrees to eps does to the
+    # weights (the GPU's dynamics maps agree with the oracle's to ~1e-9..1e-8 normwise)
+    sens = {}
+    srng = np.random.RandomState(78)
+    for eps in (1e-12, 1e-10, 1e-9, 1e-8):
+        sp = rc.states_propagated * (1.0 + eps * srng.uniform(-1.0, 1.0, rc.states_propagated.shape))
+        _, w_s = O.normalise(O.log_likelihoods(om_c, sp, zs[2]))
+        sens[f"{eps:g}"] = nrel(w_s, w_c)
+    mu_c, var_c = om_c.map_x_to_y(rc.states_propagated)
+    mu_i, var_i = om_i.map_x_to_y(rc.states_propagated)
+    out = {
+        "config": a.config, "N": int(om_c.X.shape[0]), "D": int(om_c.D), "d": d, "C": C, "P": P,
+        "precompute_s": {"cholesky": t_c, "inverse": t_i},
+        "weights_nrel_inverse_vs_cholesky": nrel(w_i, w_c),
+        "weights_maxabs_inverse_vs_cholesky": float(np.max(np.abs(w_i - w_c))),
+        "ll_nrel_inverse_vs_cholesky": nrel(ll_i, ll_c),
+        "ll_maxabs_inverse_vs_cholesky": float(np.max(np.abs(ll_i - ll_c))),
+        "weights_nrel_perturbed_vs_cholesky": nrel(w_p, w_c),
+        "ll_nrel_perturbed_vs_cholesky": nrel(ll_p, ll_c),
+        "ll_maxabs_perturbed_vs_cholesky": float(np.max(np.abs(ll_p - ll_c))),
+        "weights_nrel_vs_state_perturbation": sens,
+        "obs_var_nrel": nrel(var_i, var_c), "obs_mean_nrel": nrel(mu_i, mu_c),
+        "step_weights_nrel": nrel(ri.w, rc.w), "step_states_equal": bool(np.array_equal(ri.states, rc.states)),
+        "ess_frac": float(1.0 / np.sum(w_c * w_c) / P),
+        "note": "fp64 oracle recipes of the same observation GP on the same cloud: explicit U^-1 U^-T "
+                "(the reference's, gpmdm.py:1284-1305) vs Cholesky solves (the large-config tests' oracle), "
+                "and Cholesky solves of K_y perturbed at relative 2^-53 per entry (symmetric, seeded): the "
+                "spread between two backward-stable factorisations of the same matrix",
+    }
+    print(json.dumps(out, indent=1))
+    if a.out:
+        Path(a.out).parent.mkdir(parents=True, exist_ok=True)
+        Path(a.out).write_text(json.dumps(out, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()
