@@ -109,6 +109,7 @@ class OracleModel:
     Xin_c: list = field(default=None, repr=False)
     Xout_c: list = field(default=None, repr=False)
     Kx_inv_c: list = field(default=None, repr=False)
+    Kx_R_c: list = field(default=None, repr=False)
 
     @property
     def n_classes(self):
@@ -142,14 +143,23 @@ class OracleModel:
                 off += L
         return np.concatenate(Xin), np.concatenate(Xout), np.concatenate(cls)
 
-    def precompute(self, obs_factor: str = "inverse"):
+    def precompute(self, obs_factor: str = "inverse", dyn_form: str = "inverse"):
         """gpmdm.py:1284-1305 (class blocks only for the dynamics inverse).
 
         ``obs_factor="cholesky"`` keeps the lower Cholesky factor L of K_y instead of the
         explicit inverse and evaluates the observation map with triangular solves
         (``k^T K_y^-1 k = |L^-1 k|^2``, mean weights ``K_y^-1 Y`` by two solves): the same
         mathematics with a third of the O(N^3) setup, for the N = 10^4 / 2 x 10^4
-        configurations where the explicit recipe would dominate a test's run time."""
+        configurations where the explicit recipe would dominate a test's run time.
+
+        ``dyn_form="triangular"`` evaluates the dynamics GP's quadratic form as |R_c^T k|^2
+        with R_c = U_c^-1 (the same Cholesky recipe, gpmdm.py:1299-1305: A_c = R_c R_c^T) and
+        the linear kernel folded into H = (X~in C^2)^T R_c (k^T R_c = k_rbf^T R_c + x~^T H):
+        the same mathematics in another fp64 association.  The dynamics variance
+        vc = k_diag - k^T A_c k cancels (k_diag carries the linear kernel's diagonal, ~1e2 at
+        config 3), so the two associations differ by ~1e-7..1e-6 relative in vc and ~1e-6 in
+        the next weights (tools/oracle_recipe_spread.py): the large-config tests check the
+        device, which uses the triangular association, against both forms."""
         Ky = rbf_kernel(self.X, self.X, self.y_log_lengthscales, self.y_log_sigma_n,
                         self.sigma_n_num_Y, noise=True)
         self.Ly = None
@@ -162,7 +172,7 @@ class OracleModel:
             self.Ky_inv = chol_inverse(Ky)
         del Ky
         Xin, Xout, cls = self.xin_xout()
-        self.Xin_c, self.Xout_c, self.Kx_inv_c = [], [], []
+        self.Xin_c, self.Xout_c, self.Kx_inv_c, self.Kx_R_c = [], [], [], []
         for c in range(self.n_classes):
             m = cls == c
             xi, xo = Xin[m], Xout[m]
@@ -172,8 +182,28 @@ class OracleModel:
             K = K + 1e-6 * np.eye(K.shape[0])
             self.Xin_c.append(xi)
             self.Xout_c.append(xo)
-            self.Kx_inv_c.append(chol_inverse(K))
+            if dyn_form == "triangular":
+                Rc = np.linalg.inv(np.linalg.cholesky(K).T)            # U^-1, upper
+                self.Kx_R_c.append(Rc)
+                self.Kx_inv_c.append(Rc @ Rc.T)
+            else:
+                self.Kx_inv_c.append(chol_inverse(K))
         return self
+
+    def with_triangular_dynamics(self):
+        """A copy sharing this model's observation factor whose dynamics GPs use the
+        triangular association (precompute's ``dyn_form="triangular"``)."""
+        import copy
+        o = copy.copy(self)
+        o.Kx_R_c, o.Kx_inv_c = [], []
+        for c in range(self.n_classes):
+            xi = self.Xin_c[c]
+            K = rbf_kernel(xi, xi, self.x_log_lengthscales, self.x_log_sigma_n, self.sigma_n_num_X, noise=True)
+            K = K + lin_kernel(xi, xi, self.x_log_lin_coeff) + 1e-6 * np.eye(K.shape[0])
+            Rc = np.linalg.inv(np.linalg.cholesky(K).T)
+            o.Kx_R_c.append(Rc)
+            o.Kx_inv_c.append(Rc @ Rc.T)
+        return o
 
     # -- predictive maps ------------------------------------------------------
 
@@ -197,7 +227,15 @@ class OracleModel:
         Ks = rbf_kernel(xi, Xs, self.x_log_lengthscales) + lin_kernel(xi, Xs, self.x_log_lin_coeff)
         kd = x_diag_kernel(Xs, self.x_log_lin_coeff)
         mean = ((xo.T @ A) @ Ks).T
-        vc = kd - np.sum((Ks.T @ A) * Ks.T, axis=1)
+        if getattr(self, "Kx_R_c", None):                # precompute(dyn_form="triangular")
+            R = self.Kx_R_c[c]
+            c2 = np.exp(self.x_log_lin_coeff) ** 2
+            xt_in = np.concatenate([xi, np.ones((xi.shape[0], 1))], 1)
+            xt = np.concatenate([Xs, np.ones((Xs.shape[0], 1))], 1)
+            V = rbf_kernel(xi, Xs, self.x_log_lengthscales).T @ R + xt @ ((xt_in * c2).T @ R)
+            vc = kd - np.sum(V * V, axis=1)
+        else:
+            vc = kd - np.sum((Ks.T @ A) * Ks.T, axis=1)
         lam = np.exp(self.x_log_lambdas) ** -2
         return mean, vc[:, None] * lam[None, :]
 

@@ -99,6 +99,46 @@ def main():
         sp = rc.states_propagated * (1.0 + eps * srng.uniform(-1.0, 1.0, rc.states_propagated.shape))
         _, w_s = O.normalise(O.log_likelihoods(om_c, sp, zs[2]))
         sens[f"{eps:g}"] = nrel(w_s, w_c)
+    # the dynamics GP's linear kernel folded into H = (X~in C^2)^T alpha (the GPU's association,
+    # gp_tile.h: mu = K_rbf alpha + x~^T H) instead of (K_rbf + K_lin) then alpha (the oracle's /
+    # reference's): propagated states and weights of the same step
+    def dyn_map_h(Xs, k):
+        xi, xo, A = om_c.Xin_c[k], om_c.Xout_c[k], om_c.Kx_inv_c[k]
+        alpha = A @ xo
+        c2 = np.exp(om_c.x_log_lin_coeff) ** 2
+        xt_in = np.concatenate([xi, np.ones((xi.shape[0], 1))], 1)
+        H = (xt_in * c2).T @ alpha
+        xt = np.concatenate([Xs, np.ones((Xs.shape[0], 1))], 1)
+        return O.rbf_kernel(Xs, xi, om_c.x_log_lengthscales) @ alpha + xt @ H
+    def dyn_var_r(Xs, k):
+        # vc = k_diag - |R^T k|^2 with R = U^-1 (the GPU's triangular form) and the linear
+        # kernel folded into H_R = (X~in C^2)^T R
+        xi = om_c.Xin_c[k]
+        K = (O.rbf_kernel(xi, xi, om_c.x_log_lengthscales, om_c.x_log_sigma_n, 0.0, noise=True)
+             + O.lin_kernel(xi, xi, om_c.x_log_lin_coeff) + 1e-6 * np.eye(xi.shape[0]))
+        R = np.linalg.inv(np.linalg.cholesky(K).T)
+        c2 = np.exp(om_c.x_log_lin_coeff) ** 2
+        xt_in = np.concatenate([xi, np.ones((xi.shape[0], 1))], 1)
+        xt = np.concatenate([Xs, np.ones((Xs.shape[0], 1))], 1)
+        V = O.rbf_kernel(Xs, xi, om_c.x_log_lengthscales) @ R + xt @ ((xt_in * c2).T @ R)
+        vc = O.x_diag_kernel(Xs, om_c.x_log_lin_coeff) - np.sum(V * V, axis=1)
+        return vc[:, None] * (np.exp(om_c.x_log_lambdas) ** -2)[None, :]
+    prop_h = rc.states_propagated.copy()
+    prop_v = rc.states_propagated.copy()
+    var_spread = []
+    for k in range(C):
+        sel = rc.classes_switched == k
+        if sel.any():
+            mu_o, var_o = om_c.map_x_dynamics_for_class(s[sel], k)
+            prop_h[sel] += dyn_map_h(s[sel], k) - mu_o
+            var_r = dyn_var_r(s[sel], k)
+            var_spread.append(nrel(var_r, var_o))
+            prop_v[sel] = mu_o + (rc.states_propagated[sel] - mu_o) * np.sqrt(var_r / var_o)   # same normals
+    _, w_h = O.normalise(O.log_likelihoods(om_c, prop_h, zs[2]))
+    _, w_v = O.normalise(O.log_likelihoods(om_c, prop_v, zs[2]))
+    dyn_assoc = {"mean_H_form": {"states_nrel": nrel(prop_h, rc.states_propagated), "weights_nrel": nrel(w_h, w_c)},
+                 "var_R_form": {"var_nrel_per_class": var_spread,
+                                "states_nrel": nrel(prop_v, rc.states_propagated), "weights_nrel": nrel(w_v, w_c)}}
     mu_c, var_c = om_c.map_x_to_y(rc.states_propagated)
     mu_i, var_i = om_i.map_x_to_y(rc.states_propagated)
     out = {
@@ -112,6 +152,7 @@ def main():
         "ll_nrel_perturbed_vs_cholesky": nrel(ll_p, ll_c),
         "ll_maxabs_perturbed_vs_cholesky": float(np.max(np.abs(ll_p - ll_c))),
         "weights_nrel_vs_state_perturbation": sens,
+        "dynamics_linear_kernel_association": dyn_assoc,
         "obs_var_nrel": nrel(var_i, var_c), "obs_mean_nrel": nrel(mu_i, mu_c),
         "step_weights_nrel": nrel(ri.w, rc.w), "step_states_equal": bool(np.array_equal(ri.states, rc.states)),
         "ess_frac": float(1.0 / np.sum(w_c * w_c) / P),
