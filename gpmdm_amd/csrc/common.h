@@ -13,7 +13,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 struct SegDesc {                  // one GP: the observation GP, or the class-c dynamics GP
   const double* Xrec;             // row_cap(n_rows) x (d + 1): row records [Xs_i, |Xs_i|^2 * 64/ln2]
   const double* Hf;               // dyn only: H = (Xin C^2)^T B, (d+1) x cols, fragment order
-  const double* Bf;               // B = [triu(R) | M] in fragment order (see capi.hip)
+  const double* Bf;               // B = [triu(R) | M] in fragment order (see capi_model.hip build_image)
   int n_rows;                     // training rows = R columns
   int n_m;                        // mean columns (D or d)
   int n_j;                        // column blocks
@@ -88,7 +88,7 @@ __device__ __forceinline__ double ord_dec(unsigned long long u) {
 // Publish a sequence number the host polls in mapped (fine-grained) host memory: a
 // system-scope release store -- everything this thread's program order and the stream's
 // earlier kernels wrote before it is visible to a host that observes the number with an
-// acquire load (capi.hip gpmdm_pf::min_mapped).  A vector store with release semantics (the
+// acquire load (capi_internal.h gpmdm_pf::min_mapped).  A vector store with release semantics (the
 // compiler emits the system-scope fence sequence in front of it); never a volatile plain store.
 __device__ __forceinline__ void publish_seq(long long* p, long long v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -743,10 +743,10 @@ void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
   } else if (g.mt == 2) {
     hipLaunchKernelGGL((k_gp_tile<DI, false, kCoordVar, 4, 2, 8>), grid, dim3(256), 0, stream, p);
   } else if (g.mt == 1 && g.ntw == 8) {
-    // 16-row tiles over the 32 x 512 image (small filters, capi.hip obs_pick; d <= 12)
+    // 16-row tiles over the 32 x 512 image (small filters, capi_model.hip obs_pick; d <= 12)
     if constexpr (DI <= 12) hipLaunchKernelGGL((k_gp_tile<DI, false, 0, 4, 1, 8>), grid, dim3(256), 0, stream, p);
   } else if (g.mt == 1 && g.ntw == 4) {
-    // the 16 x 256 image of small models and filters (capi.hip obs_pick; d <= 12)
+    // the 16 x 256 image of small models and filters (capi_model.hip obs_pick; d <= 12)
     if constexpr (DI <= 12) hipLaunchKernelGGL((k_gp_tile<DI, false, 0, 4, 1, 4>), grid, dim3(256), 0, stream, p);
   } else if (g.nw == 8) {
     hipLaunchKernelGGL((k_gp_tile<DI, false, 0, 8>), grid, dim3(512), 0, stream, p);

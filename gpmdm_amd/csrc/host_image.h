@@ -1,5 +1,5 @@
 // Host-side construction of a GP's device image and the model-descriptor checks
-// (plain C++17: no HIP; capi.hip uploads what this produces, and the host sanitizer test
+// (plain C++17: no HIP; capi_model.hip uploads what this produces, and the host sanitizer test
 // tests/test_host_asan.py builds it with -fsanitize=address,undefined).
 //
 // Fragment layout (consumed by gp_tile.h), for a tile shape (nw waves, each owning ntw

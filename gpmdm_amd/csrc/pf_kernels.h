@@ -133,7 +133,7 @@ struct DynFinishArgs {
   long long P;
   unsigned* health;               // kHealth* counters (PF) or nullptr
   // PF bookkeeping done by output 0 / outputs < F (not by the switch, which may run ahead:
-  // capi.hip pre-switch): the normaliser maxima reset, and the row count of this dynamics
+  // capi_frame.hip pre-switch): the normaliser maxima reset, and the row count of this dynamics
   // pass (sum over n_rows_seg segments of rows_e - rows_b) for gpmdm_pf_dyn_rows
   unsigned long long* gmax_reset; // F maxima, or nullptr
   int F;
@@ -142,7 +142,7 @@ struct DynFinishArgs {
   int n_rows_seg;
   int* rows_out;                  // or nullptr
   int* rows_host;                 // the same count into mapped host memory (the next frames'
-                                  // tile-height choice, capi.hip dyn_frame_geo), or nullptr
+                                  // tile-height choice, capi_frame.hip dyn_frame_geo), or nullptr
   // the frame's observation copied by outputs < z_n from host-mapped memory to the device
   // buffer the observation GP reads (no copy launch on the critical path), or z_n = 0
   const double* z_src;

@@ -1,4 +1,4 @@
-// Status plumbing shared by the C-ABI translation units (capi.hip, precompute.hip).
+// Status plumbing shared by the C-ABI translation units (capi_*.hip, precompute.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>

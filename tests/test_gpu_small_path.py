@@ -1,7 +1,7 @@
 """GPU: the one-launch paths of small filters (pf_kernels.hip: k_small_switch -- switch, class
 scan, grouping, leader compaction -- for P <= 1024 particles on one shard, k_small_resample
 -- normalise, resample, read-out -- for P <= 1024 per filter) are bitwise the multi-kernel
-path (GPMDM_NO_SMALL_PATH=1), the observation GP's 16-row tiles (capi.hip obs_run_geo)
+path (GPMDM_NO_SMALL_PATH=1), the observation GP's 16-row tiles (capi_model.hip obs_pick)
 are bitwise its 32-row tiles, and a small replay filter's class counts computed on the host
 (no mid-frame sync) are the device's (GPMDM_NO_HOST_COUNTS=1), and a Philox filter whose
 next switch the resample launches ahead (pre-switch) is bitwise one that switches in the next
@@ -44,7 +44,7 @@ for name, P, rng, res, dd in (("replay100", 100, "torch", "multinomial", True),
     pf = GPMDM_PF(m, T, P, rng=rng, seed=9 if rng == "philox" else None, resample=res, dedup=dd)
     for k in range(4):
         pf.update(Y[50 + 9 * k] + 0.01)
-        if k == 1:                           # between frames: drops a pre-switch (capi.hip)
+        if k == 1:                           # between frames: drops a pre-switch (capi_pf.hip drop_preswitch)
             out[f"{name}_{k}_pred"] = pf.predict().numpy()
         out[f"{name}_{k}_post"] = pf.class_probabilities().numpy()
         out[f"{name}_{k}_mean"] = pf.current_state_mean().numpy()
@@ -54,7 +54,7 @@ for name, P, rng, res, dd in (("replay100", 100, "torch", "multinomial", True),
     for key in ("states", "classes", "ll", "w", "resample_idx"):
         out[f"{name}_{key}"] = st[key]
 # replay updates with no read-out between them: the host class counts wait for the
-# previous resample themselves (capi.hip gpmdm_pf::cls_ev)
+# previous resample themselves (capi_internal.h gpmdm_pf::cls_ev)
 torch.manual_seed(4)
 pf = GPMDM_PF(m, T, 300, rng="torch")
 for k in range(5):
@@ -91,7 +91,7 @@ def test_small_path_is_bitwise_the_multi_kernel_path(tmp_path):
     # Philox filters' next switch launched by the resample (pre-switch) or by the next update
     nopre = _run(tmp_path, "nopre", {"GPMDM_NO_PRESWITCH": "1"})
     # de-duplicated dynamics passes on the wide 32 x 512 image every frame instead of the
-    # narrow 16 x 256 one (capi.hip dyn_frame_wide: the two are bitwise the same at d <= 12)
+    # narrow 16 x 256 one (capi_frame.hip dyn_frame_wide: the two are bitwise the same at d <= 12)
     widedyn = _run(tmp_path, "widedyn", {"GPMDM_DYN_WIDE_ROWS": "0"})
     assert fused.keys() == multi.keys() == tiles16.keys() == devcounts.keys() == nopre.keys() == widedyn.keys()
     for k in fused:
@@ -104,7 +104,7 @@ def test_small_path_is_bitwise_the_multi_kernel_path(tmp_path):
 
 def test_deferred_likelihood_is_flushed_for_an_early_reader():
     """A single-shard small filter defers its likelihood finish into the resampling launch
-    (capi.hip weigh / flush_ll): an export between propagate and resample must still see
+    (capi_frame.hip weigh / capi_pf.hip flush_ll): an export between propagate and resample must still see
     the finished ll, and the frame must end bitwise as an uninterrupted update."""
     import torch
     from conftest import load_fixture, product_model
@@ -166,7 +166,7 @@ np.savez(sys.argv[1], **out)
 
 @pytest.mark.timeout(600)
 def test_small_observation_image_matches_the_default_image(tmp_path):
-    """Small models and filters run the observation GP over a 16 x 256 image (capi.hip
+    """Small models and filters run the observation GP over a 16 x 256 image (capi_model.hip
     obs_pick): its column blocks partition the sums differently, so the filter agrees with
     the 32 x 512 image to rounding (not bit for bit) -- same classes and resampling
     indices, states and read-outs to 1e-9 -- on the config-1 model (N = 500)."""

@@ -1,6 +1,6 @@
 """Host sanitizers on the C ABI's host-side code: the model
 descriptor validation and the MFMA-fragment image packing of gpmdm_model_create
-(gpmdm_amd/csrc/host_image.h, the same header capi.hip compiles) built with
+(gpmdm_amd/csrc/host_image.h, the same header capi_model.hip compiles) built with
 -fsanitize=address,undefined and driven by tests/asan/host_image_check.cpp.  CPU only."""
 import os
 import shutil

@@ -79,7 +79,7 @@ def _tile_args(kernel: str):
 
 
 def _default_shape(kernel: str) -> bool:
-    """A k_gp_tile instantiation a default model uses (capi.hip gpmdm_model_create: the
+    """A k_gp_tile instantiation a default model uses (capi_model.hip gpmdm_model_create: the
     observation GP 32x512 for d <= 12 / 64x512 above, dynamics 16x256 plus a wide image in
     the observation shape).  Template args: <d, dyn, VAR, NW, MT, NTW>."""
     m = re.search(r"k_gp_tileILi(\d+)ELb([01])ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", kernel)

@@ -27,7 +27,7 @@ int main(int argc, char** argv) {
   const int N = argc > 2 ? atoi(argv[2]) : 2000, D = argc > 3 ? atoi(argv[3]) : 62, d = TB_D;
   std::mt19937_64 rng(1);
   std::normal_distribution<double> nd(0.0, 1.0);
-  const int cap = row_cap(N);   // padded like capi.hip::build_image
+  const int cap = row_cap(N);   // padded like capi_model.hip build_image
   std::vector<double> hXs((size_t)cap * d, 0.0), hXsq(cap, kPadSq), hX((size_t)P * d);
   for (int i = 0; i < N; ++i) {
     double s = 0;
