@@ -348,6 +348,76 @@ def spread_line(device, steps, warmup=5, y_lambda=SPREAD_LAMBDA, dyn_tiles="auto
                     "(ms_per_step includes them)"}
 
 
+def cutoff_line(model, T, P, zs, warmup, steps, headline_ms=None, headline_obs_ms=None):
+    """The same step with the observation GP's opt-in kernel-value cutoff
+    (GPMDM_PF(obs_cutoff=True)): kernel values below the model's tau flushed to
+    0 and the unreachable 16-row K-steps skipped.  A timed pass (the roofline kernel's events
+    on every 4th frame), then an untimed stats pass counting the MFMA groups the kernel ran
+    against the dense kernel's (executed FLOP = groups x 16 x 16 x 16 x 2).  Results equal the
+    dense filter's to rounding (tests/test_gpu_obs_cutoff.py); beside the headline, never it."""
+    import torch
+    from gpmdm_amd import GPMDM_PF, _lib
+    t0 = time.perf_counter()
+    model.enable_obs_cutoff(True)
+    setup_s = time.perf_counter() - t0
+    torch.manual_seed(11)
+    pf = GPMDM_PF(model, T, P, rng="philox", seed=11, obs_cutoff=True)
+
+    def frame(k):
+        pf.update(zs[k])
+        pf.get_most_likely_class()
+        pf.class_probabilities()
+        pf.current_state_mean()
+
+    for k in range(warmup):
+        frame(k)
+    torch.cuda.synchronize()
+    pf.stage_times()
+    pf.enable_timing(True, stages=("obs_gemm",))
+    pf.enable_timing(False)
+    lib_, h_ = _lib.load(), pf._h
+    t1 = time.perf_counter()
+    for k in range(steps):
+        if k % 4 == 0:
+            lib_.gpmdm_pf_enable_timing(h_, 1)
+        frame(warmup + k)
+        if k % 4 == 0:
+            lib_.gpmdm_pf_enable_timing(h_, 0)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t1
+    pf.enable_timing(False)
+    obs_ms, obs_n = pf.stage_times()["obs_gemm"]
+    obs_launch_ms = obs_ms / max(obs_n, 1)
+    # stats pass: the next frames of the stream, MFMA groups counted by the kernel
+    pf.set_obs_cutoff(True, stats=True)
+    pf.obs_cutoff_stats(reset=True)
+    n_st = min(steps, 10)
+    for k in range(n_st):
+        frame(warmup + steps + k)
+    st = pf.obs_cutoff_stats()
+    pf.set_obs_cutoff(True, stats=False)
+    tau = model.obs_cutoff_tau
+    ms = el / steps * 1e3
+    groups_per_launch = st["run"] / max(n_st, 1)
+    exec_flop = groups_per_launch * 16 * 16 * 16 * 2
+    out = {"ms_per_step": ms, "value": P * steps / el, "steps": steps,
+           "vs_dense_headline": (headline_ms / ms) if headline_ms else None,
+           "obs_launch_ms": obs_launch_ms,
+           "obs_speedup_vs_dense": (headline_obs_ms / obs_launch_ms) if headline_obs_ms else None,
+           "tau": tau, "mfma_groups_run_fraction": st["fraction_run"],
+           "skipped_fraction": (1.0 - st["fraction_run"]) if st["fraction_run"] is not None else None,
+           "executed_tflops": exec_flop / (obs_launch_ms * 1e-3) / 1e12,
+           "executed_frac_of_peak": exec_flop / (obs_launch_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS,
+           "setup_s": setup_s,
+           "note": "GPMDM_PF(obs_cutoff=True): kernel values below tau flushed to 0 (tau bounds the change "
+                   "of 1 - k^T K^-1 k below half an ulp, DESIGN.md §3) and the MFMAs of unreachable 16-row "
+                   "K-steps skipped; mfma_groups_run_fraction = groups the kernel ran / the dense kernel's "
+                   "over a 10-frame stats pass after the timed frames; executed_tflops = those groups x 8192 "
+                   "FLOP / the observation launch time; results equal the dense filter's to rounding "
+                   "(tests/test_gpu_obs_cutoff.py)"}
+    return out
+
+
 def nodedup_line(model, T, P_total, group, dist, device, zs, steps, rng, dyn_tiles="auto"):
     """The same step with ancestor de-duplication off (every particle's dynamics GP)."""
     import torch
@@ -746,6 +816,9 @@ def main():
                          "observation dimensions need a smaller one to keep the cloud spread)")
     ap.add_argument("--spread-steps", type=int, default=None,
                     help="frames of the spread-cloud line (config 2, one GPU; default 30, 0 = off)")
+    ap.add_argument("--cutoff-steps", type=int, default=None,
+                    help="frames of the observation-GP cutoff line (obs_cutoff=True; configs 2, 3, 5 on one GPU: "
+                         "default 20, 0 = off)")
     ap.add_argument("--dyn-tiles", default="auto", choices=("auto", "narrow", "wide"),
                     help="dynamics tile shape of the headline filter (gpmdm_pf_set_dyn_tiles)")
     argv = sys.argv[1:]
@@ -937,6 +1010,15 @@ def main():
     alg, dense, executed = obs_kernel_flops(N, D)
     obs_ms, obs_n = stages["obs_gemm"]
     obs_launch_s = obs_ms / max(obs_n, 1) / 1e3
+    if args.cutoff_steps is None:
+        args.cutoff_steps = 20 if (args.config in (2, 3, 5) and rng == "philox" and args.stream == "mocap") else 0
+    cut = None
+    if args.cutoff_steps and world == 1 and args.stream == "mocap":
+        try:   # reported beside the headline, never in place of it
+            cut = cutoff_line(model, T, P_total, zs, args.warmup, args.cutoff_steps, elapsed / args.steps * 1e3,
+                              obs_launch_s * 1e3)
+        except Exception as e:  # noqa: BLE001
+            cut = {"error": repr(e)[:400]}
     achieved = alg * P_local / obs_launch_s / 1e12
     traffic, traffic_src = pmc_traffic(WORKLOAD["cfg"])
     b_image = obs_model_bytes(N, D)
@@ -1012,6 +1094,8 @@ def main():
         rec["bank"] = bank
     if spread is not None:
         rec["spread"] = spread
+    if cut is not None:
+        rec["cutoff"] = cut
     if args.config == 1:
         ms = elapsed / args.steps * 1e3
         rec["ms_per_frame"] = ms

@@ -389,16 +389,27 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     // ---- observation GP + likelihood over particles [lo, hi) ----
     pf->mark_begin(s, GPMDM_STAGE_OBS_GEMM, t0);
     TileParams tp{};
-    const GpImage& oi = *pf->obs_img;
+    // the opt-in kernel-value cutoff: the cutoff image and kernel (same column blocks and
+    // partials as the default image: the finish below is shared)
+    const bool cut = pf->obs_cutoff && m->obs_cut.Bf;
+    const GpImage& oi = cut ? m->obs_cut : *pf->obs_img;
+    const int* tab = pf->obs_tab + (cut ? 8 : 0);
     tp.seg[0] = oi.seg();
     tp.n_seg = 1;
-    tp.geo = pf->obs_geo;
-    tp.tiles_ub = (int)cdiv(nl, pf->obs_geo.pt());
+    tp.geo = cut ? oi.geo : pf->obs_geo;
+    tp.tiles_ub = (int)cdiv(nl, tp.geo.pt());
     tp.n_j_max = oi.n_j;
-    tp.seg_pos_begin = pf->obs_tab + 0;
-    tp.seg_pos_end = pf->obs_tab + 1;
-    tp.seg_out_base = pf->obs_tab + 2;
-    tp.seg_tile_start = pf->obs_tab + 3;
+    tp.seg_pos_begin = tab + 0;
+    tp.seg_pos_end = tab + 1;
+    tp.seg_out_base = tab + 2;
+    tp.seg_tile_start = tab + 3;
+    if (cut) {
+      tp.sparse = 1;
+      tp.ksph = m->obs_cut_sph;
+      tp.cut2 = m->cut2;
+      tp.t_cut = m->t_cut;
+      tp.sp_stats = pf->sp_stats_on ? pf->sp_stats : nullptr;
+    }
     tp.perm = pf->own_order();           // positions [lo, hi) of the ownership order
     tp.X = pf->X_prop;
     fill_tile_common(tp, m, false);

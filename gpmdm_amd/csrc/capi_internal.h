@@ -83,7 +83,8 @@ struct GpImage {
 };
 
 int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const double* ls,
-                const double* lin_c2, const double* R, const double* M, TileGeo geo);
+                const double* lin_c2, const double* R, const double* M, TileGeo geo,
+                const long long* perm = nullptr, bool sym = false);
 
 }  // namespace gpmdm::capi
 
@@ -119,12 +120,25 @@ struct gpmdm_model {
   double* y_il2_dev = nullptr;
   double* y_lam2_dev = nullptr;   // 1 / il2 = exp(y_log_lambdas)^2
   double sum_log_il2 = 0.0;
+  // Observation-GP cutoff image (gpmdm_model_set_obs_cutoff; empty: not set): K^-1's block
+  // upper triangle over the training rows in a spatial order, the K-step spheres, and the
+  // cutoff (tau; cut2 = the squared scaled distance past which a value is below tau, with a
+  // margin; t_cut = ln tau in the tile kernel's exponent units)
+  GpImage obs_cut;
+  double* obs_cut_sph = nullptr;
+  double cut_tau = 0.0, cut2 = 0.0, t_cut = 0.0;
+  void release_cutoff() {
+    obs_cut.release();
+    obs_cut = GpImage{};
+    dfree(obs_cut_sph);
+  }
 
   ~gpmdm_model() {
     obs.release();
     obs_small.release();
     for (auto& g : dyn) g.release();
     for (auto& g : dynw) g.release();
+    release_cutoff();
     dfree(y_il2_dev);
     dfree(y_lam2_dev);
   }
@@ -181,7 +195,12 @@ struct gpmdm_pf {
   double *T = nullptr, *X = nullptr, *X_prop = nullptr, *ll = nullptr;
   int *cls = nullptr, *cls_new = nullptr, *perm = nullptr, *ridx = nullptr;
   int *blockcounts = nullptr, *blockoff = nullptr, *small = nullptr;   // small: class tables
-  int *obs_tab = nullptr;
+  int *obs_tab = nullptr;            // [0, 5): the observation launch's segment table; [8, 13): the cutoff image's
+  // the observation GP's kernel-value cutoff (gpmdm_pf_set_obs_cutoff): on, and the skip
+  // statistics of the cutoff kernel (device: MFMA groups run, the dense kernel's count)
+  bool obs_cutoff = false;
+  unsigned long long* sp_stats = nullptr;
+  bool sp_stats_on = false;
   // likelihood finish deferred into the resampling launch (single-shard small filters:
   // k_small_resample computes ll first, one launch less per frame); flush_ll runs it for
   // any reader of ll that comes first
@@ -485,6 +504,7 @@ struct gpmdm_pf {
     for (int* p : is) dfree(p);
     dfree(own_tmp);
     dfree(gmax);
+    dfree(sp_stats);
     dfree(bmax);
     dfree(bmax_rows);
     dfree(owner);

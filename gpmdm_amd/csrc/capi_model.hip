@@ -26,8 +26,11 @@ int upload(T** dst, const std::vector<T>& v) {
 }
 
 int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const double* ls,
-                const double* lin_c2, const double* R, const double* M, TileGeo geo) {
-  const ImagePacker pk(n_rows, d, n_m, X, ls, lin_c2, R, M, geo);
+                const double* lin_c2, const double* R, const double* M, TileGeo geo, const long long* perm,
+                bool sym) {
+  ImagePacker pk(n_rows, d, n_m, X, ls, lin_c2, R, M, geo);
+  pk.perm = perm;
+  pk.sym = sym;
   g.geo = geo;
   g.dyn = lin_c2 != nullptr;
   g.n_rows = n_rows;
@@ -182,6 +185,55 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
     }
   }
   *out = m;
+  return GPMDM_OK;
+}
+
+// The observation GP's opt-in kernel-value cutoff (DESIGN.md §3 "Kernel-value cutoff"):
+// the K^-1 image in the symmetric block form over a spatial order of the training rows,
+// the per-K-step bounding spheres and tau (host_image.h).  K_inv = NULL removes it.
+int gpmdm_model_set_obs_cutoff(gpmdm_model_t m, const double* K_inv, const double* beta, double sigma2,
+                               const double* y_absmax) {
+  CHECK(m, "null model");
+  HIPCHK(hipSetDevice(m->device));
+  if (!K_inv) {
+    HIPCHK(hipDeviceSynchronize());   // filters' launches may still read the image
+    m->release_cutoff();
+    return GPMDM_OK;
+  }
+  CHECK(beta && y_absmax, "null argument");
+  CHECK(sigma2 > 0.0 && std::isfinite(sigma2), "sigma2 must be positive (the observation noise variance)");
+  CHECK(ksteps((int)m->N) <= kMaxCutoffKs, "the cutoff image holds at most 65536 training rows");
+  CHECK(m->d <= 16, "the cutoff image is built for latent dimensions d <= 16");
+  // its own tile shape (512 columns per block, as the default observation images: the same
+  // partials, so the filter's likelihood finish and buffers serve both): 32 x 512 up to d = 8,
+  // 64 x 512 above (gp_tile.h launch_d)
+  const TileGeo g = m->d <= 8 ? kGeo32x512 : kGeo64x512;
+  CHECK(m->obs.geo.nb() == g.nb() && cdiv(m->N + m->D, g.nb()) == m->obs.n_j,
+        "the cutoff image needs a model with 512-column observation blocks (the default tile shapes)");
+  const int N = (int)m->N, d = m->d;
+  const double tau = obs_cutoff_tau(N, sigma2, beta, m->D, y_absmax);
+  CHECK(tau > 0.0 && std::isfinite(tau), "no usable cutoff for this model");
+  const std::vector<long long> perm = spatial_order(m->X.data(), m->y_ls.data(), N, d);
+  std::vector<double> sph;
+  kstep_spheres(m->X.data(), m->y_ls.data(), perm.data(), N, d, sph);
+  HIPCHK(hipDeviceSynchronize());
+  m->release_cutoff();
+  int rc = build_image(m->obs_cut, N, d, m->D, m->X.data(), m->y_ls.data(), nullptr, K_inv, beta, g, perm.data(),
+                       true);
+  if (!rc) rc = upload(&m->obs_cut_sph, sph);
+  if (rc) {
+    m->release_cutoff();
+    return rc;
+  }
+  m->cut_tau = tau;
+  m->cut2 = -std::log(tau) * (1.0 + 1e-12) + 1e-6;   // margin over both tests' rounding
+  m->t_cut = std::log(tau) * kLog2eX64;
+  return GPMDM_OK;
+}
+
+int gpmdm_model_obs_cutoff(gpmdm_model_t m, double* tau) {
+  CHECK(m && tau, "null argument");
+  *tau = m->obs_cut.Bf ? m->cut_tau : 0.0;
   return GPMDM_OK;
 }
 

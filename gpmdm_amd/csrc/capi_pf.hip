@@ -54,7 +54,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   ALLOC(blockcounts, (long long)pf->nb * C);
   ALLOC(blockoff, (long long)pf->nb * C);
   ALLOC(small, 512);
-  ALLOC(obs_tab, 8);
+  ALLOC(obs_tab, 16);
   ALLOC(owner, (long long)C * P);
   ALLOC(slot, (long long)C * P);
   ALLOC(lflag, P);
@@ -562,6 +562,11 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, og.pt())};
   if (!rc && hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess)
     rc = fail(GPMDM_E_HIP, "upload of the observation tile table");
+  if (!rc && m->obs_cut.Bf) {         // the cutoff image's tile table (its own tile height)
+    const int tc[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, m->obs_cut.geo.pt())};
+    if (hipMemcpy(pf->obs_tab + 8, tc, sizeof(tc), hipMemcpyHostToDevice) != hipSuccess)
+      rc = fail(GPMDM_E_HIP, "upload of the observation tile table");
+  }
   if (rc) {
     dfree(qdyn);
     dfree(qobs);
@@ -583,6 +588,41 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
   m->refs.fetch_add(1);
   pf->m = m;
   model_release(old);
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_set_obs_cutoff(gpmdm_pf_t pf, int mode) {
+  CHECK(pf, "null handle");
+  CHECK(mode >= 0 && mode <= 2, "mode: 0 off, 1 on, 2 on with skip statistics");
+  if (pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "set_obs_cutoff between propagate and resample");
+  gpmdm_model* m = pf->m;
+  HIPCHK(hipSetDevice(m->device));
+  if (mode && !m->obs_cut.Bf) return fail(GPMDM_E_STATE, "the model has no cutoff image (gpmdm_model_set_obs_cutoff)");
+  if (mode) {
+    const int tc[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, m->obs_cut.geo.pt())};
+    HIPCHK(hipMemcpy(pf->obs_tab + 8, tc, sizeof(tc), hipMemcpyHostToDevice));
+  }
+  if (mode == 2 && !pf->sp_stats) {
+    TRY(dalloc(&pf->sp_stats, 2));
+    HIPCHK(hipMemset(pf->sp_stats, 0, 2 * sizeof(unsigned long long)));
+  }
+  pf->obs_cutoff = mode != 0;
+  pf->sp_stats_on = mode == 2;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_obs_cutoff_stats(gpmdm_pf_t pf, int64_t* run, int64_t* dense, int reset, void* stream) {
+  CHECK(pf && run && dense, "null argument");
+  *run = *dense = 0;
+  if (!pf->sp_stats) return GPMDM_OK;
+  HIPCHK(hipSetDevice(pf->m->device));
+  hipStream_t s = (hipStream_t)stream;
+  unsigned long long h[2];
+  HIPCHK(hipMemcpyAsync(h, pf->sp_stats, sizeof(h), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *run = (int64_t)h[0];
+  *dense = (int64_t)h[1];
+  if (reset) HIPCHK(hipMemsetAsync(pf->sp_stats, 0, sizeof(h), s));
   return GPMDM_OK;
 }
 

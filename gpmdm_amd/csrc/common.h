@@ -44,6 +44,15 @@ struct TileParams {
   const double* z;                // F x n_m
   const double* lam2;             // n_m: exp(y_log_lambdas)^2 = 1 / il2
   long long Pf;                   // particles per filter
+  // Observation-GP cutoff (the kTileSparse kernels, gp_tile.h; DESIGN.md §3 "Kernel-value
+  // cutoff"): per-K-step bounding spheres of the image rows (centre d, radius; scaled
+  // coordinates), the squared scaled distance beyond which every kernel value is below tau,
+  // and the flush threshold in the generation's units (t = 64/ln2 x natural exponent)
+  int sparse;                     // 0: the dense kernel
+  const double* ksph;
+  double cut2;
+  double t_cut;
+  unsigned long long* sp_stats;   // nullable: [0] MFMA groups executed, [1] the dense kernel's count
 };
 
 void launch_gp_tile(const TileParams& p, int d, bool dyn, hipStream_t stream);

@@ -55,6 +55,8 @@ constexpr double kPadSq = 268435456.0;   // 2^28: exponent ~ -2^28 even x 128/ln
                                         // (v_cvt_i32_f64 exact, ldexp underflows to 0)
 // |Xs|^2 is stored pre-scaled by 64 / ln 2 for the tile kernel's exp2 (gp_tile.h)
 constexpr double kLog2eX64 = 92.33248261689366;
+// The observation GP's cutoff image: K-steps the sparse tile kernel can list (gp_tile.h).
+constexpr int kMaxCutoffKs = 4096;
 // Dynamics linear kernel: K=4 MFMA sub-steps covering the d+1 rows of H.
 constexpr int lin_substeps(int d) { return (d + 1 + 3) / 4; }
 

@@ -18,8 +18,11 @@
 //   H[row = 4 kh + (l >> 4)][col = nb J + 16 (nw nt + w) + (l & 15) - coff].
 #pragma once
 
+#include <algorithm>
+#include <cmath>
 #include <cstddef>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/gpmdm_hip.h"
@@ -56,6 +59,13 @@ struct ImagePacker {
   int n_rows, d, n_m, coff, n_j;
   TileGeo geo;
   const double *X, *ls, *lin_c2, *R, *M;
+  // Cutoff image of the observation GP (gpmdm_model_set_obs_cutoff): R is the full symmetric
+  // K^-1 (the reference's own U^-1 U^-T, gpmdm.py:1286-1290) and B holds its block upper
+  // triangle with the off-diagonal 16 x 16 blocks doubled -- k^T K^-1 k = sum_j k_j V_j with
+  // V_j = sum over rows i of blocks <= block(j) of k_i B_ij -- over the training rows in the
+  // order perm (image row -> training row; nullptr: identity).
+  bool sym = false;
+  const long long* perm = nullptr;
 
   ImagePacker(int n_rows_, int d_, int n_m_, const double* X_, const double* ls_, const double* lin_c2_,
               const double* R_, const double* M_, TileGeo geo_)
@@ -64,12 +74,21 @@ struct ImagePacker {
     n_j = (n_rows + n_m + coff + geo.nb() - 1) / geo.nb();
   }
 
-  // B = [triu(R) | M] (row-major inputs R: n_rows x n_rows, M: n_rows x n_m)
+  long long src(long long row) const { return perm ? perm[row] : row; }
+
+  // B = [triu(R) | M] (row-major inputs R: n_rows x n_rows, M: n_rows x n_m); the cutoff
+  // image: [2 blocktriu(K^-1) + blockdiag(K^-1) | M] in the order perm
   double val(long long row, long long col) const {
     if (row >= n_rows || col < 0) return 0.0;
-    if (col < n_rows) return row <= col ? R[row * n_rows + col] : 0.0;   // upper triangle of R
+    if (col < n_rows) {
+      if (!sym) return row <= col ? R[row * n_rows + col] : 0.0;   // upper triangle of R
+      const long long bi = row / kBK, bj = col / kBK;
+      if (bi > bj) return 0.0;
+      const double a = R[src(row) * n_rows + src(col)];
+      return bi < bj ? 2.0 * a : a;
+    }
     const long long j = col - n_rows;
-    return j < n_m ? M[row * n_m + j] : 0.0;
+    return j < n_m ? M[src(row) * n_m + j] : 0.0;
   }
 
   // Row records [Xs_i, |Xs_i|^2 * 64/ln2], Xs = X / ls: (d + 1) doubles per row, padded to
@@ -81,7 +100,7 @@ struct ImagePacker {
     for (long long i = 0; i < n_rows; ++i) {
       double s = 0.0;
       for (int j = 0; j < d; ++j) {
-        const double v = X[i * d + j] / ls[j];
+        const double v = X[src(i) * d + j] / ls[j];
         rec[i * rw + j] = v;
         s += v * v;
       }
@@ -143,5 +162,103 @@ struct ImagePacker {
             }
   }
 };
+
+// ---------------------------------------------------------------------------------
+// Observation-GP cutoff (opt-in, DESIGN.md §3 "Kernel-value cutoff"): kernel values below
+// tau are flushed to exactly 0, so a K-step (16 training rows) whose values are all 0 for a
+// particle tile contributes nothing, and its MFMAs are skipped.  Three host-side pieces:
+
+// The training rows in a spatial order (recursive coordinate bisection of the scaled latents
+// X / ls, leaves of kBK rows): K-steps of nearby points, so a compact particle tile is far
+// from most K-steps.  Every leaf holds exactly kBK rows but the last.  Returns perm (image
+// row -> training row).
+inline void spatial_order_rec(const double* X, const double* ls, int d, long long* idx, long long n,
+                              std::vector<double>& key) {
+  if (n <= kBK) return;
+  int best = 0;
+  double spread = -1.0;
+  for (int j = 0; j < d; ++j) {
+    double lo = 1e300, hi = -1e300;
+    for (long long i = 0; i < n; ++i) {
+      const double v = X[idx[i] * d + j] / ls[j];
+      lo = v < lo ? v : lo;
+      hi = v > hi ? v : hi;
+    }
+    if (hi - lo > spread) {
+      spread = hi - lo;
+      best = j;
+    }
+  }
+  // stable sort of idx by the widest coordinate (ties by training row: deterministic)
+  std::vector<std::pair<double, long long>> kv((size_t)n);
+  for (long long i = 0; i < n; ++i) kv[(size_t)i] = {X[idx[i] * d + best] / ls[best], idx[i]};
+  std::sort(kv.begin(), kv.end());
+  for (long long i = 0; i < n; ++i) idx[i] = kv[(size_t)i].second;
+  const long long leaves = (n + kBK - 1) / kBK;
+  const long long left = ((leaves + 1) / 2) * kBK;   // a multiple of kBK: full leaves on the left
+  spatial_order_rec(X, ls, d, idx, left, key);
+  spatial_order_rec(X, ls, d, idx + left, n - left, key);
+}
+inline std::vector<long long> spatial_order(const double* X, const double* ls, long long n, int d) {
+  std::vector<long long> idx((size_t)n);
+  for (long long i = 0; i < n; ++i) idx[(size_t)i] = i;
+  std::vector<double> key;
+  spatial_order_rec(X, ls, d, idx.data(), n, key);
+  return idx;
+}
+
+// One bounding sphere per K-step of the image (rows in the order perm), in scaled
+// coordinates: centre (d doubles) then radius, padded up to the radius of every row (a
+// relative and absolute margin over the computed distances).
+inline void kstep_spheres(const double* X, const double* ls, const long long* perm, long long n, int d,
+                          std::vector<double>& out) {
+  const long long nks = (n + kBK - 1) / kBK;
+  out.assign((size_t)nks * (d + 1), 0.0);
+  std::vector<double> c((size_t)d);
+  for (long long k = 0; k < nks; ++k) {
+    const long long r0 = k * kBK, r1 = (k + 1) * kBK < n ? (k + 1) * kBK : n;
+    for (int j = 0; j < d; ++j) {
+      double s = 0.0;
+      for (long long r = r0; r < r1; ++r) s += X[perm[r] * d + j] / ls[j];
+      c[(size_t)j] = s / (double)(r1 - r0);
+    }
+    double rad = 0.0;
+    for (long long r = r0; r < r1; ++r) {
+      double s = 0.0;
+      for (int j = 0; j < d; ++j) {
+        const double t = X[perm[r] * d + j] / ls[j] - c[(size_t)j];
+        s += t * t;
+      }
+      rad = s > rad ? s : rad;
+    }
+    for (int j = 0; j < d; ++j) out[(size_t)k * (d + 1) + j] = c[(size_t)j];
+    out[(size_t)k * (d + 1) + d] = std::sqrt(rad) * (1.0 + 1e-12) + 1e-12;
+  }
+}
+
+// The cutoff tau: every kernel value below it is flushed to 0.  Bounds:
+//  * the quadratic form: flushing delta (0 <= delta_i <= tau) moves q = k^T K^-1 k by at most
+//    (2 + e) e with e = sqrt(N) tau / sigma (|R^T k| = sqrt(q) <= 1, |R| <= 1 / sigma for
+//    K_y = K + sigma^2 I), and 1 - q >= sigma^2 / (N + sigma^2) (lambda_max(K) <= N), so
+//    tau_q = sigma h / (2.001 sqrt(N)), h = half an ulp of sigma^2 / (N + sigma^2), keeps the
+//    change below half an ulp of the smallest possible 1 - q;
+//  * each mean mu_j = sum_i k_i M_ij moves by at most tau |M_j|_1: tau_mu = min_j half an
+//    ulp of max_i |Y_ij| / |M_j|_1 (below the resolution of the training observations).
+// Returns min(tau_q, tau_mu).
+inline double obs_cutoff_tau(long long N, double sigma2, const double* M, int D, const double* y_absmax) {
+  const double vc_min = sigma2 / ((double)N + sigma2);
+  const double h = 0.5 * (std::nextafter(vc_min, 1.0) - vc_min);
+  double tau = std::sqrt(sigma2) * h / (2.001 * std::sqrt((double)N));
+  for (int j = 0; j < D; ++j) {
+    double m1 = 0.0;
+    for (long long i = 0; i < N; ++i) m1 += std::fabs(M[i * D + j]);
+    const double yj = y_absmax[j];
+    if (m1 > 0.0 && yj > 0.0) {
+      const double t = 0.5 * (std::nextafter(yj, 1e308) - yj) / m1;
+      tau = t < tau ? t : tau;
+    }
+  }
+  return tau;
+}
 
 }  // namespace gpmdm

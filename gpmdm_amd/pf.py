@@ -92,7 +92,7 @@ class GPMDM_PF:
     def __init__(self, gpmdm: GPMDM, markov_switching_model, num_particles: int, *,
                  rng: str = "torch", seed=None, resample: str = "multinomial", process_group=None,
                  shard=None, exchange=None, dedup: bool = True, shard_order: bool = True,
-                 dyn_tiles: str = "auto", devices=None):
+                 dyn_tiles: str = "auto", devices=None, obs_cutoff: bool = False):
         self._gpmdm = gpmdm
         self._gpmdm.set_evaluation_mode()
         self._markov_switching_model = torch.as_tensor(markov_switching_model).type(self.dtype)
@@ -142,6 +142,10 @@ class GPMDM_PF:
         if dyn_tiles not in _lib.DYN_TILES:
             raise ValueError("dyn_tiles must be 'auto', 'narrow' or 'wide'")
 
+        self._obs_cutoff = 1 if obs_cutoff else 0
+        if obs_cutoff:
+            gpmdm.enable_obs_cutoff(True)       # the model's cutoff image (built once)
+
         def create(model_handle, rank):
             h = ctypes.c_void_p()
             _lib.check(lib.gpmdm_pf_create(
@@ -153,6 +157,8 @@ class GPMDM_PF:
             _lib.check(lib.gpmdm_pf_set_dedup(h, 1 if dedup else 0), "dedup")
             _lib.check(lib.gpmdm_pf_set_shard_order(h, 1 if shard_order else 0), "shard_order")
             _lib.check(lib.gpmdm_pf_set_dyn_tiles(h, _lib.DYN_TILES[dyn_tiles]), "dyn_tiles")
+            if self._obs_cutoff:
+                _lib.check(lib.gpmdm_pf_set_obs_cutoff(h, self._obs_cutoff), "obs_cutoff")
             return h
 
         self._peers = []                        # devices=: ranks 1.. as (handle, device index)
@@ -523,6 +529,29 @@ class GPMDM_PF:
             raise ValueError("the state was exported by a filter with another Philox seed")
         self.load_state(st["states"], st["classes"], ll=st["ll"], log_w=st["log_w"], w=st["w"],
                         resample_idx=st.get("resample_idx"), frame=st.get("frame"))
+
+    def set_obs_cutoff(self, on: bool = True, stats: bool = False):
+        """Run the observation GP with the model's kernel-value cutoff (GPMDM.enable_obs_cutoff,
+        built here if needed) or the dense kernel; ``stats`` also counts the MFMA groups run
+        (obs_cutoff_stats).  Between frames only."""
+        if on:
+            self._gpmdm.enable_obs_cutoff(True)
+            self._sync_model()
+        mode = (2 if stats else 1) if on else 0
+        lib = _lib.load()
+        for h in [self._h] + [p[0] for p in self._peers]:
+            _lib.check(lib.gpmdm_pf_set_obs_cutoff(h, mode), "set_obs_cutoff")
+        self._obs_cutoff = mode
+
+    def obs_cutoff_stats(self, reset: bool = True) -> dict:
+        """MFMA groups (16-particle x 16-column tile x 16-row K-step) the cutoff kernel ran since
+        the last reset, against the dense kernel's count for the same launches."""
+        lib = _lib.load()
+        run, dense = ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(lib.gpmdm_pf_obs_cutoff_stats(self._h, ctypes.byref(run), ctypes.byref(dense), 1 if reset else 0,
+                                                 self._stream()), "obs_cutoff_stats")
+        return {"run": run.value, "dense": dense.value,
+                "fraction_run": run.value / dense.value if dense.value else None}
 
     def dynamics_rows(self) -> int:
         """Rows the last dynamics-GP pass evaluated (distinct ancestor/class keys when

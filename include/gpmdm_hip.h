@@ -354,6 +354,28 @@ int gpmdm_pf_frame(gpmdm_pf_t pf, int64_t* frame);
  * between switch and resample. */
 int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t model);
 
+/* Observation-GP kernel-value cutoff (opt-in; DESIGN.md §3 "Kernel-value cutoff").  The
+ * observation GP of map_x_to_y / _update_weights (gpmdm.py:923-963, gpmdm_pf.py:170-192) with
+ * every kernel value k_i = exp(-|x* - X_i|^2 / l^2) below tau replaced by exactly 0, tau the
+ * largest cutoff whose effect provably stays below half an ulp of the smallest possible
+ * 1 - k^T K_y^-1 k and below half an ulp of each output dimension's largest training
+ * observation in the means; the kernel then skips the 16-row K-steps a particle tile cannot
+ * reach.  gpmdm_model_set_obs_cutoff builds the model's cutoff image from
+ *   K_inv     N x N row-major, K_y^-1 -- the reference's Ky_inv = U^-1 U^-T (gpmdm.py:1286-1290)
+ *   beta      N x D row-major, K_y^-1 Y (the mean weights, gpmdm.py:955-957)
+ *   sigma2    the noise variance on K_y's diagonal (exp(y_log_sigma_n)^2 + sigma_n_num_Y^2)
+ *   y_absmax  D values, max_i |Y_ij|
+ * (K_inv = NULL removes it); gpmdm_model_obs_cutoff returns tau (0: none).  A filter uses it
+ * after gpmdm_pf_set_obs_cutoff(pf, 1) (2: also count the MFMA groups run against the dense
+ * kernel's, read and optionally reset by gpmdm_pf_obs_cutoff_stats; 0: the dense kernel).
+ * Results are the dense filter's to rounding (not bit for bit), and do not depend on the
+ * tiling or the shard count. */
+int gpmdm_model_set_obs_cutoff(gpmdm_model_t model, const double* K_inv, const double* beta, double sigma2,
+                               const double* y_absmax);
+int gpmdm_model_obs_cutoff(gpmdm_model_t model, double* tau);
+int gpmdm_pf_set_obs_cutoff(gpmdm_pf_t pf, int mode);
+int gpmdm_pf_obs_cutoff_stats(gpmdm_pf_t pf, int64_t* run, int64_t* dense, int reset, void* stream);
+
 /* Failure detection.  The filter keeps the reference's arithmetic: a
  * non-positive predictive variance gives NaN log-likelihoods / states as it does in
  * gpmdm_pf.py:167-168, 188-192.  Each event is counted on the device (per particle and

@@ -163,7 +163,7 @@ def test_config4_one_million_particles_8_shards(fx_config2):
         del full
 
 
-def _philox_step_vs_oracle(m, om, T, P, seed, z_warm, z, what, sub_n=2000):
+def _philox_step_vs_oracle(m, om, T, P, seed, z_warm, z, what, sub_n=2000, **pf_kw):
     """One warm-up Philox step at P particles (shared ancestors: the de-duplicated dynamics
     path and the guided inverse-CDF search), then one resynced step against the oracle
     (gpmdm_pf.py:137-262):
@@ -180,7 +180,7 @@ def _philox_step_vs_oracle(m, om, T, P, seed, z_warm, z, what, sub_n=2000):
     from oracle import gpmdm_oracle as O
     from oracle import philox as X
     C, d = m.n_classes, m.d
-    pf = GPMDM_PF(m, torch.tensor(T), P, rng="philox", seed=seed)
+    pf = GPMDM_PF(m, torch.tensor(T), P, rng="philox", seed=seed, **pf_kw)
     pf.update(z_warm)
     pre = pf.export_state()
     frame = pf.frame
@@ -260,3 +260,25 @@ def test_large_config_benchmarked_particles_vs_oracle(cfg):
     zs = data.observation_stream(2, seed=1)
     P = {3: 100_000, 5: 125_000}[cfg]
     _philox_step_vs_oracle(m, om_t, T, P, 11, zs[0], zs[1], f"config {cfg} at P={P}")
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_large_config_cutoff_vs_oracle(cfg):
+    """The observation GP's kernel-value cutoff (GPMDM_PF(obs_cutoff=True)) at
+    configs[2] / [4]'s benchmarked particle counts: the same checks as the dense filter
+    (_philox_step_vs_oracle) at the same tolerances, and the kernel skips most of the dense
+    MFMA work on this cloud."""
+    from gpmdm_amd import synthetic
+    m, om, om_t, data, c = _synthetic(cfg)
+    m.enable_obs_cutoff(True)
+    assert m.obs_cutoff_tau > 0
+    T = synthetic.markov_matrix(c["C"])
+    zs = data.observation_stream(2, seed=1)
+    P = {3: 100_000, 5: 125_000}[cfg]
+    pf, _ = _philox_step_vs_oracle(m, om_t, T, P, 11, zs[0], zs[1], f"config {cfg} at P={P}, cutoff",
+                                   obs_cutoff=True)
+    pf.set_obs_cutoff(True, stats=True)
+    pf.update(zs[0])
+    st = pf.obs_cutoff_stats()
+    assert 0 < st["run"] < 0.5 * st["dense"], st

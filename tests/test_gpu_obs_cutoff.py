@@ -1,0 +1,213 @@
+"""The observation GP's opt-in kernel-value cutoff (``GPMDM_PF(..., obs_cutoff=True)``,
+DESIGN.md §3 "Kernel-value cutoff"): kernel values k_i = exp(-|x - X_i|^2 / l^2) below the
+model's tau are flushed to exactly 0 and the MFMAs of the 16-row K-steps a particle tile
+cannot reach are skipped (gpmdm.py:923-963 / gpmdm_pf.py:170-192 otherwise unchanged).
+
+Checked at the dense filter's tolerances:
+  * the reference's golden vectors: config-1 per-step parity over 200 frames, the 200-frame
+    torch-seeded trajectory, the N = 2000 per-step fixture (tests/golden, make_golden.py);
+  * the oracle: three resynced Philox steps at the benchmarked P = 100k (config 2);
+  * tiling / shard invariance: 4 and 8 logical shards bitwise equal one rank (the flush is
+    per value, and a skipped K-step or column tile contributes only exact zeros);
+  * against the dense kernel from the same state with the same draws (the two evaluate
+    k^T K^-1 k in different associations: symmetric K^-1 vs |R^T k|^2);
+  * tau equals the bound restated here (host_image.h obs_cutoff_tau), and the kernel skips
+    work on the benchmark's collapsed cloud.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import assert_step_matches, nrel, oracle_model, product_model
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def m1c(fx_config1):
+    m = product_model(fx_config1)
+    m.enable_obs_cutoff(True)
+    return m
+
+
+@pytest.fixture(scope="module")
+def m2c(fx_config2):
+    m = product_model(fx_config2)
+    m.enable_obs_cutoff(True)
+    return m
+
+
+def _tau_bound(m):
+    """host_image.h obs_cutoff_tau restated: min(tau_q, tau_mu)."""
+    Y = np.asarray(m.get_Y(), dtype=np.float64)
+    N = Y.shape[0]
+    sigma2 = float(torch.exp(m.y_log_sigma_n.detach().cpu())) ** 2 + m.sigma_n_num_Y ** 2
+    vc_min = sigma2 / (N + sigma2)
+    h = 0.5 * (np.nextafter(vc_min, 1.0) - vc_min)
+    tau = np.sqrt(sigma2) * h / (2.001 * np.sqrt(N))
+    X = m.X.detach().cpu().numpy()
+    ls = np.exp(m.y_log_lengthscales.detach().cpu().numpy())
+    from oracle import gpmdm_oracle as O
+    K = O.rbf_kernel(X, X, np.log(ls), float(m.y_log_sigma_n.detach().cpu()), m.sigma_n_num_Y, noise=True)
+    beta = np.linalg.solve(K, Y)
+    for j in range(Y.shape[1]):
+        m1 = np.sum(np.abs(beta[:, j]))
+        y = np.max(np.abs(Y[:, j]))
+        tau = min(tau, 0.5 * (np.nextafter(y, np.inf) - y) / m1)
+    return tau
+
+
+def test_tau_is_the_bound(m2c):
+    # beta from a fresh solve here, the library's from the precompute: the mean bound moves
+    # with |beta_j|_1 at the 1e-9 level
+    t = m2c.obs_cutoff_tau
+    assert t > 0
+    assert abs(t - _tau_bound(m2c)) <= 1e-6 * t, (t, _tau_bound(m2c))
+
+
+def _per_step_cutoff(m, f, pre, z_offset=0):
+    from gpmdm_amd import GPMDM_PF
+    P = f[pre + "E"].shape[1]
+    pf = GPMDM_PF(m, torch.tensor(f["T"]), P, rng="torch", obs_cutoff=True)
+    worst = {}
+    for k in range(f[pre + "E"].shape[0]):
+        pf.load_state(f[pre + "pre_states"][k], f[pre + "pre_classes"][k])
+        pf.update_with_draws(f["z"][k + z_offset], f[pre + "E"][k], f[pre + "normals"][k], f[pre + "u"][k])
+        st = pf.export_state()
+        assert np.array_equal(st["classes"], f[pre + "classes"][k].reshape(-1)), f"frame {k}: classes"
+        err = {"states": nrel(st["states"], f[pre + "states"][k]), "w": nrel(st["w"], f[pre + "w"][k]),
+               "post": float(np.max(np.abs(pf.class_probabilities().numpy() - f[pre + "posterior"][k]))),
+               "mean": nrel(pf.current_state_mean().numpy(), f[pre + "mean"][k]),
+               "lik": abs(pf.log_likelihood() - f[pre + "lik"][k]) / abs(f[pre + "lik"][k])}
+        assert pf.get_most_likely_class() == int(f[pre + "most_likely"][k])
+        for key, v in err.items():
+            worst[key] = max(worst.get(key, 0.0), v)
+    assert worst["states"] < 1e-6, worst
+    assert worst["w"] < 1e-5, worst
+    assert worst["post"] < 1e-6, worst
+    assert worst["mean"] < 1e-6, worst
+    assert worst["lik"] < 1e-5, worst
+    return worst
+
+
+def test_step_parity_config1_cutoff(m1c, fx_config1):
+    _per_step_cutoff(m1c, fx_config1, "traj_")
+
+
+def test_step_parity_config2_p1000_cutoff(m2c, fx_config2):
+    f = fx_config2
+    _per_step_cutoff(m2c, f, "step_", z_offset=f["z"].shape[0] - f["step_E"].shape[0])
+
+
+def test_trajectory_config1_cutoff(m1c, fx_config1):
+    """The 200-frame torch-seeded trajectory of the reference (test_gpu_parity.py's dense
+    test) with the cutoff: same classes, posterior and mean to 1e-5."""
+    from gpmdm_amd import GPMDM_PF
+    f = fx_config1
+    torch.manual_seed(11)
+    pf = GPMDM_PF(m1c, torch.tensor(f["T"]), 100, obs_cutoff=True)
+    wp = wm = 0.0
+    for k in range(200):
+        pf.update(f["z"][k])
+        assert pf.get_most_likely_class() == int(f["traj_most_likely"][k])
+        wp = max(wp, float(np.max(np.abs(pf.class_probabilities().numpy() - f["traj_posterior"][k]))))
+        wm = max(wm, nrel(pf.current_state_mean().numpy(), f["traj_mean"][k]))
+    assert wp < 1e-5 and wm < 1e-5, (wp, wm)
+
+
+def test_philox_steps_cutoff_vs_oracle(m2c, fx_config2):
+    """The benchmarked configuration (config-2 model, P = 100k, Philox, multinomial): three
+    resynced steps after a warm-up step against the oracle (conftest.assert_step_matches:
+    weights 1e-5, indices of the GPU's weights exact up to 2 ties, states / read-outs 1e-6)."""
+    from gpmdm_amd import GPMDM_PF
+    from oracle import gpmdm_oracle as O
+    from oracle import philox as X
+    om = oracle_model(fx_config2)
+    T = np.asarray(fx_config2["T"], dtype=np.float64)
+    P, seed = 100_000, 11
+    pf = GPMDM_PF(m2c, torch.tensor(T), P, rng="philox", seed=seed, obs_cutoff=True)
+    Y = m2c.get_Y()
+    pf.update(Y[10])
+    for k in range(3):
+        pre = pf.export_state()
+        frame = pf.frame
+        z = Y[11 + k] + 0.01
+        pf.update(z)
+        post = pf.export_state()
+        E = X.switch_draws(seed, frame, P, 2)
+        nrm = X.dynamics_normals(seed, frame, P, 3)
+        u = X.resample_uniforms(seed, frame, P)
+        r = O.step(om, T, pre["states"], pre["classes"], z, E, nrm, u, normals_by_particle=True)
+        assert_step_matches(post, r, pf.class_probabilities().numpy(), pf.current_state_mean().numpy(), u,
+                            "multinomial", ("cutoff", k))
+        assert pf.health() == {h: 0 for h in pf.health()}
+
+
+def test_cutoff_vs_dense_same_state(m2c, fx_config2):
+    """The cutoff and the dense kernel from one state with the same draws: log-likelihoods
+    and weights agree to the rounding of the two associations (the flushed values move q by
+    less than half an ulp of 1 - q by construction)."""
+    from gpmdm_amd import GPMDM_PF
+    T = torch.tensor(fx_config2["T"])
+    P = 20_000
+    Y = m2c.get_Y()
+    torch.manual_seed(3)
+    a = GPMDM_PF(m2c, T, P, rng="torch")
+    a.update(Y[30])
+    st = a.export_state()
+    b = GPMDM_PF(m2c, T, P, rng="torch", obs_cutoff=True)
+    b.load_state(st["states"], st["classes"], ll=st["ll"], log_w=st["log_w"], w=st["w"],
+                 resample_idx=st["resample_idx"], frame=st.get("frame"))
+    rng = np.random.RandomState(5)
+    E, nrm, u = rng.exponential(size=(P, 2)), rng.randn(P, 3), rng.rand(P)
+    a.update_with_draws(Y[31], E, nrm, u)
+    b.update_with_draws(Y[31], E, nrm, u)
+    sa, sb = a.export_state(), b.export_state()
+    assert np.array_equal(sa["classes"], sb["classes"])
+    dll = np.max(np.abs(sa["ll"] - sb["ll"]) / np.maximum(np.abs(sa["ll"]), 1.0))
+    assert dll < 1e-8, dll
+    assert nrel(sb["w"], sa["w"]) < 1e-7, nrel(sb["w"], sa["w"])
+
+
+@pytest.mark.parametrize("world,P", [(4, 10_007), (8, 100_000)])
+def test_cutoff_logical_shards_match_one_rank(m2c, world, P):
+    """R logical shards of a cutoff filter (ancestor-ordered shards: another particle tiling
+    than one rank's) are bitwise the one-rank cutoff filter over 3 frames."""
+    from gpmdm_amd import GPMDM_PF
+    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
+    Y = m2c.get_Y()
+    torch.manual_seed(4)
+    ref = GPMDM_PF(m2c, T, P, rng="philox", seed=91, obs_cutoff=True)
+    ranks = []
+    for r in range(world):
+        torch.manual_seed(4)
+        ranks.append(GPMDM_PF(m2c, T, P, rng="philox", seed=91, shard=(world, r), obs_cutoff=True))
+    for k in range(3):
+        z = np.ascontiguousarray(np.asarray(Y[60 + 3 * k], dtype=np.float64))
+        ref.update(z)
+        full = torch.cat([pf._stage_propagate(z) for pf in ranks], 0)
+        for pf in ranks:
+            pf._recv.copy_(full)
+            pf._stage_resample()
+        a = ref.export_state()
+        for pf in ranks:
+            b = pf.export_state()
+            for key in ("states", "classes", "ll", "resample_idx"):
+                assert np.array_equal(a[key], b[key]), (k, key)
+            assert np.array_equal(ref.class_probabilities().numpy(), pf.class_probabilities().numpy())
+
+
+def test_cutoff_skips_work_on_the_benchmark_cloud(m2c):
+    """The bench's workload (config-2 model, P = 100k, the mocap-surrogate stream): the
+    cutoff kernel runs a fraction of the dense kernel's MFMA groups."""
+    from gpmdm_amd import GPMDM_PF, synthetic
+    data = synthetic.make_sequences(2, 5, 200, 62, 3, seed=0)
+    zs = data.observation_stream(8, seed=1)
+    pf = GPMDM_PF(m2c, torch.tensor(synthetic.markov_matrix(2)), 100_000, rng="philox", seed=11)
+    pf.set_obs_cutoff(True, stats=True)
+    for k in range(6):
+        pf.update(zs[k])
+    pf.obs_cutoff_stats(reset=True)
+    pf.update(zs[6])
+    st = pf.obs_cutoff_stats()
+    assert st["dense"] > 0 and 0 < st["run"] < st["dense"], st
