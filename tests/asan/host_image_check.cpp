@@ -6,6 +6,7 @@
 // Packing check, independent of the layout formula: R and M are filled with distinct
 // values, so a correct image is a permutation of exactly the non-zero entries of
 // B = [triu(R) | M] plus zeros -- every distinct value must occur exactly once.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <map>
@@ -117,8 +118,75 @@ static void check_desc() {
   EXPECT(check_model_desc(&d) == "class 1 has no dynamics rows", "Nc=0");
 }
 
+// The cutoff image (gpmdm_model_set_obs_cutoff): spatial_order is a permutation whose
+// K-steps are full leaves but the last; every row lies inside its K-step's sphere; the
+// symmetric block image stores exactly 2 K^-1 off the diagonal blocks and K^-1 on them, in
+// the permuted order, and nothing below the block diagonal; tau obeys its two bounds.
+static void check_cutoff(int n, int D, int d) {
+  std::mt19937_64 rng(n * 17 + d);
+  std::normal_distribution<double> G(0.0, 3.0);
+  std::vector<double> X((size_t)n * d), ls(d), S((size_t)n * n), M((size_t)n * D), ymax(D);
+  for (auto& v : X) v = G(rng);
+  for (int j = 0; j < d; ++j) ls[j] = 0.7 + 0.1 * j;
+  for (long long i = 0; i < n; ++i)
+    for (long long j = 0; j < n; ++j) S[i * n + j] = 1.0 + (double)(std::min(i, j) * n + std::max(i, j));   // symmetric
+  for (auto& v : M) v = G(rng);
+  for (auto& v : ymax) v = 1.0 + std::fabs(G(rng));
+  const std::vector<long long> perm = spatial_order(X.data(), ls.data(), n, d);
+  std::vector<int> hit(n, 0);
+  for (long long r : perm) {
+    EXPECT(r >= 0 && r < n, "perm value %lld", r);
+    if (r >= 0 && r < n) ++hit[r];
+  }
+  for (int i = 0; i < n; ++i) EXPECT(hit[i] == 1, "row %d appears %d times", i, hit[i]);
+  std::vector<double> sph;
+  kstep_spheres(X.data(), ls.data(), perm.data(), n, d, sph);
+  const long long nks = (n + kBK - 1) / kBK;
+  EXPECT((long long)sph.size() == nks * (d + 1), "spheres %zu", sph.size());
+  for (long long r = 0; r < n; ++r) {
+    const long long k = r / kBK;
+    double s = 0.0;
+    for (int j = 0; j < d; ++j) {
+      const double t = X[perm[r] * d + j] / ls[j] - sph[k * (d + 1) + j];
+      s += t * t;
+    }
+    EXPECT(std::sqrt(s) <= sph[k * (d + 1) + d], "row %lld outside its sphere", r);
+  }
+  ImagePacker pk(n, d, D, X.data(), ls.data(), nullptr, S.data(), M.data(), kGeo32x512);
+  pk.sym = true;
+  pk.perm = perm.data();
+  for (long long i = 0; i < n; ++i)
+    for (long long j = 0; j < n + D; ++j) {
+      const double v = pk.val(i, j);
+      double want;
+      if (j >= n) want = M[perm[i] * D + (j - n)];
+      else if (i / kBK > j / kBK) want = 0.0;
+      else want = (i / kBK < j / kBK ? 2.0 : 1.0) * S[perm[i] * n + perm[j]];
+      EXPECT(v == want, "sym val(%lld, %lld) %.17g vs %.17g", i, j, v, want);
+    }
+  std::vector<double> img((size_t)pk.total_doubles());
+  long long off = 0;
+  for (int J = 0; J < pk.n_j; ++J) {
+    pk.pack_block(J, img.data() + off);
+    off += pk.block_doubles(J);
+  }
+  EXPECT(off == (long long)img.size(), "sym total");
+  const double sigma2 = 0.01;
+  const double tau = obs_cutoff_tau(n, sigma2, M.data(), D, ymax.data());
+  const double vc_min = sigma2 / (n + sigma2);
+  const double e = std::sqrt((double)n) * tau / std::sqrt(sigma2);
+  EXPECT(tau > 0.0 && (2.0 + e) * e <= 0.5 * (std::nextafter(vc_min, 1.0) - vc_min), "tau_q bound %.3g", tau);
+  for (int j = 0; j < D; ++j) {
+    double m1 = 0.0;
+    for (int i = 0; i < n; ++i) m1 += std::fabs(M[(size_t)i * D + j]);
+    EXPECT(tau * m1 <= 0.5 * (std::nextafter(ymax[j], 1e308) - ymax[j]), "tau_mu bound column %d", j);
+  }
+}
+
 int main() {
   check_desc();
+  const int cut[][3] = {{1, 2, 1}, {16, 3, 2}, {37, 5, 3}, {300, 7, 8}, {517, 4, 16}};
+  for (const auto& c : cut) check_cutoff(c[0], c[1], c[2]);
   const TileGeo geos[] = {kGeo64x256, kGeo64x512, kGeo32x512, kGeo32x256, kGeo16x256};
   const int shapes[][3] = {{1, 1, 1}, {7, 3, 2}, {16, 62, 3}, {17, 5, 3}, {250, 62, 3}, {513, 8, 16}, {300, 3, 8}};
   for (const auto& g : geos)
