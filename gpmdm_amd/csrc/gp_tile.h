@@ -340,11 +340,12 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     for (int k = k0, q = base; k < k1; ++k)
       if (bits >> (k - k0) & 1u) klist[q++] = (unsigned short)k;
     n_act = __builtin_amdgcn_readfirstlane(n_act);
-    // this wave's column tiles: an R tile is active with its own K-step, mean tiles always
+    // this wave's column tiles: an R tile is active with its own K-step, a tile holding mean
+    // columns always (including the tile that straddles n_rows when 16 does not divide N)
 #pragma unroll
     for (int tt = 0; tt < NTW; ++tt) {
       const int c0 = J * NB + 16 * (NW * tt + w) - coff;
-      const bool act = c0 >= 0 && (c0 >= n_rows ? c0 < n_cols : (kbits[c0 >> 9] >> ((c0 >> 4) & 31)) & 1u);
+      const bool act = c0 >= 0 && (c0 + 16 > n_rows ? c0 < n_cols : (kbits[c0 >> 9] >> ((c0 >> 4) & 31)) & 1u);
       if (!act) cmask &= ~(1u << tt);
     }
     cmask = __builtin_amdgcn_readfirstlane(cmask);
