@@ -227,8 +227,11 @@ struct gpmdm_pf {
   int* own_next = nullptr;
   int* inv_next = nullptr;
   long long own_next_frame = -1;     // the frame own_next was computed for (-1: none)
+  // (single-rank filters keep it only with the observation-GP cutoff: particles of one
+  // resampling-ancestor range form compact tiles, which skip more of the cutoff's K-steps)
   bool order_wanted() const {
-    return own && dedup && shard_order && resample_mode != GPMDM_RESAMPLE_SYSTEMATIC && uniform_order_supported(P);
+    return own && (n_ranks > 1 || obs_cutoff) && dedup && shard_order && resample_mode != GPMDM_RESAMPLE_SYSTEMATIC &&
+           uniform_order_supported(P);
   }
   // Exchanged rows read in place (gpmdm_pf_unpack_part): the all-gathered {class, state} rows
   // are read by the resample's gathers through the ownership order (only the ancestors' rows

@@ -602,6 +602,21 @@ int gpmdm_pf_set_obs_cutoff(gpmdm_pf_t pf, int mode) {
     const int tc[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, m->obs_cut.geo.pt())};
     HIPCHK(hipMemcpy(pf->obs_tab + 8, tc, sizeof(tc), hipMemcpyHostToDevice));
   }
+  if (mode && !pf->own && pf->rng_mode == GPMDM_RNG_PHILOX && pf->F == 1 && uniform_order_supported(pf->P)) {
+    // the ownership order for single-rank filters (order_wanted): resampling-ancestor ranges
+    // of particles evaluated together, so the cutoff's particle tiles are compact
+    pf->own_tmp_bytes = std::max<size_t>(uniform_order_temp_bytes(pf->P), 1);
+    if (dalloc(&pf->own, (size_t)pf->P) || dalloc(&pf->own_inv, (size_t)pf->P) || dalloc(&pf->own_next, (size_t)pf->P) ||
+        dalloc(&pf->inv_next, (size_t)pf->P) || dalloc(&pf->own_tmp, pf->own_tmp_bytes)) {
+      dfree(pf->own);
+      dfree(pf->own_inv);
+      dfree(pf->own_next);
+      dfree(pf->inv_next);
+      dfree(pf->own_tmp);
+      return fail(GPMDM_E_NOMEM, "ownership order buffers");
+    }
+  }
+  if (!mode && pf->n_ranks == 1) pf->own_valid = false;   // (the order is the cutoff's only)
   if (mode == 2 && !pf->sp_stats) {
     TRY(dalloc(&pf->sp_stats, 2));
     HIPCHK(hipMemset(pf->sp_stats, 0, 2 * sizeof(unsigned long long)));
