@@ -356,7 +356,8 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       for (int c = c_lo; c < c_hi; c += kBK) any = any || ((kbits[c >> 9] >> ((c >> 4) & 31)) & 1u);
     }
     if (prm.sp_stats && lane == 0) {
-      // MFMA groups (tile x K-step) this wave runs, and the dense kernel's
+      // MFMA groups (16 particles x 16 columns x one 16-row K-step: 4 MFMAs, 8192 FLOP) this
+      // wave runs, and the dense kernel's (each of the wave's tiles is MT particle groups)
       unsigned long long run = 0, dense = 0;
 #pragma unroll
       for (int tt = 0; tt < NTW; ++tt) {
@@ -367,8 +368,8 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
           if (e & 31) run += (unsigned)__builtin_popcount(kbits[e >> 5] & ((1u << (e & 31)) - 1u));
         }
       }
-      atomicAdd(prm.sp_stats + 0, run);
-      atomicAdd(prm.sp_stats + 1, dense);
+      atomicAdd(prm.sp_stats + 0, run * MT);
+      atomicAdd(prm.sp_stats + 1, dense * MT);
     }
     __syncthreads();                                           // klist complete
     if (!any) {

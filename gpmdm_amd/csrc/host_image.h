@@ -172,8 +172,7 @@ struct ImagePacker {
 // X / ls, leaves of kBK rows): K-steps of nearby points, so a compact particle tile is far
 // from most K-steps.  Every leaf holds exactly kBK rows but the last.  Returns perm (image
 // row -> training row).
-inline void spatial_order_rec(const double* X, const double* ls, int d, long long* idx, long long n,
-                              std::vector<double>& key) {
+inline void spatial_order_rec(const double* X, const double* ls, int d, long long* idx, long long n) {
   if (n <= kBK) return;
   int best = 0;
   double spread = -1.0;
@@ -196,14 +195,13 @@ inline void spatial_order_rec(const double* X, const double* ls, int d, long lon
   for (long long i = 0; i < n; ++i) idx[i] = kv[(size_t)i].second;
   const long long leaves = (n + kBK - 1) / kBK;
   const long long left = ((leaves + 1) / 2) * kBK;   // a multiple of kBK: full leaves on the left
-  spatial_order_rec(X, ls, d, idx, left, key);
-  spatial_order_rec(X, ls, d, idx + left, n - left, key);
+  spatial_order_rec(X, ls, d, idx, left);
+  spatial_order_rec(X, ls, d, idx + left, n - left);
 }
 inline std::vector<long long> spatial_order(const double* X, const double* ls, long long n, int d) {
   std::vector<long long> idx((size_t)n);
   for (long long i = 0; i < n; ++i) idx[(size_t)i] = i;
-  std::vector<double> key;
-  spatial_order_rec(X, ls, d, idx.data(), n, key);
+  spatial_order_rec(X, ls, d, idx.data(), n);
   return idx;
 }
 
