@@ -135,7 +135,9 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   constexpr int NG = NT / PT;                                // generation row groups
   constexpr int GV = kBK / NG;                               // K* values per thread per K-step
   static_assert(GV * NG == kBK, "generation split");
-  constexpr int LDA = PT + 16;                               // rows k, k+1 land 32 banks apart
+  // A-fragment rows k, k+1 (one 32-lane half of a ds_read_b64) land 32 banks apart: the row
+  // pitch is 16 (mod 32) doubles (PT = 16: PT + 16 = 32 put both rows on the same banks)
+  constexpr int LDA = (PT + 16) % 32 == 16 ? PT + 16 : PT + 32;
   constexpr int RW = DI + 1;                                 // row record: Xs[DI], |Xs|^2
   constexpr int NRV = kBK * RW;                              // row values per K-step
   constexpr int RPT = (NRV + NT - 1) / NT;                   // row values per thread
