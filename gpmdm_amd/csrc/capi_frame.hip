@@ -388,49 +388,75 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
   if (nl > 0) {
     // ---- observation GP + likelihood over particles [lo, hi) ----
     pf->mark_begin(s, GPMDM_STAGE_OBS_GEMM, t0);
-    TileParams tp{};
-    // the opt-in kernel-value cutoff: the cutoff image and kernel (same column blocks and
-    // partials as the default image: the finish below is shared)
-    const bool cut = pf->obs_cutoff && m->obs_cut.Bf;
-    const GpImage& oi = cut ? m->obs_cut : *pf->obs_img;
-    const int* tab = pf->obs_tab + (cut ? 8 : 0);
-    tp.seg[0] = oi.seg();
-    tp.n_seg = 1;
-    tp.geo = cut ? oi.geo : pf->obs_geo;
-    tp.tiles_ub = (int)cdiv(nl, tp.geo.pt());
-    tp.n_j_max = oi.n_j;
-    tp.seg_pos_begin = tab + 0;
-    tp.seg_pos_end = tab + 1;
-    tp.seg_out_base = tab + 2;
-    tp.seg_tile_start = tab + 3;
+    // the opt-in kernel-value cutoff: its own kernel over the cutoff image (obs_cutoff.h),
+    // one q and one S partial per particle
+    const bool cut = pf->obs_cutoff && m->has_cutoff();
+    const GpImage& oi = *pf->obs_img;
+    // Particle order of the tiles: positions [lo, hi) of the ownership order -- or, for a
+    // single-rank cutoff filter, the switch's class grouping (stable within a class in the
+    // ownership order, i.e. by resampling ancestor): a tile then holds particles propagated
+    // from one (ancestor, class) mean where it can, so its bounding sphere -- and the K-steps
+    // it reaches -- are small.  Any order gives the same values (the flush is per value).
+    const int* obs_order = (cut && pf->n_ranks == 1) ? pf->perm : pf->own_order();
     if (cut) {
-      tp.sparse = 1;
-      tp.ksph = m->obs_cut_sph;
-      tp.cut2 = m->cut2;
-      tp.t_cut = m->t_cut;
-      tp.sp_stats = pf->sp_stats_on ? pf->sp_stats : nullptr;
+      const auto& ci = m->obs_cut;
+      CutoffParams cp{};
+      cp.X = pf->X_prop;
+      cp.perm = obs_order;
+      cp.pos_begin = (int)pf->lo;
+      cp.pos_end = (int)pf->hi;
+      for (int j = 0; j < d; ++j) cp.ls[j] = m->y_ls[j];
+      cp.Xrec = ci.Xrec;
+      cp.Bt = ci.Bt;
+      cp.toff = ci.toff;
+      cp.ksph = ci.sph;
+      cp.n_rows = ci.n_rows;
+      cp.n_m = ci.n_m;
+      cp.T_R = ci.T_R;
+      cp.T_M = ci.T_M;
+      cp.cut2 = m->cut2;
+      cp.t_cut = m->t_cut;
+      cp.q = pf->qobs;
+      cp.S = pf->sobs;
+      cp.z = zsrc;
+      cp.lam2 = m->y_lam2_dev;
+      cp.Pf = pf->Pf;
+      cp.sp_stats = pf->sp_stats_on ? pf->sp_stats : nullptr;
+      launch_obs_cutoff(cp, d, s);
+    } else {
+      TileParams tp{};
+      const int* tab = pf->obs_tab;
+      tp.seg[0] = oi.seg();
+      tp.n_seg = 1;
+      tp.geo = pf->obs_geo;
+      tp.tiles_ub = (int)cdiv(nl, tp.geo.pt());
+      tp.n_j_max = oi.n_j;
+      tp.seg_pos_begin = tab + 0;
+      tp.seg_pos_end = tab + 1;
+      tp.seg_out_base = tab + 2;
+      tp.seg_tile_start = tab + 3;
+      tp.perm = obs_order;
+      tp.X = pf->X_prop;
+      fill_tile_common(tp, m, false);
+      tp.qpart = pf->qobs;
+      tp.ld_q = nl;
+      tp.spart = pf->sobs;
+      tp.z = zsrc;
+      tp.lam2 = m->y_lam2_dev;
+      tp.Pf = pf->Pf;
+      launch_gp_tile(tp, d, false, s);
     }
-    tp.perm = pf->own_order();           // positions [lo, hi) of the ownership order
-    tp.X = pf->X_prop;
-    fill_tile_common(tp, m, false);
-    tp.qpart = pf->qobs;
-    tp.ld_q = nl;
-    tp.spart = pf->sobs;
-    tp.z = zsrc;
-    tp.lam2 = m->y_lam2_dev;
-    tp.Pf = pf->Pf;
-    launch_gp_tile(tp, d, false, s);
     pf->mark_end(s, GPMDM_STAGE_OBS_GEMM, t0);
     pf->mark_begin(s, GPMDM_STAGE_OBS_FINISH, t0);
     ObsFinishArgs oa{};
     oa.n_out = nl;
-    oa.n_parts = oi.n_parts();
+    oa.n_parts = cut ? 1 : oi.n_parts();
     oa.D = D;
     oa.qpart = pf->qobs;
     oa.ld_q = nl;
     oa.spart = pf->sobs;
-    oa.jm0 = oi.jm0();                   // first part with mean columns
-    oa.n_j = oi.n_pblocks();
+    oa.jm0 = cut ? 0 : oi.jm0();         // first part with mean columns
+    oa.n_j = cut ? 1 : oi.n_pblocks();
     oa.sum_log_il2 = m->sum_log_il2;
     oa.z = zsrc;
     oa.Pf = pf->Pf;
@@ -438,7 +464,7 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     oa.ll_const = (double)((float)(0.5 * D) * (float)1.8378770351409912);
     oa.ll = pf->ll;
     oa.ll_offset = pf->lo;
-    oa.own = pf->own_order();
+    oa.own = obs_order;
     oa.health = pf->health;
     pf->ll_pending = false;
     pf->bmax_ready = false;

@@ -83,8 +83,7 @@ struct GpImage {
 };
 
 int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const double* ls,
-                const double* lin_c2, const double* R, const double* M, TileGeo geo,
-                const long long* perm = nullptr, bool sym = false);
+                const double* lin_c2, const double* R, const double* M, TileGeo geo);
 
 }  // namespace gpmdm::capi
 
@@ -121,16 +120,25 @@ struct gpmdm_model {
   double* y_lam2_dev = nullptr;   // 1 / il2 = exp(y_log_lambdas)^2
   double sum_log_il2 = 0.0;
   // Observation-GP cutoff image (gpmdm_model_set_obs_cutoff; empty: not set): K^-1's block
-  // upper triangle over the training rows in a spatial order, the K-step spheres, and the
-  // cutoff (tau; cut2 = the squared scaled distance past which a value is below tau, with a
-  // margin; t_cut = ln tau in the tile kernel's exponent units)
-  GpImage obs_cut;
-  double* obs_cut_sph = nullptr;
+  // upper triangle and M over the training rows in a spatial order, tile-major
+  // (host_image.h CutoffPacker, obs_cutoff.h), the K-step spheres, and the cutoff (tau; cut2 =
+  // the squared scaled distance past which a value is below tau, with a margin; t_cut = ln tau
+  // in the generation's exponent units)
+  struct CutImage {
+    int n_rows = 0, n_m = 0, T_R = 0, T_M = 0;
+    double* Xrec = nullptr;
+    double* Bt = nullptr;
+    long long* toff = nullptr;
+    double* sph = nullptr;
+  } obs_cut;
+  bool has_cutoff() const { return obs_cut.Bt != nullptr; }
   double cut_tau = 0.0, cut2 = 0.0, t_cut = 0.0;
   void release_cutoff() {
-    obs_cut.release();
-    obs_cut = GpImage{};
-    dfree(obs_cut_sph);
+    dfree(obs_cut.Xrec);
+    dfree(obs_cut.Bt);
+    dfree(obs_cut.toff);
+    dfree(obs_cut.sph);
+    obs_cut = CutImage{};
   }
 
   ~gpmdm_model() {
@@ -387,7 +395,7 @@ struct gpmdm_pf {
   // the leader election's owner table is all 0xffffffff (the last compaction restored it)
   bool owner_clean = false;
   double *e = nullptr, *local = nullptr, *blocksum = nullptr, *blockoffw = nullptr, *total = nullptr,
-         *cum = nullptr, *partials = nullptr, *readout = nullptr;
+         *partials = nullptr, *readout = nullptr;
   // library-driven exchange (gpmdm_pf_set_comm): an RCCL communicator of n_ranks ranks, a
   // library-owned stream for the collectives, and the packed rows.  pad = rows per rank in
   // the collective (the largest shard; ranks' shards differ by at most one row).  When the
@@ -499,7 +507,7 @@ struct gpmdm_pf {
     if (up_stream) (void)hipStreamSynchronize(up_stream);
     release_comm();
     double* ds[] = {T, X, X_prop, ll, qdyn, mudyn, qobs, sobs, z, E, normals, U,
-                    e, local, blocksum, blockoffw, total, cum, partials, readout,
+                    e, local, blocksum, blockoffw, total, partials, readout,
                     pred_q, pred_mu, pred_mu_p, pred_out};
     for (double* p : ds) dfree(p);
     int* is[] = {cls, cls_new, perm, ridx, blockcounts, blockoff, small, obs_tab,

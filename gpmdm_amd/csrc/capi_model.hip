@@ -26,11 +26,8 @@ int upload(T** dst, const std::vector<T>& v) {
 }
 
 int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const double* ls,
-                const double* lin_c2, const double* R, const double* M, TileGeo geo, const long long* perm,
-                bool sym) {
+                const double* lin_c2, const double* R, const double* M, TileGeo geo) {
   ImagePacker pk(n_rows, d, n_m, X, ls, lin_c2, R, M, geo);
-  pk.perm = perm;
-  pk.sym = sym;
   g.geo = geo;
   g.dyn = lin_c2 != nullptr;
   g.n_rows = n_rows;
@@ -190,7 +187,8 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
 
 // The observation GP's opt-in kernel-value cutoff (DESIGN.md §3 "Kernel-value cutoff"):
 // the K^-1 image in the symmetric block form over a spatial order of the training rows,
-// the per-K-step bounding spheres and tau (host_image.h).  K_inv = NULL removes it.
+// tile-major (host_image.h CutoffPacker), the per-K-step bounding spheres and tau.
+// K_inv = NULL removes it.
 int gpmdm_model_set_obs_cutoff(gpmdm_model_t m, const double* K_inv, const double* beta, double sigma2,
                                const double* y_absmax) {
   CHECK(m, "null model");
@@ -204,27 +202,43 @@ int gpmdm_model_set_obs_cutoff(gpmdm_model_t m, const double* K_inv, const doubl
   CHECK(sigma2 > 0.0 && std::isfinite(sigma2), "sigma2 must be positive (the observation noise variance)");
   CHECK(ksteps((int)m->N) <= kMaxCutoffKs, "the cutoff image holds at most 65536 training rows");
   CHECK(m->d <= 16, "the cutoff image is built for latent dimensions d <= 16");
-  // its own tile shape (512 columns per block, as the default observation images: the same
-  // partials, so the filter's likelihood finish and buffers serve both): 32 x 512 up to d = 8,
-  // 64 x 512 above (gp_tile.h launch_d)
-  const TileGeo g = m->d <= 8 ? kGeo32x512 : kGeo64x512;
-  CHECK(m->obs.geo.nb() == g.nb() && cdiv(m->N + m->D, g.nb()) == m->obs.n_j,
-        "the cutoff image needs a model with 512-column observation blocks (the default tile shapes)");
   const int N = (int)m->N, d = m->d;
   const double tau = obs_cutoff_tau(N, sigma2, beta, m->D, y_absmax);
   CHECK(tau > 0.0 && std::isfinite(tau), "no usable cutoff for this model");
   const std::vector<long long> perm = spatial_order(m->X.data(), m->y_ls.data(), N, d);
-  std::vector<double> sph;
+  CutoffPacker pk(N, d, m->D, m->X.data(), m->y_ls.data(), K_inv, beta, perm.data());
+  const std::vector<long long> toff = pk.offsets();
+  // the kernel addresses the image with 32-bit byte offsets (one buffer resource)
+  CHECK(toff.back() * 8 < (1LL << 32), "the cutoff image exceeds 4 GiB (about 32k training rows)");
+  std::vector<double> sph, rec;
   kstep_spheres(m->X.data(), m->y_ls.data(), perm.data(), N, d, sph);
+  pk.records(rec);
   HIPCHK(hipDeviceSynchronize());
   m->release_cutoff();
-  int rc = build_image(m->obs_cut, N, d, m->D, m->X.data(), m->y_ls.data(), nullptr, K_inv, beta, g, perm.data(),
-                       true);
-  if (!rc) rc = upload(&m->obs_cut_sph, sph);
+  auto& ci = m->obs_cut;
+  int rc = upload(&ci.sph, sph);
+  if (!rc) rc = upload(&ci.Xrec, rec);
+  if (!rc) rc = upload(&ci.toff, toff);
+  if (!rc) rc = dalloc(&ci.Bt, (size_t)toff.back());
+  // packed and uploaded a group of tiles at a time (the host never holds the whole image)
+  std::vector<double> buf;
+  for (int t0 = 0; !rc && t0 < pk.tiles();) {
+    int t1 = t0 + 1;
+    while (t1 < pk.tiles() && toff[(size_t)t1 + 1] - toff[(size_t)t0] <= (1LL << 22)) ++t1;
+    buf.assign((size_t)(toff[(size_t)t1] - toff[(size_t)t0]), 0.0);
+    for (int t = t0; t < t1; ++t) pk.pack_tile(t, buf.data() + (toff[(size_t)t] - toff[(size_t)t0]));
+    if (hipMemcpy(ci.Bt + toff[(size_t)t0], buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+      rc = fail(GPMDM_E_HIP, "upload of the cutoff image");
+    t0 = t1;
+  }
   if (rc) {
     m->release_cutoff();
     return rc;
   }
+  ci.n_rows = N;
+  ci.n_m = m->D;
+  ci.T_R = pk.T_R;
+  ci.T_M = pk.T_M;
   m->cut_tau = tau;
   m->cut2 = -std::log(tau) * (1.0 + 1e-12) + 1e-6;   // margin over both tests' rounding
   m->t_cut = std::log(tau) * kLog2eX64;
@@ -233,7 +247,7 @@ int gpmdm_model_set_obs_cutoff(gpmdm_model_t m, const double* K_inv, const doubl
 
 int gpmdm_model_obs_cutoff(gpmdm_model_t m, double* tau) {
   CHECK(m && tau, "null argument");
-  *tau = m->obs_cut.Bf ? m->cut_tau : 0.0;
+  *tau = m->has_cutoff() ? m->cut_tau : 0.0;
   return GPMDM_OK;
 }
 

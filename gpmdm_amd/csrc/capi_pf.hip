@@ -79,7 +79,6 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   ALLOC(blocksum, F * pf->nbf);
   ALLOC(blockoffw, F * pf->nbf);
   ALLOC(total, F);
-  ALLOC(cum, P);
   ALLOC(guide, guide_buckets_used(Pf) > 0 ? F * (guide_buckets(Pf) + 3) : 1);
   ALLOC(partials, F * pf->nbf * (C + 1 + d));
   ALLOC(readout, F * (C + d + 1));
@@ -218,7 +217,8 @@ ResampleArgs resample_args(gpmdm_pf* pf) {
   ra.frame = pf->frame;
   ra.seed_lo = pf->seed_lo;
   ra.seed_hi = pf->seed_hi;
-  ra.cum = pf->cum;
+  ra.local = pf->local;
+  ra.blockoff = pf->blockoffw;
   ra.ll = pf->ll;
   ra.e = pf->e;
   ra.total = pf->total;
@@ -250,7 +250,6 @@ NormArgs norm_args(gpmdm_pf* pf) {
   na.blocksum = pf->blocksum;
   na.blockoff = pf->blockoffw;
   na.total = pf->total;
-  na.cum = pf->cum;
   if (pf->ll_pending) {
     na.obs = pf->oa_pending;
     na.obs_pending = 1;
@@ -562,11 +561,6 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, og.pt())};
   if (!rc && hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess)
     rc = fail(GPMDM_E_HIP, "upload of the observation tile table");
-  if (!rc && m->obs_cut.Bf) {         // the cutoff image's tile table (its own tile height)
-    const int tc[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, m->obs_cut.geo.pt())};
-    if (hipMemcpy(pf->obs_tab + 8, tc, sizeof(tc), hipMemcpyHostToDevice) != hipSuccess)
-      rc = fail(GPMDM_E_HIP, "upload of the observation tile table");
-  }
   if (rc) {
     dfree(qdyn);
     dfree(qobs);
@@ -597,11 +591,7 @@ int gpmdm_pf_set_obs_cutoff(gpmdm_pf_t pf, int mode) {
   if (pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "set_obs_cutoff between propagate and resample");
   gpmdm_model* m = pf->m;
   HIPCHK(hipSetDevice(m->device));
-  if (mode && !m->obs_cut.Bf) return fail(GPMDM_E_STATE, "the model has no cutoff image (gpmdm_model_set_obs_cutoff)");
-  if (mode) {
-    const int tc[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, m->obs_cut.geo.pt())};
-    HIPCHK(hipMemcpy(pf->obs_tab + 8, tc, sizeof(tc), hipMemcpyHostToDevice));
-  }
+  if (mode && !m->has_cutoff()) return fail(GPMDM_E_STATE, "the model has no cutoff image (gpmdm_model_set_obs_cutoff)");
   if (mode && !pf->own && pf->rng_mode == GPMDM_RNG_PHILOX && pf->F == 1 && uniform_order_supported(pf->P)) {
     // the ownership order for single-rank filters (order_wanted): resampling-ancestor ranges
     // of particles evaluated together, so the cutoff's particle tiles are compact

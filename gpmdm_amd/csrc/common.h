@@ -44,18 +44,31 @@ struct TileParams {
   const double* z;                // F x n_m
   const double* lam2;             // n_m: exp(y_log_lambdas)^2 = 1 / il2
   long long Pf;                   // particles per filter
-  // Observation-GP cutoff (the kTileSparse kernels, gp_tile.h; DESIGN.md §3 "Kernel-value
-  // cutoff"): per-K-step bounding spheres of the image rows (centre d, radius; scaled
-  // coordinates), the squared scaled distance beyond which every kernel value is below tau,
-  // and the flush threshold in the generation's units (t = 64/ln2 x natural exponent)
-  int sparse;                     // 0: the dense kernel
-  const double* ksph;
-  double cut2;
-  double t_cut;
-  unsigned long long* sp_stats;   // nullable: [0] MFMA groups executed, [1] the dense kernel's count
 };
 
 void launch_gp_tile(const TileParams& p, int d, bool dyn, hipStream_t stream);
+
+// The observation GP's kernel-value cutoff kernel (obs_cutoff.h).
+struct CutoffParams {
+  const double* X;           // particle states, d doubles each
+  const int* perm;           // tile position -> particle (nullptr: identity)
+  int pos_begin, pos_end;    // this launch's positions; outputs at pos - pos_begin
+  double ls[kMaxD];          // observation GP lengthscales
+  const double* Xrec;        // row records in image-row order, row_cap(n_rows) rows
+  const double* Bt;          // the tile-major image
+  const long long* toff;     // first double of each tile (T_R + T_M + 1)
+  const double* ksph;        // per K-step bounding sphere: centre (d), radius
+  int n_rows, n_m, T_R, T_M;
+  double cut2;               // squared cutoff distance (scaled units), with rounding margin
+  double t_cut;              // the flush threshold on the generation's exponent
+  double* q;                 // per position: k^T K^-1 k
+  double* S;                 // per position: sum_j (z_j - mu_j)^2 lam2_j
+  const double* z;           // F x n_m observations
+  const double* lam2;        // n_m
+  long long Pf;              // particles per filter
+  unsigned long long* sp_stats;   // MFMA groups run / the dense kernel's, or nullptr
+};
+void launch_obs_cutoff(const CutoffParams& p, int d, hipStream_t stream);
 
 // ---------------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11), counter = (index, frame, stream, sub).

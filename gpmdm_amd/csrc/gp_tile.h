@@ -92,20 +92,6 @@ __device__ __forceinline__ double exp2_64(double t, const double* tab) {
 // The A/B variants measured against this kernel (other exp tables, barrier cadences, wave
 // specialisation, the K* cache, ablations) live in tools/microbench/gp_tile_lab.h.
 constexpr int kTileCoordLDS = 131072;
-// kTileSparse -- the observation GP's opt-in kernel-value cutoff (DESIGN.md §3 "Kernel-value
-// cutoff"; host side: host_image.h obs_cutoff_tau / spatial_order / kstep_spheres):
-//  * every generated value below tau is flushed to exactly 0 (t < t_cut), so the result is
-//    the dense one with those values replaced by 0 -- whatever the tile;
-//  * B is the cutoff image (K^-1's block upper triangle, off-diagonal blocks doubled, rows in
-//    a spatial order), so q = sum_j k_j V_j (the epilogue regenerates k_j) instead of |V|^2;
-//  * a K-step whose 16 rows are all farther than the cutoff from the tile's bounding sphere
-//    is skipped (its values would all be 0), and so is every MFMA of a column tile whose
-//    K-step is skipped (V_j k_j = 0 for every particle of the tile).  Skipping adds nothing
-//    that was not an exact 0, so the results do not depend on which K-steps a tile skips.
-// Limits: N <= kMaxSparseKs x 16 training rows (the host refuses larger models).
-constexpr int kTileSparse = 262144;
-constexpr int kMaxSparseKs = kMaxCutoffKs;
-
 template <int I, int E, class F>
 __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (I < E) {
@@ -118,9 +104,7 @@ template <int DI, bool DYN, int FLAGS = 0, int NW = 4, int MT = 4, int NTW = 4>
 __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const TileParams prm) {
   static_assert(MT == 1 || MT == 2 || MT == 4, "MT");
   static_assert(NTW == 4 || NTW == 6 || NTW == 8 || NTW == 16, "NTW");
-  static_assert((FLAGS & ~(kTileCoordLDS | kTileSparse)) == 0, "FLAGS");
-  constexpr bool SP = (FLAGS & kTileSparse) != 0;
-  static_assert(!SP || !DYN, "the cutoff kernel is the observation GP's");
+  static_assert((FLAGS & ~kTileCoordLDS) == 0, "FLAGS");
   // B fragments in flight: BR sub-steps (a full K-step, 4, for NTW <= 8; 2 for NTW = 16,
   // whose full K-step of fragments would not fit next to 128 accumulator VGPRs)
   constexpr int BR = NTW >= 16 ? 2 : 4;
@@ -135,9 +119,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   constexpr int NG = NT / PT;                                // generation row groups
   constexpr int GV = kBK / NG;                               // K* values per thread per K-step
   static_assert(GV * NG == kBK, "generation split");
-  // A-fragment rows k, k+1 (one 32-lane half of a ds_read_b64) land 32 banks apart: the row
-  // pitch is 16 (mod 32) doubles (PT = 16: PT + 16 = 32 put both rows on the same banks)
-  constexpr int LDA = (PT + 16) % 32 == 16 ? PT + 16 : PT + 32;
+  constexpr int LDA = PT + 16;                               // rows k, k+1 land 32 banks apart
   constexpr int RW = DI + 1;                                 // row record: Xs[DI], |Xs|^2
   constexpr int NRV = kBK * RW;                              // row values per K-step
   constexpr int RPT = (NRV + NT - 1) / NT;                   // row values per thread
@@ -165,13 +147,6 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   constexpr bool PLDS = (FLAGS & kTileCoordLDS) != 0;
   __shared__ double PA[PLDS ? PT : 1][PLDS ? DI + 1 : 1];
   __shared__ double sred[NHS * NW][PT];
-  // SP: the block's active K-steps (ascending), their bitmask, the tile's particles (a2, asq),
-  // the tile's bounding sphere (centre, radius; in a2 units) and per-wave counts
-  __shared__ unsigned short klist[SP ? kMaxSparseKs : 1];
-  __shared__ unsigned kbits[SP ? kMaxSparseKs / 32 : 1];
-  __shared__ double PK[SP ? PT : 1][SP ? DI + 1 : 1];
-  __shared__ double tsph[SP ? DI + 1 : 1];
-  __shared__ int wtot[SP ? NW : 1];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -268,127 +243,6 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   for (int tt = 0; tt < NTW; ++tt) kmaxw = max(kmaxw, kend[tt]);
   const int ks_last = (kmaxw > 0 ? kmaxw : 1) - 1;
 
-  // ---- SP: which K-steps of the block's range [0, nks) can hold a value above the cutoff --
-  int n_act = nks;                                           // positions of the K loop
-  unsigned cmask = ~0u;                                      // this wave's active column tiles
-  if constexpr (SP) {
-    if (g == 0) {
-#pragma unroll
-      for (int j = 0; j < DI; ++j) PK[m][j] = a2[j];
-      PK[m][DI] = asq;
-    }
-    __syncthreads();
-    // the tile's bounding sphere in a2 units (2 kScale x / l): centre = mean, radius = the
-    // largest distance, padded (the K-step spheres are in x / l units: scaled below)
-    if (tid < DI) {
-      double c = 0.0;
-      for (int p = 0; p < PT; ++p) c += PK[p][tid];
-      tsph[tid] = c * (1.0 / PT);
-    }
-    for (int i = tid; i < kMaxSparseKs / 32; i += NT) kbits[i] = 0u;
-    __syncthreads();
-    if (w == 0) {
-      double r2 = 0.0;
-      if (lane < PT) {
-#pragma unroll
-        for (int j = 0; j < DI; ++j) {
-          const double t = PK[lane][j] - tsph[j];
-          r2 = fma(t, t, r2);
-        }
-      }
-      r2 = wave_max(r2);
-      if (lane == 0) tsph[DI] = sqrt(r2) * (1.0 + 1e-12) + 1e-12;
-    }
-    __syncthreads();
-    // K-step k is inactive when the gap between the spheres exceeds the cutoff distance: every
-    // value is then exp(-|x - X_i|^2) < tau, i.e. t < t_cut, and flushed (the margin in cut2
-    // covers the rounding of both tests).  Each thread tests a contiguous range of K-steps.
-    constexpr double kInv = 1.0 / (2.0 * kScale);
-    const int per = (nks + NT - 1) / NT;
-    const int k0 = tid * per, k1 = min(k0 + per, nks);
-    const double rt = tsph[DI] * kInv;
-    unsigned bits = 0u;                                        // per <= 16 (nks <= 4096, NT >= 256)
-    for (int k = k0; k < k1; ++k) {
-      const double* sp = prm.ksph + (long long)k * (DI + 1);
-      double d2 = 0.0;
-#pragma unroll
-      for (int j = 0; j < DI; ++j) {
-        const double t = tsph[j] * kInv - sp[j];
-        d2 = fma(t, t, d2);
-      }
-      const double gap = sqrt(d2) - rt - sp[DI];
-      const bool off = gap > 0.0 && gap * gap > prm.cut2;
-      if (!off) {
-        bits |= 1u << (k - k0);
-        atomicOr(&kbits[k >> 5], 1u << (k & 31));
-      }
-    }
-    // positions: an exclusive scan of the per-thread counts (wave shuffles, wave totals in LDS)
-    const int cnt = __builtin_popcount(bits);
-    int incl = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(incl, off);
-      if (lane >= off) incl += y;
-    }
-    if (lane == 63) wtot[w] = incl;
-    __syncthreads();
-    int base = incl - cnt;
-    n_act = 0;
-    for (int ww = 0; ww < NW; ++ww) {
-      base += ww < w ? wtot[ww] : 0;
-      n_act += wtot[ww];
-    }
-    for (int k = k0, q = base; k < k1; ++k)
-      if (bits >> (k - k0) & 1u) klist[q++] = (unsigned short)k;
-    n_act = __builtin_amdgcn_readfirstlane(n_act);
-    // this wave's column tiles: an R tile is active with its own K-step, a tile holding mean
-    // columns always (including the tile that straddles n_rows when 16 does not divide N)
-#pragma unroll
-    for (int tt = 0; tt < NTW; ++tt) {
-      const int c0 = J * NB + 16 * (NW * tt + w) - coff;
-      const bool act = c0 >= 0 && (c0 + 16 > n_rows ? c0 < n_cols : (kbits[c0 >> 9] >> ((c0 >> 4) & 31)) & 1u);
-      if (!act) cmask &= ~(1u << tt);
-    }
-    cmask = __builtin_amdgcn_readfirstlane(cmask);
-    // a block without an active column: its partial is 0 (the other waves' tiles included)
-    bool any = (J + 1) * NB - coff > n_rows;                   // holds mean columns
-    {
-      const int c_lo = max(J * NB - coff, 0), c_hi = min((J + 1) * NB - coff, n_rows);
-      for (int c = c_lo; c < c_hi; c += kBK) any = any || ((kbits[c >> 9] >> ((c >> 4) & 31)) & 1u);
-    }
-    if (prm.sp_stats && lane == 0) {
-      // MFMA groups (16 particles x 16 columns x one 16-row K-step: 4 MFMAs, 8192 FLOP) this
-      // wave runs, and the dense kernel's (each of the wave's tiles is MT particle groups)
-      unsigned long long run = 0, dense = 0;
-#pragma unroll
-      for (int tt = 0; tt < NTW; ++tt) {
-        dense += (unsigned)kend[tt];
-        if (any && (cmask >> tt & 1u)) {
-          const int e = kend[tt];
-          for (int q = 0; q < (e >> 5); ++q) run += (unsigned)__builtin_popcount(kbits[q]);
-          if (e & 31) run += (unsigned)__builtin_popcount(kbits[e >> 5] & ((1u << (e & 31)) - 1u));
-        }
-      }
-      atomicAdd(prm.sp_stats + 0, run * MT);
-      atomicAdd(prm.sp_stats + 1, dense * MT);
-    }
-    __syncthreads();                                           // klist complete
-    if (!any) {
-      if (tid < PT && pos0 + tid < pos_end) prm.qpart[(long long)J * prm.ld_q + out_base + pos0 + tid] = 0.0;
-      return;
-    }
-  }
-  // the K-step at loop position i (the dense kernel: i itself)
-  auto kat = [&](int i) -> int {
-    if constexpr (SP) {
-      const int ii = i < n_act ? i : n_act - 1;
-      return ii >= 0 ? __builtin_amdgcn_readfirstlane((int)klist[ii]) : 0;
-    } else {
-      return i;
-    }
-  };
-
   // Training rows of a K-step are staged through an LDS ring (RX) with vector loads, so
   // generation reads them as LDS broadcasts: no scalar loads whose lgkmcnt(0) waits would
   // serialise with the A-fragment reads.
@@ -427,9 +281,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     double x = -(asq + row[DI]);
 #pragma unroll
     for (int j = 0; j < DI; ++j) x = fma(PLDS ? PA[m][j] : a2[j], row[j], x);
-    const double e = exp2_64(x, tab);                      // padding rows: exactly 0
-    if constexpr (SP) return x < prm.t_cut ? 0.0 : e;      // the cutoff: below tau, exactly 0
-    return e;
+    return exp2_64(x, tab);                                // padding rows: exactly 0
   };
   auto gen = [&](int rb, double (&v)[GV]) {
 #pragma unroll
@@ -490,44 +342,12 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     store_rows(rslot, rr);
     if (ks % SB == SB - 1) __syncthreads();
   };
-  // SP: loop position i runs the i-th active K-step kat(i); the LDS ring slots go by
-  // position, the row and B addresses by K-step, and skipped column tiles issue no MFMA
-  auto full_step_sp = [&](auto t0c, auto t1c, int i, double (&bb)[BR * NTW]) {
-    constexpr int T0 = decltype(t0c)::value, T1c = decltype(t1c)::value;
-    const int buf = i & (ASL - 1);
-    const int gslot = (i + LOOK) & (ASL - 1);
-    const int rslot = (i + RA) & (RXS - 1);
-    const int grb = (i + LOOK) & (RXS - 1);
-    const int kcur = kat(i), knext = kat(i + 1);
-    double v[GV];
-    double rr[RPT];
-    load_rows(kat(i + RA), rr);
-    gen(grb, v);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      double af[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) af[mt] = As[buf][kk * 4 + lk][mt * 16 + li];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int nt = T0; nt < T1c; ++nt) {
-          if (!((cmask >> nt) & 1u)) continue;                 // a skipped column tile (uniform)
-          acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bb[(kk % BR) * NTW + nt], acc[mt][nt], 0, 0, 0);
-        }
-      loadB_part((kk + BR) / 4 ? knext : kcur, (kk + BR) % 4, kk % BR, bb);   // sub-step kk + BR
-    }
-    store(gslot, v);
-    store_rows(rslot, rr);
-    if (i % SB == SB - 1) __syncthreads();
-  };
-
   double bb[BR * NTW];
   {
     double rr[RPT];
 #pragma unroll
     for (int j = 0; j < RA; ++j) {
-      load_rows(SP ? kat(j) : j, rr);
+      load_rows(j, rr);
       store_rows(j, rr);
     }
   }
@@ -540,7 +360,7 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       store(j, v);
     }
 #pragma unroll
-    for (int kk = 0; kk < BR; ++kk) loadB_part(SP ? kat(0) : 0, kk, kk, bb);
+    for (int kk = 0; kk < BR; ++kk) loadB_part(0, kk, kk, bb);
   }
   // Drain the prologue's loads (vmcnt(0)) so that the K loop's entry carries no pending
   // loads: otherwise the waitcnt pass merges the prologue's issue order into the loop
@@ -549,7 +369,6 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
   __syncthreads();
 
   int ks = 0;
-  if constexpr (!SP) {
   // K-steps [ks, kend[T0]) with tiles [T0, T1) active, for T0 = 0 .. T1-1
   // (groups of RG tiles: phase T0 = g0 RG runs until the group's last tile retires)
   static_for<1, NTW / RG + 1>([&](auto g1c) {
@@ -572,30 +391,6 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
     store((ks + LOOK) & (ASL - 1), v);
     store_rows((ks + RA) & (RXS - 1), rr);
     if (ks % SB == SB - 1) __syncthreads();
-  }
-  } else {
-    // the same phases over the active K-steps: position ks runs K-step kat(ks)
-    static_for<1, NTW / RG + 1>([&](auto g1c) {
-      constexpr int T1c = decltype(g1c)::value * RG;
-      if ((T1 + RG - 1) / RG * RG == T1c) {
-        static_for<0, T1c / RG>([&](auto g0c) {
-          constexpr int T0 = decltype(g0c)::value * RG;
-          int e = kend[T0];
-          if constexpr (RG == 2) e = max(e, kend[T0 + 1]);
-          for (; ks < n_act && kat(ks) < e; ++ks)
-            full_step_sp(std::integral_constant<int, T0>{}, std::integral_constant<int, T1c>{}, ks, bb);
-        });
-      }
-    });
-    for (; ks < n_act; ++ks) {
-      double v[GV];
-      double rr[RPT];
-      load_rows(kat(ks + RA), rr);
-      gen((ks + LOOK) & (RXS - 1), v);
-      store((ks + LOOK) & (ASL - 1), v);
-      store_rows((ks + RA) & (RXS - 1), rr);
-      if (ks % SB == SB - 1) __syncthreads();
-    }
   }
 
   if constexpr (DYN) {
@@ -725,51 +520,6 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
       // Sum of squares over the block's R columns.  Front-padding columns (col < 0) have
       // B = 0, so V = 0 there: no mask (mean columns were zeroed above).
       double qs[MT][4];
-      if constexpr (SP) {
-        // the cutoff image: q = sum_j V_j k_j, k_j regenerated as the K loop generated it
-        // (same records, same fma chain, same flush); skipped column tiles have V = 0
-  #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-  #pragma unroll
-          for (int r = 0; r < 4; ++r) qs[mt][r] = 0.0;
-  #pragma unroll
-        for (int nt = 0; nt < NTW; ++nt) {
-          if (!((cmask >> nt) & 1u)) continue;
-          int col = J * NB + 16 * (NW * nt + w) + li - coff;
-          col = col < 0 ? 0 : (col < n_rows ? col : n_rows - 1);   // (V = 0 outside the R columns)
-          double rec[RW];
-  #pragma unroll
-          for (int j = 0; j < RW; ++j) {
-            const v2u x = __builtin_amdgcn_raw_buffer_load_b64(rrsrc, (unsigned)(col * RW + j) * 8u, 0, 0);
-            rec[j] = __builtin_bit_cast(double, (unsigned long long)x.x | ((unsigned long long)x.y << 32));
-          }
-  #pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-  #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int pr = mt * 16 + lk + 4 * r;
-              double x = -(PK[pr][DI] + rec[DI]);
-  #pragma unroll
-              for (int j = 0; j < DI; ++j) x = fma(PK[pr][j], rec[j], x);
-              const double kv = x < prm.t_cut ? 0.0 : exp2_64(x, tab);
-              qs[mt][r] = fma(acc[mt][nt][r], kv, qs[mt][r]);
-              // one value at a time: interleaving the MT x 4 exp chains would hold their
-              // temporaries beside the 128 accumulator registers (spills from d = 11)
-              __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-  #pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-  #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            double v = qs[mt][r];
-            v += __shfl_xor(v, 1);
-            v += __shfl_xor(v, 2);
-            v += __shfl_xor(v, 4);
-            v += __shfl_xor(v, 8);
-            qs[mt][r] = v;
-          }
-      } else {
   #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
   #pragma unroll
@@ -783,7 +533,6 @@ __global__ __launch_bounds__(64 * NW, (DI <= 16 ? 2 : 1)) void k_gp_tile(const T
           v += __shfl_xor(v, 8);
           qs[mt][r] = v;
         }
-      }
       if (li == 0) {
   #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
@@ -989,18 +738,6 @@ void launch_d(const TileParams& p, bool dyn, hipStream_t stream) {
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4, 1, 4>), grid, dim3(256), 0, stream, p);
     else
       hipLaunchKernelGGL((k_gp_tile<DI, true, 0, 4>), grid, dim3(256), 0, stream, p);
-  } else if (p.sparse) {
-    // the observation GP's cutoff image (capi_model.hip gpmdm_model_set_obs_cutoff): the
-    // default observation shapes only
-    // (capi_model.hip gpmdm_model_set_obs_cutoff: 32 x 512 up to d = 8, 64 x 512 up to d = 16 --
-    // the cutoff's K-step bookkeeping pushes the 32 x 512 kernel into spills from d = 11,
-    // and the 64 x 512 one above d = 16)
-    if constexpr (DI <= 8) {
-      if (g.nw == 4) hipLaunchKernelGGL((k_gp_tile<DI, false, kTileSparse, 4, 2, 8>), grid, dim3(256), 0, stream, p);
-    }
-    if constexpr (DI <= 16) {
-      if (g.nw == 8) hipLaunchKernelGGL((k_gp_tile<DI, false, kTileSparse, 8>), grid, dim3(512), 0, stream, p);
-    }
   } else if (g.mt == 2) {
     hipLaunchKernelGGL((k_gp_tile<DI, false, kCoordVar, 4, 2, 8>), grid, dim3(256), 0, stream, p);
   } else if (g.mt == 1 && g.ntw == 8) {

@@ -59,13 +59,6 @@ struct ImagePacker {
   int n_rows, d, n_m, coff, n_j;
   TileGeo geo;
   const double *X, *ls, *lin_c2, *R, *M;
-  // Cutoff image of the observation GP (gpmdm_model_set_obs_cutoff): R is the full symmetric
-  // K^-1 (the reference's own U^-1 U^-T, gpmdm.py:1286-1290) and B holds its block upper
-  // triangle with the off-diagonal 16 x 16 blocks doubled -- k^T K^-1 k = sum_j k_j V_j with
-  // V_j = sum over rows i of blocks <= block(j) of k_i B_ij -- over the training rows in the
-  // order perm (image row -> training row; nullptr: identity).
-  bool sym = false;
-  const long long* perm = nullptr;
 
   ImagePacker(int n_rows_, int d_, int n_m_, const double* X_, const double* ls_, const double* lin_c2_,
               const double* R_, const double* M_, TileGeo geo_)
@@ -74,21 +67,12 @@ struct ImagePacker {
     n_j = (n_rows + n_m + coff + geo.nb() - 1) / geo.nb();
   }
 
-  long long src(long long row) const { return perm ? perm[row] : row; }
-
-  // B = [triu(R) | M] (row-major inputs R: n_rows x n_rows, M: n_rows x n_m); the cutoff
-  // image: [2 blocktriu(K^-1) + blockdiag(K^-1) | M] in the order perm
+  // B = [triu(R) | M] (row-major inputs R: n_rows x n_rows, M: n_rows x n_m)
   double val(long long row, long long col) const {
     if (row >= n_rows || col < 0) return 0.0;
-    if (col < n_rows) {
-      if (!sym) return row <= col ? R[row * n_rows + col] : 0.0;   // upper triangle of R
-      const long long bi = row / kBK, bj = col / kBK;
-      if (bi > bj) return 0.0;
-      const double a = R[src(row) * n_rows + src(col)];
-      return bi < bj ? 2.0 * a : a;
-    }
+    if (col < n_rows) return row <= col ? R[row * n_rows + col] : 0.0;   // upper triangle of R
     const long long j = col - n_rows;
-    return j < n_m ? M[src(row) * n_m + j] : 0.0;
+    return j < n_m ? M[row * n_m + j] : 0.0;
   }
 
   // Row records [Xs_i, |Xs_i|^2 * 64/ln2], Xs = X / ls: (d + 1) doubles per row, padded to
@@ -100,7 +84,7 @@ struct ImagePacker {
     for (long long i = 0; i < n_rows; ++i) {
       double s = 0.0;
       for (int j = 0; j < d; ++j) {
-        const double v = X[src(i) * d + j] / ls[j];
+        const double v = X[i * d + j] / ls[j];
         rec[i * rw + j] = v;
         s += v * v;
       }
@@ -233,6 +217,70 @@ inline void kstep_spheres(const double* X, const double* ls, const long long* pe
     out[(size_t)k * (d + 1) + d] = std::sqrt(rad) * (1.0 + 1e-12) + 1e-12;
   }
 }
+
+// The cutoff image (obs_cutoff.h), tile-major: column tile t = 0 .. T_R - 1 holds the 16
+// columns 16t .. 16t + 15 of the symmetric block form of K^-1 (upper block triangle, the
+// off-diagonal 16 x 16 blocks doubled, rows and columns in the order perm; columns past N are
+// zero), and needs K-steps 0 .. t (kend = t + 1); mean tile T_R + m holds columns 16m .. 16m + 15
+// of M = K^-1 Y and needs every K-step (kend = T_R).  Column tiles and K-steps index the same
+// 16-row groups, so the K-step sphere test also decides which R tiles a particle tile needs.
+// Tile t's K-step ks is 2 KiB at toff[t] + 256 ks doubles, lane l's four sub-step values
+// contiguous (two 16-byte loads):
+//   Bt[toff[t] + 256 ks + 4 l + kk] = B[row = 16 ks + 4 kk + (l >> 4)][col of tile t, l & 15].
+struct CutoffPacker {
+  int n_rows, d, n_m, T_R, T_M;
+  const double *X, *ls, *Kinv, *M;
+  const long long* perm;   // image row -> training row
+
+  CutoffPacker(int n_rows_, int d_, int n_m_, const double* X_, const double* ls_, const double* Kinv_,
+               const double* M_, const long long* perm_)
+      : n_rows(n_rows_), d(d_), n_m(n_m_), X(X_), ls(ls_), Kinv(Kinv_), M(M_), perm(perm_) {
+    T_R = ksteps(n_rows);
+    T_M = (n_m + 15) / 16;
+  }
+  int tiles() const { return T_R + T_M; }
+  long long kend(int t) const { return t < T_R ? t + 1 : T_R; }
+  std::vector<long long> offsets() const {
+    std::vector<long long> o((size_t)tiles() + 1, 0);
+    for (int t = 0; t < tiles(); ++t) o[(size_t)t + 1] = o[(size_t)t] + 256 * kend(t);
+    return o;
+  }
+  // B[row][column l of tile t]
+  double val(long long row, int t, int l) const {
+    if (row >= n_rows) return 0.0;
+    if (t < T_R) {
+      const long long col = 16LL * t + l;
+      if (col >= n_rows) return 0.0;
+      const long long bi = row / kBK, bj = col / kBK;
+      if (bi > bj) return 0.0;
+      const double a = Kinv[perm[row] * n_rows + perm[col]];
+      return bi < bj ? 2.0 * a : a;
+    }
+    const long long j = 16LL * (t - T_R) + l;
+    return j < n_m ? M[perm[row] * n_m + j] : 0.0;
+  }
+  // tile t into dst[0, 256 kend(t))
+  void pack_tile(int t, double* dst) const {
+    for (long long ks = 0; ks < kend(t); ++ks)
+      for (int l = 0; l < 64; ++l)
+        for (int kk = 0; kk < 4; ++kk) dst[(ks * 64 + l) * 4 + kk] = val(ks * kBK + 4 * kk + (l >> 4), t, l & 15);
+  }
+  // row records in image-row order (as ImagePacker::records)
+  void records(std::vector<double>& rec) const {
+    const int cap = row_cap(n_rows), rw = d + 1;
+    rec.assign((size_t)cap * rw, 0.0);
+    for (int i = n_rows; i < cap; ++i) rec[(size_t)i * rw + d] = kPadSq;
+    for (long long i = 0; i < n_rows; ++i) {
+      double s = 0.0;
+      for (int j = 0; j < d; ++j) {
+        const double v = X[perm[i] * d + j] / ls[j];
+        rec[(size_t)i * rw + j] = v;
+        s += v * v;
+      }
+      rec[(size_t)i * rw + d] = s * kLog2eX64;
+    }
+  }
+};
 
 // The cutoff tau: every kernel value below it is flushed to 0.  Bounds:
 //  * the quadratic form: flushing delta (0 <= delta_i <= tau) moves q = k^T K^-1 k by at most

@@ -186,7 +186,6 @@ struct NormArgs {
   double* blocksum;               // F x nb
   double* blockoff;               // F x nb
   double* total;                  // F: sum of e
-  double* cum;                    // normalised CDF, F x P
   // a deferred likelihood finish (k_obs_ll) of a single-shard filter: the small-filter
   // kernel computes ll itself first, the multi-kernel path launches k_obs_ll first
   ObsFinishArgs obs;
@@ -214,7 +213,10 @@ struct ResampleArgs {
   int nb, F, C, d, systematic, identity;
   unsigned frame, seed_lo, seed_hi;
   const double* U;                // uniforms (replay, single filter) or nullptr
-  const double* cum;
+  // the normalised CDF is not stored: the searches evaluate it from the normaliser's
+  // block-local scan and block offsets (cdf_view, pf_kernels.hip)
+  const double* local;            // F x P
+  const double* blockoff;         // F x nb
   const double* ll;
   const double* e;
   const double* total;
@@ -231,7 +233,7 @@ struct ResampleArgs {
   long long seq;
   int* cls_host;                  // post-resample classes into mapped host memory (k_small_resample,
                                   // single replay filters: the next switch's counts on the host), or nullptr
-  int* guide;                     // F x (GB + 3): guide[b] = first i with cum[i] >= b / GB
+  int* guide;                     // F x (GB + 3): guide[b] = first i with CDF_i >= b / GB
   long long GB;                   // guide buckets per filter
   // exchanged {class, state} rows read in place instead of cls_src / X_src (multi-rank
   // filters: row rows_inv[p] holds particle p, column 0 its class, 1..d its state), or nullptr

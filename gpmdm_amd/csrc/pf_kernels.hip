@@ -7,7 +7,7 @@
 //   k_obs_finish    variance + Gaussian log-likelihood      gpmdm.py:958-961, gpmdm_pf.py:188-192
 //   k_obs_ll        the same from the tile kernel's fused partial sums (filter path)
 //   k_norm_*        log_w = ll - max, w = exp / sum          gpmdm_pf.py:200-204
-//   k_cdf/k_resample  torch.multinomial(w, P, True) inverse CDF + gathers  gpmdm_pf.py:206-213
+//   k_guide/k_resample  torch.multinomial(w, P, True) inverse CDF + gathers  gpmdm_pf.py:206-213
 //                   and the read-out partial sums            gpmdm_pf.py:224-262, 302-312
 //   k_readout       read-out totals
 // All arithmetic is fp64; every reduction has a fixed order (bitwise run-to-run repeatable).
@@ -780,13 +780,23 @@ __global__ __launch_bounds__(1024) void k_norm_total(NormArgs a) {
   if (tid == 1023) a.total[f] = part[1023];
 }
 
-__global__ __launch_bounds__(kB) void k_cdf(NormArgs a) {
-  const long long f = blockIdx.y;
-  const long long p = (long long)blockIdx.x * kB + threadIdx.x;
-  if (p >= a.P) return;
-  const double S = a.total[f];
-  // torch: cumsum(w) / sum, last bucket forced to 1
-  a.cum[f * a.P + p] = p == a.P - 1 ? 1.0 : (a.blockoff[f * a.nb + blockIdx.x] + a.local[f * a.P + p]) / S;
+// The normalised CDF of filter f at particle i: k_norm_exp_scan's block-local inclusive scan
+// plus k_norm_total's block offset, over the total, the last bucket forced to 1 (torch:
+// cumsum(w) / sum, gpmdm_pf.py:206-213).  Evaluated where the inverse-CDF searches read it
+// (k_guide, k_sys_marks, k_resample) instead of stored by a CDF pass: the same expression on
+// the same operands, so every value -- and every index -- is the stored CDF's, one dependent
+// launch fewer per frame.
+struct CdfView {
+  const double* boff;
+  const double* local;
+  double S;
+  long long P;
+  __device__ __forceinline__ double operator[](long long i) const {
+    return i == P - 1 ? 1.0 : (boff[i / kB] + local[i]) / S;
+  }
+};
+__device__ __forceinline__ CdfView cdf_view(const ResampleArgs& a, long long f) {
+  return CdfView{a.blockoff + f * a.nb, a.local + f * a.P, a.total[f], a.P};
 }
 
 // One thread per output slot s: inverse-CDF search, gather, read-out partials.
@@ -809,7 +819,7 @@ __global__ __launch_bounds__(kB) void k_guide(ResampleArgs a) {
   const long long b0 = b - lane;                       // the wave's first query
   if (b0 >= nb) return;                                // (wave-uniform)
   const long long bl = b0 + 63 < nb - 1 ? b0 + 63 : nb - 1;   // its last query
-  const double* cum = a.cum + f * a.P;
+  const CdfView cum = cdf_view(a, f);
   // two 32-way searches in lock step: half h finds the first index with cum >= t(h ? bl : b0)
   const int h = lane >> 5, k = lane & 31;
   const unsigned long long hm = h ? 0xffffffff00000000ull : 0x00000000ffffffffull;
@@ -886,7 +896,7 @@ __global__ __launch_bounds__(kB) void k_sys_marks(ResampleArgs a) {
   const long long i = (long long)blockIdx.x * kB + threadIdx.x;
   if (i >= a.P) return;
   const double u0 = sys_u0(a, f);
-  const double* cum = a.cum + f * a.P;
+  const CdfView cum = cdf_view(a, f);
   const long long lo = i > 0 ? sys_count(cum[i - 1], u0, a.P) : 0;
   const long long hi = sys_count(cum[i], u0, a.P);
   if (hi > lo) a.sys_mark[f * a.P + lo] = (int)i;
@@ -971,7 +981,7 @@ __global__ __launch_bounds__(kB) void k_resample(ResampleArgs a) {
         const uint4 r = philox4x32_10(make_uint4((unsigned)s, a.frame, kStreamResample, 0u), key);
         u = u01_co(r.x, r.y);
       }
-      const double* cum = a.cum + g0;
+      const CdfView cum = cdf_view(a, f);
       // first index with cum >= u (torch's searchsorted), searched between two guide
       // entries that bracket it: t_lo = (q0 - 1) / GB <= u and t_hi = (q0 + 2) / GB > u for
       // q0 = floor(u GB) whatever its rounding, so the result is exactly that of a search
@@ -1152,8 +1162,9 @@ __global__ __launch_bounds__(1024) void k_readout(ResampleArgs a) {
 // filter runs normalise + CDF + resample + read-out in one launch instead of six -- at the
 // notebook's P = 100 each launch of the multi-kernel path costs more than its work.  The
 // arithmetic is the multi-kernel path's, association for association: the 256-thread
-// blocks of k_norm_exp_scan / k_cdf / k_resample are the workgroup's four 256-thread
-// quarters (block b = waves 4b .. 4b+3, so every wave-level scan / sum sees the same lanes),
+// blocks of k_norm_exp_scan / k_resample (and cdf_view's 256-particle blocks) are the
+// workgroup's four 256-thread quarters (block b = waves 4b .. 4b+3, so every wave-level scan /
+// sum sees the same lanes),
 // k_norm_total / k_readout run as they are, and intermediates go through the same buffers;
 // the max is exact in any order.  Systematic resampling takes the search form, whose indices
 // the scan form reproduces exactly (k_sys_marks).  Results are bitwise those of the
@@ -1255,12 +1266,8 @@ __global__ __launch_bounds__(1024) void k_small_resample(NormArgs na, ResampleAr
   const double S = Ssh;
   if (tid < nb) na.blockoff[f * nb + tid] = boff[tid];      // one 8-byte store per lane
   if (tid == 0) na.total[f] = S;
-  // ---- k_cdf ----
-  if (p < P) {
-    const double c = p == P - 1 ? 1.0 : (boff[b] + e_incl) / S;
-    na.cum[g0 + p] = c;
-    cum_s[p] = c;
-  }
+  // ---- the CDF (cdf_view's expression) ----
+  if (p < P) cum_s[p] = p == P - 1 ? 1.0 : (boff[b] + e_incl) / S;
   __syncthreads();
   // ---- k_resample (slot s = p) ----
   const uint2 key = filter_key(a.seed_lo, a.seed_hi, f);
@@ -1512,7 +1519,6 @@ void launch_normalise(const NormArgs& a, hipStream_t s) {
   if (!a.bmax) hipLaunchKernelGGL(k_norm_max, dim3(nbm, (unsigned)a.F), dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_norm_exp_scan, g, dim3(kB), 0, s, a);
   hipLaunchKernelGGL(k_norm_total, dim3((unsigned)a.F), dim3(1024), 0, s, a);
-  hipLaunchKernelGGL(k_cdf, g, dim3(kB), 0, s, a);
 }
 void launch_resample(const ResampleArgs& a, hipStream_t s) {
   if (!a.identity && a.sys_mark) {

@@ -152,25 +152,47 @@ static void check_cutoff(int n, int D, int d) {
     }
     EXPECT(std::sqrt(s) <= sph[k * (d + 1) + d], "row %lld outside its sphere", r);
   }
-  ImagePacker pk(n, d, D, X.data(), ls.data(), nullptr, S.data(), M.data(), kGeo32x512);
-  pk.sym = true;
-  pk.perm = perm.data();
-  for (long long i = 0; i < n; ++i)
-    for (long long j = 0; j < n + D; ++j) {
-      const double v = pk.val(i, j);
-      double want;
-      if (j >= n) want = M[perm[i] * D + (j - n)];
-      else if (i / kBK > j / kBK) want = 0.0;
-      else want = (i / kBK < j / kBK ? 2.0 : 1.0) * S[perm[i] * n + perm[j]];
-      EXPECT(v == want, "sym val(%lld, %lld) %.17g vs %.17g", i, j, v, want);
-    }
-  std::vector<double> img((size_t)pk.total_doubles());
-  long long off = 0;
-  for (int J = 0; J < pk.n_j; ++J) {
-    pk.pack_block(J, img.data() + off);
-    off += pk.block_doubles(J);
+  // the tile-major cutoff image: every tile's K-steps in place, every value where the
+  // kernel (obs_cutoff.h) reads it
+  CutoffPacker pk(n, d, D, X.data(), ls.data(), S.data(), M.data(), perm.data());
+  EXPECT(pk.T_R == (int)nks && pk.T_M == (D + 15) / 16, "tiles %d %d", pk.T_R, pk.T_M);
+  const std::vector<long long> off = pk.offsets();
+  std::vector<double> img((size_t)off.back(), -7.0);
+  for (int t = 0; t < pk.tiles(); ++t) {
+    EXPECT(off[(size_t)t + 1] - off[(size_t)t] == 256 * pk.kend(t), "tile %d size", t);
+    pk.pack_tile(t, img.data() + off[(size_t)t]);
   }
-  EXPECT(off == (long long)img.size(), "sym total");
+  for (double v : img) EXPECT(v != -7.0, "an image slot left unwritten%s", "");
+  for (int t = 0; t < pk.tiles(); ++t)
+    for (long long ks = 0; ks < pk.kend(t); ++ks)
+      for (int l = 0; l < 64; ++l)
+        for (int kk = 0; kk < 4; ++kk) {
+          const long long i = ks * kBK + 4 * kk + (l >> 4);
+          double want = 0.0;
+          if (i < n) {
+            if (t < pk.T_R) {
+              const long long j = 16LL * t + (l & 15);
+              if (j < n && i / kBK <= j / kBK) want = (i / kBK < j / kBK ? 2.0 : 1.0) * S[perm[i] * n + perm[j]];
+            } else {
+              const long long j = 16LL * (t - pk.T_R) + (l & 15);
+              if (j < D) want = M[perm[i] * D + j];
+            }
+          }
+          const double v = img[(size_t)(off[(size_t)t] + (ks * 64 + l) * 4 + kk)];
+          EXPECT(v == want, "tile %d ks %lld lane %d kk %d: %.17g vs %.17g", t, ks, l, kk, v, want);
+        }
+  // every value of the block upper triangle (and of M) is stored exactly once
+  long long nz = 0;
+  for (double v : img) nz += v != 0.0;
+  long long want_nz = 0;
+  for (long long i = 0; i < n; ++i) {
+    for (long long j = 0; j < n; ++j) want_nz += (i / kBK <= j / kBK) && S[perm[i] * n + perm[j]] != 0.0;
+    for (int j = 0; j < D; ++j) want_nz += M[perm[i] * D + j] != 0.0;
+  }
+  EXPECT(nz == want_nz, "non-zeros %lld vs %lld", nz, want_nz);
+  std::vector<double> rec;
+  pk.records(rec);
+  EXPECT((long long)rec.size() == (long long)row_cap(n) * (d + 1), "records %zu", rec.size());
   const double sigma2 = 0.01;
   const double tau = obs_cutoff_tau(n, sigma2, M.data(), D, ymax.data());
   const double vc_min = sigma2 / (n + sigma2);

@@ -12,7 +12,9 @@ built code objects and fails on any wider global / buffer / flat store.
 Compiler-generated spill stores (``scratch_store_*``) fall under the same rule: a
 default-shape kernel may not spill through stores wider than 8 bytes (only the opt-in 64x256
 shape, GPMDM_TILE_SHAPE=1, does at d >= 7), and the default shapes do not spill at all for
-d <= 12 (a spill in the K loop would also cost time)."""
+d <= 12 (a spill in the K loop would also cost time).  The cutoff kernel (k_obs_cutoff,
+obs_cutoff.h) keeps a few loop-invariant addresses in scratch at some d; none of its
+scratch accesses may sit between its first and last MFMA (the K loops)."""
 import re
 import shutil
 import struct
@@ -55,10 +57,15 @@ def _code_objects(tmp_path):
     return out
 
 
+SCRATCH = re.compile(r"\bscratch_(store|load)_")
+MFMA = re.compile(r"\bv_mfma_")
+
+
 def _stores_by_kernel(co):
     asm = subprocess.run([str(LLVM / "llvm-objdump"), "-d", str(co)], check=True, capture_output=True,
                          text=True).stdout
     wide, wspill, spill, fn = {}, {}, {}, None
+    seq = {}                               # per kernel: "m" (MFMA) / "s" (scratch access) in order
     for line in asm.splitlines():
         m = re.match(r"^[0-9a-f]+ <(.*)>:$", line)
         if m:
@@ -70,7 +77,12 @@ def _stores_by_kernel(co):
             wspill[fn] = wspill.get(fn, 0) + 1
         if SPILL_STORE.search(line):
             spill[fn] = spill.get(fn, 0) + 1
-    return wide, wspill, spill
+        if MFMA.search(line):
+            seq.setdefault(fn, []).append("m")
+        elif SCRATCH.search(line):
+            seq.setdefault(fn, []).append("s")
+    in_loop = {f for f, q in seq.items() if "m" in q and "s" in "".join(q).strip("s")}
+    return wide, wspill, spill, in_loop
 
 
 def _tile_args(kernel: str):
@@ -95,16 +107,19 @@ def _default_shape(kernel: str) -> bool:
 def test_no_wide_vgpr_stores_in_production_kernels(tmp_path):
     cos = _code_objects(tmp_path)
     assert cos, "no gfx950 code object found in libgpmdm_hip.so"
-    wide, wspill, spill = {}, {}, {}
+    wide, wspill, spill, in_loop = {}, {}, {}, set()
     for co in cos:
-        w, ws, s = _stores_by_kernel(co)
+        w, ws, s, il = _stores_by_kernel(co)
         wide.update(w)
         wspill.update(ws)
         spill.update(s)
+        in_loop |= il
     bad = {k: v for k, v in wide.items() if k not in ALLOW_WIDE}
     assert not bad, f"wide (>8-byte) stores in production kernels: {bad}"
     bad = {k: v for k, v in wspill.items() if _default_shape(k)}
     assert not bad, f"default-shape kernels spill through wide scratch stores: {bad}"
     bad = {k: v for k, v in spill.items() if _default_shape(k) and _tile_args(k) and _tile_args(k)[0] <= 12}
     assert not bad, f"default-shape kernels at d <= 12 spill: {bad}"
-    assert not {k for k in spill if not _tile_args(k)}, "a non-tile kernel spills"
+    cut = {k for k in spill if "k_obs_cutoff" in k}
+    assert not {k for k in spill if not _tile_args(k)} - cut, "a non-tile kernel spills"
+    assert not (cut & in_loop), f"the cutoff kernel spills inside its K loop: {cut & in_loop}"
