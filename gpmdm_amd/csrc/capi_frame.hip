@@ -393,18 +393,22 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     const bool cut = pf->obs_cutoff && m->has_cutoff();
     const GpImage& oi = *pf->obs_img;
     // Particle order of the tiles: positions [lo, hi) of the ownership order -- or, for a
-    // single-rank cutoff filter, the switch's class grouping (stable within a class in the
-    // ownership order, i.e. by resampling ancestor): a tile then holds particles propagated
-    // from one (ancestor, class) mean where it can, so its bounding sphere -- and the K-steps
-    // it reaches -- are small.  Any order gives the same values (the flush is per value).
-    const int* obs_order = (cut && pf->n_ranks == 1) ? pf->perm : pf->own_order();
+    // cutoff filter whose switch grouped exactly this rank's particles (one rank, or a
+    // multi-rank Philox filter: its slice at grouped positions [0, nloc)), the switch's class
+    // grouping (stable within a class in the ownership order, i.e. by resampling ancestor): a
+    // tile then holds particles propagated from one (ancestor, class) mean where it can, so
+    // its bounding sphere -- and the K-steps it reaches -- are small.  Any order gives the
+    // same values (the flush is per value).
+    const bool grouped = cut && (pf->n_ranks == 1 || pf->rng_mode == GPMDM_RNG_PHILOX);
+    const int* obs_order = grouped ? pf->perm : pf->own_order();
+    const long long obs_lo = grouped ? 0 : pf->lo;   // first position of this rank's particles
     if (cut) {
       const auto& ci = m->obs_cut;
       CutoffParams cp{};
       cp.X = pf->X_prop;
       cp.perm = obs_order;
-      cp.pos_begin = (int)pf->lo;
-      cp.pos_end = (int)pf->hi;
+      cp.pos_begin = (int)obs_lo;
+      cp.pos_end = (int)(obs_lo + nl);
       for (int j = 0; j < d; ++j) cp.ls[j] = m->y_ls[j];
       cp.Xrec = ci.Xrec;
       cp.Bt = ci.Bt;
@@ -463,7 +467,7 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     oa.il2 = m->y_il2_dev;
     oa.ll_const = (double)((float)(0.5 * D) * (float)1.8378770351409912);
     oa.ll = pf->ll;
-    oa.ll_offset = pf->lo;
+    oa.ll_offset = obs_lo;
     oa.own = obs_order;
     oa.health = pf->health;
     pf->ll_pending = false;
