@@ -224,9 +224,9 @@ inline void kstep_spheres(const double* X, const double* ls, const long long* pe
 // zero), and needs K-steps 0 .. t (kend = t + 1); mean tile T_R + m holds columns 16m .. 16m + 15
 // of M = K^-1 Y and needs every K-step (kend = T_R).  Column tiles and K-steps index the same
 // 16-row groups, so the K-step sphere test also decides which R tiles a particle tile needs.
-// Tile t's K-step ks is 2 KiB at toff[t] + 256 ks doubles, lane l's four sub-step values
-// contiguous (two 16-byte loads):
-//   Bt[toff[t] + 256 ks + 4 l + kk] = B[row = 16 ks + 4 kk + (l >> 4)][col of tile t, l & 15].
+// Tile t's K-step ks is 2 KiB at toff[t] + 256 ks doubles: two halves of 1 KiB (sub-steps 0-1
+// and 2-3), each one wave's 16-byte load with lane l at 16 l bytes:
+//   Bt[toff[t] + 256 ks + 128 h + 2 l + e] = B[row = 16 ks + 4 (2h + e) + (l >> 4)][col of tile t, l & 15].
 struct CutoffPacker {
   int n_rows, d, n_m, T_R, T_M;
   const double *X, *ls, *Kinv, *M;
@@ -263,7 +263,8 @@ struct CutoffPacker {
   void pack_tile(int t, double* dst) const {
     for (long long ks = 0; ks < kend(t); ++ks)
       for (int l = 0; l < 64; ++l)
-        for (int kk = 0; kk < 4; ++kk) dst[(ks * 64 + l) * 4 + kk] = val(ks * kBK + 4 * kk + (l >> 4), t, l & 15);
+        for (int kk = 0; kk < 4; ++kk)
+          dst[ks * 256 + (kk >> 1) * 128 + 2 * l + (kk & 1)] = val(ks * kBK + 4 * kk + (l >> 4), t, l & 15);
   }
   // row records in image-row order (as ImagePacker::records)
   void records(std::vector<double>& rec) const {

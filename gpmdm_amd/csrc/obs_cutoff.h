@@ -31,6 +31,26 @@
 
 namespace gpmdm {
 
+// Sum over the 16 lanes of a row (lanes 16 r .. 16 r + 15) by DPP moves (VALU; no LDS traffic):
+// quad swaps (xor 1, xor 2), then shifts by 4 and 8 within the row (lane l reads lane l + 4,
+// l + 8).  Lane 16 r -- the only lane whose result is used -- receives ((q0 + q1) + (q2 + q3))
+// over the row's quads, each quad ((v0 + v1) + (v2 + v3)): exactly the association of the
+// xor-1/2/4/8 butterfly at that lane.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (unsigned long long)lo | ((unsigned long long)hi << 32));
+}
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_f64<0xB1>(v);    // quad_perm [1, 0, 3, 2]
+  v += dpp_f64<0x4E>(v);    // quad_perm [2, 3, 0, 1]
+  v += dpp_f64<0x104>(v);   // row_shl 4
+  v += dpp_f64<0x108>(v);   // row_shl 8
+  return v;
+}
+
 template <int DI, int NW, int MT, int NTW>
 __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams prm) {
   static_assert(NTW <= 8, "a full K-step of B fragments per tile in registers");
@@ -209,6 +229,10 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
 #pragma unroll
     for (int j = 0; j < NTW; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
   __shared__ double qrun[PT], srun[PT];                       // running sums per particle
+  // per-position R-tile partials: the tile retiring at list position i writes slot i & 3; wave 0
+  // adds slots to qrun in position order after each barrier (a slot is rewritten two barriers
+  // after it was written, by which time wave 0 has added it)
+  __shared__ double ptq[4][PT];
   if (tid < PT) {
     qrun[tid] = 0.0;
     srun[tid] = 0.0;
@@ -235,17 +259,29 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
     }
     const int last = min(c0 + TPC, n_tiles) - 1;
     const int npos = last < n_act ? last + 1 : n_act;          // list positions of this chunk
-    // B fragments of list position i, sub-steps 2h, 2h + 1, for every tile
+    // B fragments of list position i, sub-steps 2h, 2h + 1, for every tile (one contiguous
+    // KiB per load instruction)
     auto loadB = [&](int i, int h, double (&bb)[4 * NTW]) {
       const unsigned kb = (unsigned)kat(i) * 2048u;
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
-        const v4u x = __builtin_amdgcn_raw_buffer_load_b128(brsrc, (unsigned)lane * 32u + 16u * h, (int)(tb[nt] + kb), 0);
+        const v4u x = __builtin_amdgcn_raw_buffer_load_b128(brsrc, (unsigned)lane * 16u, (int)(tb[nt] + kb + 1024u * h), 0);
         bb[(2 * h) * NTW + nt] = __builtin_bit_cast(double, (unsigned long long)x.x | ((unsigned long long)x.y << 32));
         bb[(2 * h + 1) * NTW + nt] = __builtin_bit_cast(double, (unsigned long long)x.z | ((unsigned long long)x.w << 32));
       }
     };
-    auto step = [&](auto t0c, auto t1c, int i, double (&bb)[4 * NTW]) {
+    // R tiles of this chunk retire at list positions [c0, rlim), one per position, in list
+    // order: their partials are added in that order, as the sum over tiles requires
+    const int rlim = min(c0 + TPC, n_act);
+    auto consume = [&](int i0, int i1) {                     // positions i0 .. i1 (wave 0)
+      if (tid < PT) {
+        double qa = qrun[tid];
+        for (int q = i0; q <= i1; ++q)
+          if (q >= c0 && q < rlim) qa += ptq[q & 3][tid];
+        qrun[tid] = qa;
+      }
+    };
+    auto step = [&](auto t0c, auto t1c, int i, bool retire, double (&bb)[4 * NTW]) {
       constexpr int T0 = decltype(t0c)::value, T1c = decltype(t1c)::value;
       const int buf = i & (ASL - 1);
       double v[GV];
@@ -264,9 +300,25 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
             acc[mt][nt] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[mt], bb[kk * NTW + nt], acc[mt][nt], 0, 0, 0);
         if (kk & 1) loadB(i + 1, kk >> 1, bb);               // the next position's sub-steps
       }
+      if (retire) {
+        // tile T0's diagonal position: this K-step's rows are the tile's columns, so the K*
+        // just multiplied are its k_j (the flushed values, as generated): the tile's partial
+        // sum_j V_j k_j per particle, reduced over its 16 columns (lanes li)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int pr = mt * 16 + lk + 4 * r;
+            const double v = row16_sum(acc[mt][T0][r] * As[buf][li][pr]);
+            if (li == 0) ptq[i & 3][pr] = v;
+          }
+      }
       store((i + LOOK) & (ASL - 1), v);
       store_rows((i + RA) & (RXS - 1), rr);
-      if (i % SB == SB - 1) __syncthreads();
+      if (i % SB == SB - 1) {
+        __syncthreads();
+        consume(i - 1, i);
+      }
     };
 
     double bb[4 * NTW];
@@ -299,7 +351,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
         static_for<0, T1c>([&](auto t0c) {
           constexpr int T0 = decltype(t0c)::value;
           const int e = kend(T0);
-          for (; i < npos && i < e; ++i) step(std::integral_constant<int, T0>{}, std::integral_constant<int, T1c>{}, i, bb);
+          const bool rt = c0 + NW * T0 + w < n_act;          // an R tile: retires at e - 1
+          for (; i < npos && i < e; ++i)
+            step(std::integral_constant<int, T0>{}, std::integral_constant<int, T1c>{}, i, rt && i == e - 1, bb);
         });
       }
     });
@@ -310,7 +364,10 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
       gen((i + LOOK) & (RXS - 1), v);
       store((i + LOOK) & (ASL - 1), v);
       store_rows((i + RA) & (RXS - 1), rr);
-      if (i % SB == SB - 1) __syncthreads();
+      if (i % SB == SB - 1) {
+        __syncthreads();
+        consume(i - 1, i);
+      }
     }
     if (prm.sp_stats && lane == 0) {
       unsigned run = 0;
@@ -319,45 +376,17 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
       atomicAdd(prm.sp_stats + 0, (unsigned long long)run * MT);
     }
 
-    // ---- per-tile sums into LDS (aliasing the K* ring), then in list order ----------------
     __syncthreads();                                         // every wave is done with As
+    if (npos % SB == 1) consume(npos - 1, npos - 1);          // the last position's partial
+    // ---- mean tiles: per-tile sums into LDS (aliasing the K* ring), then in list order ------
+    if (last >= n_act) {                                     // (uniform) the chunk holds mean tiles
 #pragma unroll
-    for (int nt = 0; nt < NTW; ++nt) {
-      const int i2 = c0 + NW * nt + w;
-      if (i2 >= n_tiles) continue;                           // (wave-uniform)
-      // each value reduced over the tile's 16 columns (lanes li) as soon as it is formed
-      auto put = [&](int mt, int r, double v) {
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        v += __shfl_xor(v, 4);
-        v += __shfl_xor(v, 8);
-        if (li == 0) ptile[(NW * nt + w) * PT + mt * 16 + lk + 4 * r] = v;
-      };
-      if (i2 < n_act) {
-        // R tile: sum over its 16 columns of V_j k_j, k_j regenerated as the K loop generated
-        // it (same record, same fma chain, same flush)
-        const int col = 16 * kat(i2) + li;                   // image row of column j
-        double rec[RW];
-#pragma unroll
-        for (int j = 0; j < RW; ++j) {
-          const v2u x = __builtin_amdgcn_raw_buffer_load_b64(rrsrc, (unsigned)(col * RW + j) * 8u, 0, 0);
-          rec[j] = __builtin_bit_cast(double, (unsigned long long)x.x | ((unsigned long long)x.y << 32));
-        }
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int pr = mt * 16 + lk + 4 * r;
-            double x = -(PK[pr][DI] + rec[DI]);
-#pragma unroll
-            for (int j = 0; j < DI; ++j) x = fma(PK[pr][j], rec[j], x);
-            const double kv = x < prm.t_cut ? 0.0 : exp2_64(x, tab);
-            put(mt, r, acc[mt][nt][r] * kv);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-      } else {
-        // mean tile: (z_j - mu_j)^2 lam2_j over its columns (gpmdm_pf.py:188-192 with
-        // var_j = vc / lam2_j factored out; k_obs_ll finishes the likelihood)
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int i2 = c0 + NW * nt + w;
+        if (i2 < n_act || i2 >= n_tiles) continue;           // (wave-uniform)
+        // (z_j - mu_j)^2 lam2_j over the tile's columns (gpmdm_pf.py:188-192 with var_j =
+        // vc / lam2_j factored out; k_obs_ll finishes the likelihood), reduced over its 16
+        // columns (lanes li)
         const int jm = 16 * (i2 - n_act) + li;
         const bool real = jm < prm.n_m;
         const double lam = real ? prm.lam2[jm] : 0.0;
@@ -367,25 +396,22 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
           for (int r = 0; r < 4; ++r) {
             const int pr = mt * 16 + lk + 4 * r;
             const double t = real ? prm.z[pfil[pr] * prm.n_m + jm] - acc[mt][nt][r] : 0.0;
-            put(mt, r, (t * t) * lam);
+            const double v = row16_sum((t * t) * lam);
+            if (li == 0) ptile[(NW * nt + w) * PT + pr] = v;
           }
+      }
+      __syncthreads();
+      if (tid < PT) {
+        const int ns = min(TPC, n_tiles - c0);
+        double sa = srun[tid];
+        for (int s = n_act - c0 > 0 ? n_act - c0 : 0; s < ns; ++s) sa += ptile[s * PT + tid];
+        srun[tid] = sa;
       }
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) acc[mt][nt] = (d4){0.0, 0.0, 0.0, 0.0};
-    __syncthreads();
-    if (tid < PT) {
-      const int ns = min(TPC, n_tiles - c0);
-      double qa = qrun[tid], sa = srun[tid];
-      for (int s = 0; s < ns; ++s) {
-        const double v = ptile[s * PT + tid];
-        if (c0 + s < n_act) qa += v; else sa += v;
-      }
-      qrun[tid] = qa;
-      srun[tid] = sa;
-    }
     __syncthreads();                                         // before the next chunk's ring
   }
 

@@ -178,7 +178,7 @@ static void check_cutoff(int n, int D, int d) {
               if (j < D) want = M[perm[i] * D + j];
             }
           }
-          const double v = img[(size_t)(off[(size_t)t] + (ks * 64 + l) * 4 + kk)];
+          const double v = img[(size_t)(off[(size_t)t] + ks * 256 + (kk >> 1) * 128 + 2 * l + (kk & 1))];
           EXPECT(v == want, "tile %d ks %lld lane %d kk %d: %.17g vs %.17g", t, ks, l, kk, v, want);
         }
   // every value of the block upper triangle (and of M) is stored exactly once
