@@ -259,10 +259,25 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
     }
     const int last = min(c0 + TPC, n_tiles) - 1;
     const int npos = last < n_act ? last + 1 : n_act;          // list positions of this chunk
+    // The K-steps of list positions [kb0, kb0 + 128) in two VGPR windows (lane j of kw0 / kw1:
+    // position kb0 + j / kb0 + 64 + j): in the K loop a K-step is one v_readlane, not an LDS
+    // round trip in front of the B loads and the row staging
+    int kb0 = 0, kw0 = 0, kw1 = 0;
+    auto kwin = [&](int base) {
+      kb0 = base;
+      const int x0 = min(base + lane, n_act - 1), x1 = min(base + 64 + lane, n_act - 1);
+      kw0 = x0 >= 0 ? (int)klist[x0] : 0;
+      kw1 = x1 >= 0 ? (int)klist[x1] : 0;
+    };
+    auto katw = [&](int x) -> int {                          // kb0 <= x < kb0 + 128
+      const int o = x - kb0;
+      return o < 64 ? __builtin_amdgcn_readlane(kw0, o) : __builtin_amdgcn_readlane(kw1, o - 64);
+    };
+    kwin(0);
     // B fragments of list position i, sub-steps 2h, 2h + 1, for every tile (one contiguous
     // KiB per load instruction)
     auto loadB = [&](int i, int h, double (&bb)[4 * NTW]) {
-      const unsigned kb = (unsigned)kat(i) * 2048u;
+      const unsigned kb = (unsigned)katw(i) * 2048u;
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
         const v4u x = __builtin_amdgcn_raw_buffer_load_b128(brsrc, (unsigned)lane * 16u, (int)(tb[nt] + kb + 1024u * h), 0);
@@ -284,9 +299,10 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
     auto step = [&](auto t0c, auto t1c, int i, bool retire, double (&bb)[4 * NTW]) {
       constexpr int T0 = decltype(t0c)::value, T1c = decltype(t1c)::value;
       const int buf = i & (ASL - 1);
+      if (i + RA >= kb0 + 128) kwin(i);                      // (uniform; every 124 positions)
       double v[GV];
       double rr[RPT];
-      load_rows(kat(i + RA), rr);
+      load_rows(katw(i + RA), rr);
       gen((i + LOOK) & (RXS - 1), v);
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
@@ -326,7 +342,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
       double rr[RPT];
 #pragma unroll
       for (int j = 0; j < RA; ++j) {
-        load_rows(kat(j), rr);
+        load_rows(katw(j), rr);
         store_rows(j, rr);
       }
     }
@@ -358,9 +374,10 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
       }
     });
     for (; i < npos; ++i) {                                  // other waves' tiles: generate only
+      if (i + RA >= kb0 + 128) kwin(i);
       double v[GV];
       double rr[RPT];
-      load_rows(kat(i + RA), rr);
+      load_rows(katw(i + RA), rr);
       gen((i + LOOK) & (RXS - 1), v);
       store((i + LOOK) & (ASL - 1), v);
       store_rows((i + RA) & (RXS - 1), rr);
