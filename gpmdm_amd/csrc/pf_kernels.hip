@@ -285,18 +285,87 @@ __device__ __forceinline__ void lead_tables_body(const LeadArgs& a) {
 }
 __global__ __launch_bounds__(1024) void k_lead_tables(LeadArgs a) { lead_tables_body(a); }
 
-__global__ __launch_bounds__(kB) void k_lead_compact(LeadArgs a) {
-  const long long pos = (long long)blockIdx.x * kB + threadIdx.x;
+__device__ __forceinline__ void lead_compact_row(const LeadArgs& a, long long pos, int first) {
   if (pos >= a.npos) return;
   const int v = a.lflag_scan[pos];
   if (!(v & 1)) return;
   const long long p = a.perm[pos];
-  const int r = a.lblock[blockIdx.x] + (v >> 1);
+  const int r = first + (v >> 1);
   const long long f = p / a.Pf;
   a.lperm[r] = (int)p;
   const long long key = (long long)a.cls_new[p] * a.P + f * a.Pf + a.anc[p];
   a.slot[key] = r;
   if (a.owner_reset) a.owner_reset[key] = 0xffffffffu;   // the next election's preset
+}
+__global__ __launch_bounds__(kB) void k_lead_compact(LeadArgs a) {
+  lead_compact_row(a, (long long)blockIdx.x * kB + threadIdx.x, a.lblock[blockIdx.x]);
+}
+
+// k_lead_tables + k_lead_compact in one launch (nb <= kMaxLeadBlocks): block b's first leader
+// row is the sum of the leader counts of blocks 0 .. b-1, which the block adds up itself
+// (integers: any order gives k_lead_tables's prefix); block 0 also scans every block's count
+// and writes the leader segment tables with k_lead_tables's row rule.  Same rows, same tables.
+constexpr int kMaxLeadBlocks = 8192;
+__global__ __launch_bounds__(kB) void k_lead_tables_compact(LeadArgs a) {
+  __shared__ int red[kB / 64];
+  __shared__ int pre[kMaxLeadBlocks];          // block 0: exclusive prefix of every block's count
+  __shared__ int total_s;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x, nb = a.nb;
+  int s = 0;
+  for (int bb = tid; bb < b; bb += kB) s += a.lblock[bb];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  int first = 0;
+#pragma unroll
+  for (int v = 0; v < kB / 64; ++v) first += red[v];
+  if (b == 0) {
+    // exclusive scan of the counts: per thread a chunk of consecutive blocks, then a
+    // 256-wide scan of the chunk sums (wave shuffles + the four wave totals)
+    const int chunk = (nb + kB - 1) / kB;
+    int cs = 0;
+    for (int i = 0; i < chunk; ++i) {
+      const int bb = tid * chunk + i;
+      if (bb < nb) cs += a.lblock[bb];
+    }
+    int incl = cs;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(incl, off);
+      if (lane >= off) incl += y;
+    }
+    __syncthreads();                           // (red is reused)
+    if (lane == 63) red[w] = incl;
+    __syncthreads();
+    int run = incl - cs;
+    for (int v = 0; v < w; ++v) run += red[v];
+    for (int i = 0; i < chunk; ++i) {
+      const int bb = tid * chunk + i;
+      if (bb < nb) {
+        pre[bb] = run;
+        run += a.lblock[bb];
+      }
+    }
+    if (tid == kB - 1) total_s = run;
+    __syncthreads();
+    if (tid == 0) {
+      const int total = total_s;
+      auto row = [&](long long x) { return x >= a.npos ? total : pre[x / kB] + (a.lflag_scan[x] >> 1); };
+      int ts = 0;
+      for (int c = 0; c < a.C; ++c) {
+        const int b0 = row(a.seg_pos_begin[c]), e0 = row(a.seg_pos_end[c]);
+        a.lseg_pos_begin[c] = b0;
+        a.lseg_pos_end[c] = e0;
+        a.lseg_out_base[c] = b0;
+        a.lseg_tile_start[c] = ts;
+        ts += (e0 - b0 + a.pt - 1) / a.pt;
+      }
+      a.lseg_tile_start[a.C] = ts;
+    }
+  }
+  lead_compact_row(a, (long long)b * kB + tid, first);
 }
 
 
@@ -1500,8 +1569,12 @@ bool launch_switch_group(const SwitchArgs& sa, const ScanArgs& sc, const GroupAr
 }
 void launch_lead(const LeadArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_lead_flags, dim3((unsigned)a.nb), dim3(kB), 0, s, a);
-  hipLaunchKernelGGL(k_lead_tables, dim3(1), dim3(1024), 0, s, a);
-  hipLaunchKernelGGL(k_lead_compact, dim3((unsigned)a.nb), dim3(kB), 0, s, a);
+  if (a.nb <= kMaxLeadBlocks) {
+    hipLaunchKernelGGL(k_lead_tables_compact, dim3((unsigned)a.nb), dim3(kB), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(k_lead_tables, dim3(1), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_lead_compact, dim3((unsigned)a.nb), dim3(kB), 0, s, a);
+  }
 }
 void launch_dyn_finish(const DynFinishArgs& a, hipStream_t s) {
   if (a.n_out > 0) hipLaunchKernelGGL(k_dyn_finish, dim3(nblk(a.n_out, kB)), dim3(kB), 0, s, a);
