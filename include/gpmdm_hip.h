@@ -369,7 +369,8 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t model);
  * after gpmdm_pf_set_obs_cutoff(pf, 1) (2: also count the MFMA groups run against the dense
  * kernel's, read and optionally reset by gpmdm_pf_obs_cutoff_stats; 0: the dense kernel).
  * Results are the dense filter's to rounding (not bit for bit), and do not depend on the
- * tiling or the shard count. */
+ * tiling or the shard count.  Limits: d <= 16 and an image below 4 GiB (about 32k training
+ * rows); GPMDM_E_INVALID otherwise. */
 int gpmdm_model_set_obs_cutoff(gpmdm_model_t model, const double* K_inv, const double* beta, double sigma2,
                                const double* y_absmax);
 int gpmdm_model_obs_cutoff(gpmdm_model_t model, double* tau);
