@@ -1013,7 +1013,7 @@ def main():
     if args.cutoff_steps is None:
         args.cutoff_steps = 20 if (args.config in (2, 3, 5) and rng == "philox" and args.stream == "mocap") else 0
     cut = None
-    if args.cutoff_steps and world == 1 and args.stream == "mocap":
+    if args.cutoff_steps and world == 1 and len(zs) >= args.warmup + args.cutoff_steps + 10:
         try:   # reported beside the headline, never in place of it
             cut = cutoff_line(model, T, P_total, zs, args.warmup, args.cutoff_steps, elapsed / args.steps * 1e3,
                               obs_launch_s * 1e3)
