@@ -20,8 +20,11 @@
 //    last is full whatever the cloud, so the MFMAs per generated K-step stay those of the
 //    dense kernel however few tiles are active;
 //  * q = sum_j k_j V_j, V = K* B over the symmetric image, and S = sum_j (z_j - mu_j)^2 lam2_j
-//    (mu = the mean tiles' V) are summed per column tile (its 16 columns by lane xor 1, 2, 4,
-//    8) and then over the tiles in list order, by one thread per particle.
+//    (mu = the mean tiles' V) are summed per column tile (its 16 columns by a DPP row
+//    reduction) and then over the tiles in list order, by one thread per particle.  An R
+//    tile's last list position is its own diagonal K-step, whose K* in the LDS ring are the
+//    tile's k_j: its partial is formed there, with no regeneration; mean tiles after the
+//    chunk's K loop.
 // Invariance: a K-step or R tile dropped for one tile composition contributes exact zeros to
 // every particle of another composition that includes it (its values are flushed for that
 // particle), and the sums run in increasing tile order, so a particle's q and S do not
