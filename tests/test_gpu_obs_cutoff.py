@@ -212,3 +212,35 @@ def test_cutoff_skips_work_on_the_benchmark_cloud(m2c):
     pf.update(zs[6])
     st = pf.obs_cutoff_stats()
     assert st["dense"] > 0 and 0 < st["run"] < st["dense"], st
+
+
+def test_cutoff_far_cloud_has_no_reachable_kstep(m2c):
+    """A cloud far from every training latent: every K-step is out of reach (the kernel runs
+    the mean tiles only, with V = 0), and the likelihoods equal the dense kernel's, whose
+    kernel values underflow to 0 there, to the rounding of the S sum's association."""
+    from gpmdm_amd import GPMDM_PF
+    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
+    P = 1000
+    X = m2c.X.detach().cpu().numpy()
+    rng = np.random.RandomState(7)
+    far = X.max(0) + 50.0 * np.exp(m2c.y_log_lengthscales.detach().cpu().numpy()) + rng.rand(P, X.shape[1])
+    cls = rng.randint(0, 2, size=P)
+    Y = m2c.get_Y()
+    E, nrm, u = rng.exponential(size=(P, 2)), np.zeros((P, X.shape[1])), rng.rand(P)
+    out = {}
+    for cut in (False, True):
+        pf = GPMDM_PF(m2c, T, P, rng="torch", obs_cutoff=cut)
+        pf.load_state(far, cls)
+        if cut:
+            pf.set_obs_cutoff(True, stats=True)
+            pf.obs_cutoff_stats(reset=True)
+        pf.update_with_draws(Y[5], E, nrm, u)
+        out[cut] = pf.export_state()
+        if cut:
+            st = pf.obs_cutoff_stats()
+    a, b = out[False], out[True]
+    assert np.array_equal(a["classes"], b["classes"])
+    # the propagated cloud (the dynamics GP's linear kernel extrapolates the far states) stays
+    # out of reach: only the mean tiles ran
+    assert st["dense"] > 0 and st["run"] < 0.05 * st["dense"], st
+    assert np.max(np.abs(a["ll"] - b["ll"]) / np.maximum(np.abs(a["ll"]), 1.0)) < 1e-12
