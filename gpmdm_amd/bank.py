@@ -33,7 +33,7 @@ from .model import GPMDM
 class GPMDM_PF_Bank:
     def __init__(self, gpmdm: GPMDM, markov_switching_model, num_filters: int, num_particles: int, *,
                  seed=None, resample: str = "multinomial", process_group=None, shard=None,
-                 dedup: bool = True, dyn_tiles: str = "auto"):
+                 dedup: bool = True, dyn_tiles: str = "auto", obs_cutoff: bool = False):
         self._gpmdm = gpmdm
         self._gpmdm.set_evaluation_mode()
         self._T = torch.as_tensor(markov_switching_model).type(torch.float64)
@@ -65,6 +65,8 @@ class GPMDM_PF_Bank:
         self._f_lo, self._f_hi = shard_range(self._num_filters, world, rank)
         self._h = None
         self._readout = None
+        if obs_cutoff:
+            gpmdm.enable_obs_cutoff(True)     # the model's cutoff image (built once)
         if self.local_filters > 0:
             T = np.ascontiguousarray(self._T.numpy(), dtype=np.float64)
             h = ctypes.c_void_p()
@@ -79,6 +81,8 @@ class GPMDM_PF_Bank:
             if dyn_tiles not in _lib.DYN_TILES:
                 raise ValueError("dyn_tiles must be 'auto', 'narrow' or 'wide'")
             _lib.check(_lib.load().gpmdm_pf_set_dyn_tiles(h, _lib.DYN_TILES[dyn_tiles]), "dyn_tiles")
+            if obs_cutoff:                    # the observation GP's kernel-value cutoff (GPMDM_PF's)
+                _lib.check(_lib.load().gpmdm_pf_set_obs_cutoff(h, 1), "obs_cutoff")
             self._init_particles()
 
     def __del__(self):

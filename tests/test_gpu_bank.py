@@ -80,3 +80,30 @@ def test_bank_rejects_bad_shapes(m1, fx_config1):
         bank.update(np.zeros((3, m1.D)))
     with pytest.raises(ValueError):
         GPMDM_PF_Bank(m1, torch.eye(3), 4, 50)
+
+
+def test_bank_with_cutoff_equals_independent_cutoff_filters(m1, fx_config1):
+    """The observation GP's kernel-value cutoff in a bank (GPMDM_PF_Bank(obs_cutoff=True):
+    the cutoff kernel's tiles then mix filters, each particle reading its own filter's
+    observation) is bitwise F single cutoff filters: a particle's cutoff results do not depend
+    on its tile-mates (DESIGN.md §3 "Kernel-value cutoff")."""
+    from gpmdm_amd import GPMDM_PF, GPMDM_PF_Bank
+    T = torch.tensor(fx_config1["T"])
+    F, P = 3, 1000
+    bank = GPMDM_PF_Bank(m1, T, F, P, seed=700, obs_cutoff=True)
+    st0 = bank.export_state()
+    singles = []
+    for i in range(F):
+        pf = GPMDM_PF(m1, T, P, rng="philox", seed=700 + i, obs_cutoff=True)
+        pf.load_state(st0["states"][i], st0["classes"][i])
+        singles.append(pf)
+    for Z in _obs(fx_config1, F, 3):
+        bank.update(Z)
+        for i, pf in enumerate(singles):
+            pf.update(Z[i])
+        b = bank.export_state()
+        for i, pf in enumerate(singles):
+            s = pf.export_state()
+            for key in ("states", "classes", "ll", "w", "resample_idx"):
+                assert np.array_equal(b[key][i], s[key]), (i, key)
+    m1.enable_obs_cutoff(False)
