@@ -363,6 +363,16 @@ int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s, bool 
 
 // _update_weights' likelihoods for this rank's particles (gpmdm_pf.py:170-192): uploads z,
 // runs the observation GP tile and the likelihood finish.
+// Particle tiles of the cutoff launch that run as two workgroups each
+// (gpmdm_pf_set_obs_cutoff_split): by default the tiles past the last full round of resident
+// slots (all of them below one round).
+static int cut_split_tiles(const gpmdm_pf* pf, int tiles, int slots) {
+  if (pf->cut_split_policy == GPMDM_CUT_SPLIT_NONE) return 0;
+  if (pf->cut_split_policy == GPMDM_CUT_SPLIT_ALL) return tiles;
+  if (slots <= 0 || tiles <= slots) return tiles;
+  return tiles % slots;
+}
+
 int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
   gpmdm_model* m = pf->m;
   const int d = m->d, D = m->D;
@@ -402,6 +412,8 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     const bool grouped = cut && (pf->n_ranks == 1 || pf->rng_mode == GPMDM_RNG_PHILOX);
     const int* obs_order = grouped ? pf->perm : pf->own_order();
     const long long obs_lo = grouped ? 0 : pf->lo;   // first position of this rank's particles
+    bool cut_tail = false;
+    long long cut_o0 = 0, cut_ld = 0;
     if (cut) {
       const auto& ci = m->obs_cut;
       CutoffParams cp{};
@@ -426,7 +438,26 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
       cp.lam2 = m->y_lam2_dev;
       cp.Pf = pf->Pf;
       cp.sp_stats = pf->sp_stats_on ? pf->sp_stats : nullptr;
-      launch_obs_cutoff(cp, d, s);
+      // the grid's tail: equal workgroups run in whole rounds of the resident slots, so the
+      // tiles past the last full round are split in two workgroups each (chunks [0, c*) and
+      // [c*, nc); bitwise the whole tile's sums, k_obs_ll chains the second part on).  Below
+      // one round every tile is split.
+      const int PT = cutoff_tile_particles(d), TPC = cutoff_tile_list_chunk();
+      const int tiles = (int)cdiv(nl, PT);
+      const int slots = cutoff_slots(d);
+      int n_split = cut_split_tiles(pf, tiles, slots);
+      const long long entries = (long long)ci.T_R + ci.T_M - TPC;   // list entries a second part can hold
+      if (entries <= 0) n_split = 0;
+      if (n_split > 0) TRY(pf->ensure_cut_split((size_t)entries * n_split * PT, n_split));
+      cp.n_whole = tiles - n_split;
+      cp.n_split = n_split;
+      cp.part = pf->cut_part;
+      cp.ld_part = (long long)n_split * PT;
+      cp.split = pf->cut_split;
+      if (!launch_obs_cutoff(cp, d, s)) return fail(GPMDM_E_INVALID, "cutoff launch shape");
+      cut_tail = n_split > 0;
+      cut_o0 = (long long)cp.n_whole * PT;
+      cut_ld = cp.ld_part;
     } else {
       TileParams tp{};
       const int* tab = pf->obs_tab;
@@ -469,6 +500,15 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     oa.ll = pf->ll;
     oa.ll_offset = obs_lo;
     oa.own = obs_order;
+    if (cut_tail) {
+      oa.cut_part = pf->cut_part;
+      oa.cut_ld = cut_ld;
+      oa.cut_split = pf->cut_split;
+      oa.cut_o0 = cut_o0;
+      oa.cut_pt = cutoff_tile_particles(d);
+      oa.cut_tpc = cutoff_tile_list_chunk();
+      oa.cut_tm = m->obs_cut.T_M;
+    }
     oa.health = pf->health;
     pf->ll_pending = false;
     pf->bmax_ready = false;

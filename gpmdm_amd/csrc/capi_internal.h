@@ -209,6 +209,28 @@ struct gpmdm_pf {
   bool obs_cutoff = false;
   unsigned long long* sp_stats = nullptr;
   bool sp_stats_on = false;
+  // the cutoff kernel's split tiles (capi_frame.hip): second parts' partials, (n_act, c*) per
+  // split tile; grown on demand
+  int cut_split_policy = GPMDM_CUT_SPLIT_TAIL;
+  double* cut_part = nullptr;
+  size_t cut_part_cap = 0;
+  int2* cut_split = nullptr;
+  int cut_split_cap = 0;
+  int ensure_cut_split(size_t n_part, int n_split) {
+    if (n_part > cut_part_cap) {
+      dfree(cut_part);
+      cut_part_cap = 0;
+      if (dalloc(&cut_part, n_part)) return fail(GPMDM_E_NOMEM, "cutoff split partials");
+      cut_part_cap = n_part;
+    }
+    if (n_split > cut_split_cap) {
+      dfree(cut_split);
+      cut_split_cap = 0;
+      if (dalloc(&cut_split, (size_t)n_split)) return fail(GPMDM_E_NOMEM, "cutoff split table");
+      cut_split_cap = n_split;
+    }
+    return GPMDM_OK;
+  }
   // likelihood finish deferred into the resampling launch (single-shard small filters:
   // k_small_resample computes ll first, one launch less per frame); flush_ll runs it for
   // any reader of ll that comes first
@@ -516,6 +538,8 @@ struct gpmdm_pf {
     dfree(own_tmp);
     dfree(gmax);
     dfree(sp_stats);
+    dfree(cut_part);
+    dfree(cut_split);
     dfree(bmax);
     dfree(bmax_rows);
     dfree(owner);

@@ -616,6 +616,15 @@ int gpmdm_pf_set_obs_cutoff(gpmdm_pf_t pf, int mode) {
   return GPMDM_OK;
 }
 
+int gpmdm_pf_set_obs_cutoff_split(gpmdm_pf_t pf, int policy) {
+  CHECK(pf, "null handle");
+  CHECK(policy == GPMDM_CUT_SPLIT_TAIL || policy == GPMDM_CUT_SPLIT_NONE || policy == GPMDM_CUT_SPLIT_ALL,
+        "policy: GPMDM_CUT_SPLIT_TAIL, _NONE or _ALL");
+  if (pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "set_obs_cutoff_split between propagate and resample");
+  pf->cut_split_policy = policy;
+  return GPMDM_OK;
+}
+
 int gpmdm_pf_obs_cutoff_stats(gpmdm_pf_t pf, int64_t* run, int64_t* dense, int reset, void* stream) {
   CHECK(pf && run && dense, "null argument");
   *run = *dense = 0;

@@ -67,8 +67,46 @@ struct CutoffParams {
   const double* lam2;        // n_m
   long long Pf;              // particles per filter
   unsigned long long* sp_stats;   // MFMA groups run / the dense kernel's, or nullptr
+  // split tiles (the grid's tail): particle tiles [n_whole, n_whole + n_split) run as two
+  // workgroups each, chunks [0, c*) (q, S as a whole tile's, so far) and [c*, nc) (each list
+  // entry's partial into part[(i - tpc) * ld_part + o - n_whole * PT], k_obs_ll chains them on)
+  int n_whole, n_split;
+  double* part;
+  long long ld_part;
+  int2* split;               // per split tile: (n_act, c*), written by its first workgroup
 };
-void launch_obs_cutoff(const CutoffParams& p, int d, hipStream_t stream);
+bool launch_obs_cutoff(const CutoffParams& p, int d, hipStream_t stream);   // false: bad shape
+int cutoff_tile_particles(int d);   // PT of the cutoff kernel at d
+int cutoff_tile_list_chunk();       // tpc: list entries per chunk
+int cutoff_slots(int d);            // workgroups resident at once on the device (cached per d)
+
+// K-loop positions chunk c of a tile list runs (obs_cutoff.h): up to its last R tile's
+// diagonal, every active K-step once it holds a mean tile
+__host__ __device__ inline int cutoff_chunk_positions(int c, int n_act, int T_M, int tpc) {
+  const int nt = n_act + T_M;
+  const int last = (c + 1) * tpc < nt ? (c + 1) * tpc - 1 : nt - 1;
+  return last < n_act ? last + 1 : n_act;
+}
+// The split chunk c* of a split tile: the first chunk of its second workgroup, balancing the
+// two workgroups' positions (plus a chunk's pipeline fill); nc (no second part) below two chunks
+__host__ __device__ inline int cutoff_split_chunk(int n_act, int T_M, int tpc) {
+  const int nc = (n_act + T_M + tpc - 1) / tpc;
+  if (nc < 2) return nc;
+  constexpr int kFill = 4;
+  long long tot = 0;
+  for (int c = 0; c < nc; ++c) tot += cutoff_chunk_positions(c, n_act, T_M, tpc) + kFill;
+  long long pre = 0, best_v = tot;
+  int best = 1;
+  for (int c = 1; c < nc; ++c) {
+    pre += cutoff_chunk_positions(c - 1, n_act, T_M, tpc) + kFill;
+    const long long v = pre > tot - pre ? pre : tot - pre;
+    if (v < best_v) {
+      best_v = v;
+      best = c;
+    }
+  }
+  return best;
+}
 
 // ---------------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11), counter = (index, frame, stream, sub).

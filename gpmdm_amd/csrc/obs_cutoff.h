@@ -93,7 +93,15 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
   constexpr double kScale = kLog2eX64;
   for (int i = tid; i < 64; i += NT) tab[i] = kExp2Tab[i];
 
-  const int pos0 = prm.pos_begin + (int)blockIdx.x * PT;
+  // the workgroup's particle tile and part: whole tiles first, then the split tiles' second
+  // parts (the longer ones in the balanced split's usual case), then their first parts
+  int tile = (int)blockIdx.x, part = -1;                      // -1: the whole tile
+  if (tile >= prm.n_whole) {
+    const int r = tile - prm.n_whole;
+    part = r < prm.n_split ? 1 : 0;
+    tile = prm.n_whole + (r < prm.n_split ? r : r - prm.n_split);
+  }
+  const int pos0 = prm.pos_begin + tile * PT;
   const int pos_end = prm.pos_end;
   const int T_R = prm.T_R;
 
@@ -181,6 +189,22 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
   }
   __syncthreads();                                           // klist complete
   const int n_tiles = n_act + prm.T_M;
+  // the chunks [c_lo, c_hi) of the tile list this workgroup runs (none: a second part of a
+  // tile below two chunks; no early exit, which costs the K loop registers)
+  int c_lo = 0, c_hi = (n_tiles + TPC - 1) / TPC;
+  if (part >= 0) {
+    const int cs = __builtin_amdgcn_readfirstlane(cutoff_split_chunk(n_act, prm.T_M, TPC));
+    if (part == 0) {
+      c_hi = cs;
+      if (tid == 0) prm.split[tile - prm.n_whole] = make_int2(n_act, cs);
+    } else {
+      c_lo = cs;
+    }
+  }
+  // (the second part's partials: list entry i of particle m at part[(i - TPC) ld + o])
+  // (uniform, so it stays out of the K loop's VGPRs)
+  const bool second = part == 1;
+  const long long pbase = __builtin_amdgcn_readfirstlane(pos0 - prm.pos_begin - prm.n_whole * PT);
   auto kat = [&](int i) -> int {                             // the K-step at list position i
     const int ii = i < n_act ? i : n_act - 1;
     return ii >= 0 ? __builtin_amdgcn_readfirstlane((int)klist[ii]) : 0;
@@ -241,7 +265,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
     srun[tid] = 0.0;
   }
 
-  for (int c0 = 0; c0 < n_tiles; c0 += TPC) {
+  for (int c0 = c_lo * TPC; c0 < c_hi * TPC; c0 += TPC) {
     // ---- this wave's tiles of the chunk: list index i = c0 + NW nt + w ----------------
     // kend: list positions the tile multiplies; tb: byte offset of its data in the image (a
     // retired tile's prefetch past its diagonal reads the following tiles' data, never past
@@ -293,10 +317,15 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
     const int rlim = min(c0 + TPC, n_act);
     auto consume = [&](int i0, int i1) {                     // positions i0 .. i1 (wave 0)
       if (tid < PT) {
-        double qa = qrun[tid];
-        for (int q = i0; q <= i1; ++q)
-          if (q >= c0 && q < rlim) qa += ptq[q & 3][tid];
-        qrun[tid] = qa;
+        if (second) {                                        // a second part: the partials
+          for (int q = i0; q <= i1; ++q)
+            if (q >= c0 && q < rlim) prm.part[pbase + (long long)(q - TPC) * prm.ld_part + tid] = ptq[q & 3][tid];
+        } else {
+          double qa = qrun[tid];
+          for (int q = i0; q <= i1; ++q)
+            if (q >= c0 && q < rlim) qa += ptq[q & 3][tid];
+          qrun[tid] = qa;
+        }
       }
     };
     auto step = [&](auto t0c, auto t1c, int i, bool retire, double (&bb)[4 * NTW]) {
@@ -423,9 +452,14 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
       __syncthreads();
       if (tid < PT) {
         const int ns = min(TPC, n_tiles - c0);
-        double sa = srun[tid];
-        for (int s = n_act - c0 > 0 ? n_act - c0 : 0; s < ns; ++s) sa += ptile[s * PT + tid];
-        srun[tid] = sa;
+        if (second) {
+          for (int s = n_act - c0 > 0 ? n_act - c0 : 0; s < ns; ++s)
+            prm.part[pbase + (long long)(c0 + s - TPC) * prm.ld_part + tid] = ptile[s * PT + tid];
+        } else {
+          double sa = srun[tid];
+          for (int s = n_act - c0 > 0 ? n_act - c0 : 0; s < ns; ++s) sa += ptile[s * PT + tid];
+          srun[tid] = sa;
+        }
       }
     }
 #pragma unroll
@@ -435,11 +469,11 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
     __syncthreads();                                         // before the next chunk's ring
   }
 
-  if (tid < PT && pos0 + tid < pos_end) {
+  if (part != 1 && tid < PT && pos0 + tid < pos_end) {
     prm.q[pos0 + tid - prm.pos_begin] = qrun[tid];
     prm.S[pos0 + tid - prm.pos_begin] = srun[tid];
   }
-  if (prm.sp_stats && tid == 0) {
+  if (prm.sp_stats && part != 1 && tid == 0) {
     {
       // the dense kernel's MFMA groups for this tile: every R tile to its diagonal, every
       // mean tile over all K-steps
@@ -452,13 +486,33 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
 // 32-particle tiles of 4 waves x 8 column tiles up to d = 8, 64-particle tiles of 8 waves x 4
 // above (the dense kernel's shapes; the particle coordinates push 32 x 512 into spills)
 template <int DI>
-void launch_cut_d(const CutoffParams& p, hipStream_t s) {
+bool launch_cut_d(const CutoffParams& p, hipStream_t s) {
   const long long n = (long long)p.pos_end - p.pos_begin;
-  if (n <= 0) return;
+  if (n <= 0) return true;
+  constexpr int PT = DI <= 8 ? 32 : 64;
+  // grid: the whole tiles, then two workgroups per split tile (capi_frame.hip sets n_whole +
+  // n_split = the tile count)
+  const unsigned grid = (unsigned)(p.n_whole + 2 * p.n_split);
+  if (p.n_whole < 0 || p.n_split < 0 || (long long)(p.n_whole + p.n_split) * PT < n ||
+      (long long)(p.n_whole + p.n_split - 1) * PT >= n || (p.n_split > 0 && (!p.part || !p.split)))
+    return false;
   if constexpr (DI <= 8)
-    hipLaunchKernelGGL((k_obs_cutoff<DI, 4, 2, 8>), dim3((unsigned)((n + 31) / 32)), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((k_obs_cutoff<DI, 4, 2, 8>), dim3(grid), dim3(256), 0, s, p);
   else
-    hipLaunchKernelGGL((k_obs_cutoff<DI, 8, 4, 4>), dim3((unsigned)((n + 63) / 64)), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((k_obs_cutoff<DI, 8, 4, 4>), dim3(grid), dim3(512), 0, s, p);
+  return true;
+}
+
+// workgroups of the cutoff kernel resident per CU at d
+template <int DI>
+int cut_blocks_per_cu_d() {
+  int b = 0;
+  hipError_t e;
+  if constexpr (DI <= 8)
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_obs_cutoff<DI, 4, 2, 8>), 256, 0);
+  else
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_obs_cutoff<DI, 8, 4, 4>), 512, 0);
+  return e == hipSuccess && b > 0 ? b : 1;
 }
 
 }  // namespace gpmdm

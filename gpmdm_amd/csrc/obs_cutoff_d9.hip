@@ -3,12 +3,20 @@
 #include "obs_cutoff.h"
 
 namespace gpmdm {
-template void launch_cut_d<9>(const CutoffParams&, hipStream_t);
-template void launch_cut_d<10>(const CutoffParams&, hipStream_t);
-template void launch_cut_d<11>(const CutoffParams&, hipStream_t);
-template void launch_cut_d<12>(const CutoffParams&, hipStream_t);
-template void launch_cut_d<13>(const CutoffParams&, hipStream_t);
-template void launch_cut_d<14>(const CutoffParams&, hipStream_t);
-template void launch_cut_d<15>(const CutoffParams&, hipStream_t);
-template void launch_cut_d<16>(const CutoffParams&, hipStream_t);
+template bool launch_cut_d<9>(const CutoffParams&, hipStream_t);
+template int cut_blocks_per_cu_d<9>();
+template bool launch_cut_d<10>(const CutoffParams&, hipStream_t);
+template int cut_blocks_per_cu_d<10>();
+template bool launch_cut_d<11>(const CutoffParams&, hipStream_t);
+template int cut_blocks_per_cu_d<11>();
+template bool launch_cut_d<12>(const CutoffParams&, hipStream_t);
+template int cut_blocks_per_cu_d<12>();
+template bool launch_cut_d<13>(const CutoffParams&, hipStream_t);
+template int cut_blocks_per_cu_d<13>();
+template bool launch_cut_d<14>(const CutoffParams&, hipStream_t);
+template int cut_blocks_per_cu_d<14>();
+template bool launch_cut_d<15>(const CutoffParams&, hipStream_t);
+template int cut_blocks_per_cu_d<15>();
+template bool launch_cut_d<16>(const CutoffParams&, hipStream_t);
+template int cut_blocks_per_cu_d<16>();
 }  // namespace gpmdm

@@ -173,6 +173,12 @@ struct ObsFinishArgs {
   // single filters: the maximum of each block's ll (ord_enc keys), which the normaliser
   // reads instead of running k_norm_max (nullptr: not produced)
   unsigned long long* bmax;
+  // the cutoff kernel's split tiles (obs_cutoff.h): outputs from cut_o0 on chain their second
+  // part's partials onto q and S in list order (nullptr: no split tiles)
+  const double* cut_part;
+  long long cut_ld, cut_o0;
+  const int2* cut_split;
+  int cut_pt, cut_tpc, cut_tm;
 };
 
 // Normalisation and resampling run per filter: grid (nb, F), nb blocks of 256 per filter.

@@ -715,6 +715,21 @@ __device__ __forceinline__ double obs_ll_value(const ObsFinishArgs& a, long long
   for (int k = 0; k < a.n_parts; ++k) q += a.qpart[(long long)k * a.ld_q + o];
   double S = 0.0;
   for (int k = a.jm0; k < a.n_j; ++k) S += a.spart[(long long)k * a.ld_q + o];
+  if (a.cut_part && o >= a.cut_o0) {
+    // a split tile: its first part left q and S over list entries [0, tpc c*); the second
+    // part's entries follow in list order (R tiles into q, then mean tiles into S), the whole
+    // tile's running sums exactly
+    const long long r = o - a.cut_o0;
+    const int2 sp = a.cut_split[r / a.cut_pt];
+    const int nt = sp.x + a.cut_tm;
+    for (int i = sp.y * a.cut_tpc; i < nt; ++i) {
+      const double v = a.cut_part[(long long)(i - a.cut_tpc) * a.cut_ld + r];
+      if (i < sp.x)
+        q += v;
+      else
+        S += v;
+    }
+  }
   vc = 1.0 - q;                                        // k(x*,x*) = 1 (gpmdm.py:991)
   return -0.5 * S / vc - a.D * log(vc) - a.sum_log_il2 - a.ll_const;
 }

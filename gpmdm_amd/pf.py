@@ -530,10 +530,16 @@ class GPMDM_PF:
         self.load_state(st["states"], st["classes"], ll=st["ll"], log_w=st["log_w"], w=st["w"],
                         resample_idx=st.get("resample_idx"), frame=st.get("frame"))
 
-    def set_obs_cutoff(self, on: bool = True, stats: bool = False):
+    _CUT_SPLIT = {"tail": 0, "none": 1, "all": 2}
+
+    def set_obs_cutoff(self, on: bool = True, stats: bool = False, split: str | None = None):
         """Run the observation GP with the model's kernel-value cutoff (GPMDM.enable_obs_cutoff,
         built here if needed) or the dense kernel; ``stats`` also counts the MFMA groups run
-        (obs_cutoff_stats).  Between frames only."""
+        (obs_cutoff_stats); ``split`` ("tail" default, "none", "all") schedules the particle
+        tiles run as two workgroups each (gpmdm_pf_set_obs_cutoff_split; the same results
+        under every policy).  Between frames only."""
+        if split is not None and split not in self._CUT_SPLIT:
+            raise ValueError(f"split: one of {sorted(self._CUT_SPLIT)}")
         if on:
             self._gpmdm.enable_obs_cutoff(True)
             self._sync_model()
@@ -541,6 +547,8 @@ class GPMDM_PF:
         lib = _lib.load()
         for h in [self._h] + [p[0] for p in self._peers]:
             _lib.check(lib.gpmdm_pf_set_obs_cutoff(h, mode), "set_obs_cutoff")
+            if split is not None:
+                _lib.check(lib.gpmdm_pf_set_obs_cutoff_split(h, self._CUT_SPLIT[split]), "set_obs_cutoff")
         self._obs_cutoff = mode
 
     def obs_cutoff_stats(self, reset: bool = True) -> dict:

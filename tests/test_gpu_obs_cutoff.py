@@ -198,6 +198,34 @@ def test_cutoff_logical_shards_match_one_rank(m2c, world, P):
             assert np.array_equal(ref.class_probabilities().numpy(), pf.class_probabilities().numpy())
 
 
+@pytest.mark.parametrize("P", [100_000, 20_000])
+def test_cutoff_split_policies_bitwise(m2c, P):
+    """The cutoff kernel's tile scheduling (set_obs_cutoff(split=...)): whole tiles, the grid's
+    tail as two workgroups per tile (the default), every tile as two -- the same states,
+    classes, log-likelihoods and ancestors bit for bit over 4 frames of the bench's stream: the
+    second workgroup's per-tile partials, chained on in list order by the likelihood finish,
+    are the whole tile's running sums."""
+    from gpmdm_amd import GPMDM_PF, synthetic
+    data = synthetic.make_sequences(2, 5, 200, 62, 3, seed=0)
+    zs = data.observation_stream(6, seed=1)
+    T = torch.tensor(synthetic.markov_matrix(2))
+    out = {}
+    for split in ("none", "tail", "all"):
+        torch.manual_seed(4)                 # (the initial cloud)
+        pf = GPMDM_PF(m2c, T, P, rng="philox", seed=11, obs_cutoff=True)
+        pf.set_obs_cutoff(True, split=split)
+        out[split] = []
+        for k in range(4):
+            pf.update(zs[k])
+            out[split].append(pf.export_state())
+    with pytest.raises(ValueError):
+        pf.set_obs_cutoff(True, split="half")
+    for split in ("tail", "all"):
+        for k in range(4):
+            for key in ("states", "classes", "ll", "log_w", "resample_idx"):
+                assert np.array_equal(out["none"][k][key], out[split][k][key]), (split, k, key)
+
+
 def test_cutoff_skips_work_on_the_benchmark_cloud(m2c):
     """The bench's workload (config-2 model, P = 100k, the mocap-surrogate stream): the
     cutoff kernel runs a fraction of the dense kernel's MFMA groups."""
