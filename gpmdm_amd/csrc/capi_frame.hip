@@ -446,8 +446,9 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
       const int tiles = (int)cdiv(nl, PT);
       const int slots = cutoff_slots(d);
       int n_split = cut_split_tiles(pf, tiles, slots);
-      const long long entries = (long long)ci.T_R + ci.T_M - TPC;   // list entries a second part can hold
-      if (entries <= 0) n_split = 0;
+      // list entries a second part can hold (all but the first chunk's, at least one)
+      const long long entries = (long long)ci.T_R + ci.T_M - 1;
+      if (ci.T_R + ci.T_M <= TPC) n_split = 0;   // one chunk: nothing to split
       if (n_split > 0) TRY(pf->ensure_cut_split((size_t)entries * n_split * PT, n_split));
       cp.n_whole = tiles - n_split;
       cp.n_split = n_split;

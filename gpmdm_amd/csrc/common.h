@@ -68,8 +68,9 @@ struct CutoffParams {
   long long Pf;              // particles per filter
   unsigned long long* sp_stats;   // MFMA groups run / the dense kernel's, or nullptr
   // split tiles (the grid's tail): particle tiles [n_whole, n_whole + n_split) run as two
-  // workgroups each, chunks [0, c*) (q, S as a whole tile's, so far) and [c*, nc) (each list
-  // entry's partial into part[(i - tpc) * ld_part + o - n_whole * PT], k_obs_ll chains them on)
+  // workgroups each, chunks [0, c*) (q, S as a whole tile's, so far) and [c*, nc) (list entry
+  // i's partial into part[(i - r0) * ld_part + o - n_whole * PT], r0 = the first chunk's
+  // size; k_obs_ll chains them on)
   int n_whole, n_split;
   double* part;
   long long ld_part;
@@ -80,11 +81,17 @@ int cutoff_tile_particles(int d);   // PT of the cutoff kernel at d
 int cutoff_tile_list_chunk();       // tpc: list entries per chunk
 int cutoff_slots(int d);            // workgroups resident at once on the device (cached per d)
 
-// K-loop positions chunk c of a tile list runs (obs_cutoff.h): up to its last R tile's
-// diagonal, every active K-step once it holds a mean tile
+// First list entry of chunk c of a tile list of nt entries (obs_cutoff.h): the partial chunk
+// first (nt - (nc - 1) tpc entries: the chunk that runs the fewest positions), then full ones
+__host__ __device__ inline int cutoff_chunk_begin(int c, int nt, int tpc) {
+  if (c <= 0) return 0;
+  const int nc = (nt + tpc - 1) / tpc;
+  return nt - (nc - c) * tpc;
+}
+// K-loop positions chunk c runs: up to its last R tile's diagonal, every active K-step once it
+// holds a mean tile
 __host__ __device__ inline int cutoff_chunk_positions(int c, int n_act, int T_M, int tpc) {
-  const int nt = n_act + T_M;
-  const int last = (c + 1) * tpc < nt ? (c + 1) * tpc - 1 : nt - 1;
+  const int last = cutoff_chunk_begin(c + 1, n_act + T_M, tpc) - 1;
   return last < n_act ? last + 1 : n_act;
 }
 // The split chunk c* of a split tile: the first chunk of its second workgroup, balancing the

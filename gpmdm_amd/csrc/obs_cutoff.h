@@ -17,8 +17,9 @@
 //    and each chunk runs the dense kernel's K loop (gp_tile.h: generation two positions ahead
 //    into an LDS ring, rows staged four ahead, B one position ahead in VGPRs, one barrier per
 //    two positions, tiles retiring in phases) over list positions only: every chunk but the
-//    last is full whatever the cloud, so the MFMAs per generated K-step stay those of the
-//    dense kernel however few tiles are active;
+//    first is full whatever the cloud (the partial one first, where it runs the fewest
+//    positions), so the MFMAs per generated K-step stay those of the dense kernel however few
+//    tiles are active;
 //  * q = sum_j k_j V_j, V = K* B over the symmetric image, and S = sum_j (z_j - mu_j)^2 lam2_j
 //    (mu = the mean tiles' V) are summed per column tile (its 16 columns by a DPP row
 //    reduction) and then over the tiles in list order, by one thread per particle.  An R
@@ -201,9 +202,10 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
       c_lo = cs;
     }
   }
-  // (the second part's partials: list entry i of particle m at part[(i - TPC) ld + o])
-  // (uniform, so it stays out of the K loop's VGPRs)
+  // (the second part's partials: list entry i of particle m at part[(i - r0) ld + o], r0 the
+  // first chunk's size; uniform, so it stays out of the K loop's VGPRs)
   const bool second = part == 1;
+  const int r0 = __builtin_amdgcn_readfirstlane(cutoff_chunk_begin(1, n_tiles, TPC));
   const long long pbase = __builtin_amdgcn_readfirstlane(pos0 - prm.pos_begin - prm.n_whole * PT);
   auto kat = [&](int i) -> int {                             // the K-step at list position i
     const int ii = i < n_act ? i : n_act - 1;
@@ -265,26 +267,29 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
     srun[tid] = 0.0;
   }
 
-  for (int c0 = c_lo * TPC; c0 < c_hi * TPC; c0 += TPC) {
-    // ---- this wave's tiles of the chunk: list index i = c0 + NW nt + w ----------------
+  for (int c = c_lo; c < c_hi; ++c) {
+    // ---- this wave's tiles of the chunk: list index i = c0 + NW nt + w < cend ----------
+    // (the partial chunk first: cutoff_chunk_begin)
+    const int c0 = __builtin_amdgcn_readfirstlane(cutoff_chunk_begin(c, n_tiles, TPC));
+    const int cend = __builtin_amdgcn_readfirstlane(cutoff_chunk_begin(c + 1, n_tiles, TPC));
     // kend: list positions the tile multiplies; tb: byte offset of its data in the image (a
     // retired tile's prefetch past its diagonal reads the following tiles' data, never past
     // the image: every tile is followed by at least T_R K-steps of mean tiles)
     auto kend = [&](int nt) -> int {
       const int i = c0 + NW * nt + w;
-      return i >= n_tiles ? 0 : (i < n_act ? i + 1 : n_act);
+      return i >= cend ? 0 : (i < n_act ? i + 1 : n_act);
     };
     unsigned tb[NTW];
     int T1 = 0;
 #pragma unroll
     for (int nt = 0; nt < NTW; ++nt) {
       const int i = c0 + NW * nt + w;
-      const bool valid = i < n_tiles;
+      const bool valid = i < cend;
       if (valid) T1 = nt + 1;
       const int t = !valid ? 0 : (i < n_act ? kat(i) : T_R + (i - n_act));
       tb[nt] = __builtin_amdgcn_readfirstlane((unsigned)(prm.toff[t] * 8));
     }
-    const int last = min(c0 + TPC, n_tiles) - 1;
+    const int last = cend - 1;
     const int npos = last < n_act ? last + 1 : n_act;          // list positions of this chunk
     // The K-steps of list positions [kb0, kb0 + 128) in two VGPR windows (lane j of kw0 / kw1:
     // position kb0 + j / kb0 + 64 + j): in the K loop a K-step is one v_readlane, not an LDS
@@ -314,12 +319,12 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
     };
     // R tiles of this chunk retire at list positions [c0, rlim), one per position, in list
     // order: their partials are added in that order, as the sum over tiles requires
-    const int rlim = min(c0 + TPC, n_act);
+    const int rlim = min(cend, n_act);
     auto consume = [&](int i0, int i1) {                     // positions i0 .. i1 (wave 0)
       if (tid < PT) {
         if (second) {                                        // a second part: the partials
           for (int q = i0; q <= i1; ++q)
-            if (q >= c0 && q < rlim) prm.part[pbase + (long long)(q - TPC) * prm.ld_part + tid] = ptq[q & 3][tid];
+            if (q >= c0 && q < rlim) prm.part[pbase + (long long)(q - r0) * prm.ld_part + tid] = ptq[q & 3][tid];
         } else {
           double qa = qrun[tid];
           for (int q = i0; q <= i1; ++q)
@@ -432,7 +437,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
         const int i2 = c0 + NW * nt + w;
-        if (i2 < n_act || i2 >= n_tiles) continue;           // (wave-uniform)
+        if (i2 < n_act || i2 >= cend) continue;              // (wave-uniform)
         // (z_j - mu_j)^2 lam2_j over the tile's columns (gpmdm_pf.py:188-192 with var_j =
         // vc / lam2_j factored out; k_obs_ll finishes the likelihood), reduced over its 16
         // columns (lanes li)
@@ -451,10 +456,10 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
       }
       __syncthreads();
       if (tid < PT) {
-        const int ns = min(TPC, n_tiles - c0);
+        const int ns = cend - c0;
         if (second) {
           for (int s = n_act - c0 > 0 ? n_act - c0 : 0; s < ns; ++s)
-            prm.part[pbase + (long long)(c0 + s - TPC) * prm.ld_part + tid] = ptile[s * PT + tid];
+            prm.part[pbase + (long long)(c0 + s - r0) * prm.ld_part + tid] = ptile[s * PT + tid];
         } else {
           double sa = srun[tid];
           for (int s = n_act - c0 > 0 ? n_act - c0 : 0; s < ns; ++s) sa += ptile[s * PT + tid];

@@ -722,8 +722,9 @@ __device__ __forceinline__ double obs_ll_value(const ObsFinishArgs& a, long long
     const long long r = o - a.cut_o0;
     const int2 sp = a.cut_split[r / a.cut_pt];
     const int nt = sp.x + a.cut_tm;
-    for (int i = sp.y * a.cut_tpc; i < nt; ++i) {
-      const double v = a.cut_part[(long long)(i - a.cut_tpc) * a.cut_ld + r];
+    const int r0 = cutoff_chunk_begin(1, nt, a.cut_tpc);
+    for (int i = cutoff_chunk_begin(sp.y, nt, a.cut_tpc); i < nt; ++i) {
+      const double v = a.cut_part[(long long)(i - r0) * a.cut_ld + r];
       if (i < sp.x)
         q += v;
       else
