@@ -352,8 +352,9 @@ def cutoff_line(model, T, P, zs, warmup, steps, headline_ms=None, headline_obs_m
     """The same step with the observation GP's opt-in kernel-value cutoff
     (GPMDM_PF(obs_cutoff=True)): kernel values below the model's tau flushed to
     0 and the unreachable 16-row K-steps skipped.  A timed pass (the roofline kernel's events
-    on every 4th frame), then an untimed stats pass counting the MFMA groups the kernel ran
-    against the dense kernel's (executed FLOP = groups x 16 x 16 x 16 x 2).  Results equal the
+    on every 4th frame), then the same frames replayed from the same state, untimed, counting
+    the MFMA groups the kernel ran on the event-timed frames against the dense kernel's
+    (executed FLOP = groups x 16 x 16 x 16 x 2).  Results equal the
     dense filter's to rounding (tests/test_gpu_obs_cutoff.py); beside the headline, never it."""
     import torch
     from gpmdm_amd import GPMDM_PF, _lib
@@ -376,6 +377,8 @@ def cutoff_line(model, T, P, zs, warmup, steps, headline_ms=None, headline_obs_m
     pf.enable_timing(True, stages=("obs_gemm",))
     pf.enable_timing(False)
     lib_, h_ = _lib.load(), pf._h
+    snap = pf.export_state()             # (the stats pass replays the timed frames from here)
+    torch.cuda.synchronize()
     t1 = time.perf_counter()
     for k in range(steps):
         if k % 4 == 0:
@@ -388,14 +391,20 @@ def cutoff_line(model, T, P, zs, warmup, steps, headline_ms=None, headline_obs_m
     pf.enable_timing(False)
     obs_ms, obs_n = pf.stage_times()["obs_gemm"]
     obs_launch_ms = obs_ms / max(obs_n, 1)
-    # stats pass: the next frames of the stream, MFMA groups counted by the kernel
-    pf.set_obs_cutoff(True, stats=True)
+    # stats pass: the timed frames again from the same state (Philox: the same clouds), the
+    # MFMA groups counted by the kernel on the frames whose launches were timed
+    pf.load_state(snap["states"], snap["classes"], ll=snap["ll"], log_w=snap["log_w"], w=snap["w"],
+                  resample_idx=snap["resample_idx"], frame=snap.get("frame"))
     pf.obs_cutoff_stats(reset=True)
-    n_st = min(steps, 10)
-    for k in range(n_st):
-        frame(warmup + steps + k)
+    n_st = 0
+    for k in range(steps):
+        if k % 4 == 0:
+            _lib.check(lib_.gpmdm_pf_set_obs_cutoff(h_, 2), "stats")
+        frame(warmup + k)
+        if k % 4 == 0:
+            _lib.check(lib_.gpmdm_pf_set_obs_cutoff(h_, 1), "stats")
+            n_st += 1
     st = pf.obs_cutoff_stats()
-    pf.set_obs_cutoff(True, stats=False)
     tau = model.obs_cutoff_tau
     ms = el / steps * 1e3
     groups_per_launch = st["run"] / max(n_st, 1)
@@ -411,9 +420,10 @@ def cutoff_line(model, T, P, zs, warmup, steps, headline_ms=None, headline_obs_m
            "setup_s": setup_s,
            "note": "GPMDM_PF(obs_cutoff=True): kernel values below tau flushed to 0 (tau bounds the change "
                    "of 1 - k^T K^-1 k below half an ulp, DESIGN.md §3) and the MFMAs of unreachable 16-row "
-                   "K-steps skipped; mfma_groups_run_fraction = groups the kernel ran / the dense kernel's "
-                   "over a 10-frame stats pass after the timed frames; executed_tflops = those groups x 8192 "
-                   "FLOP / the observation launch time; results equal the dense filter's to rounding "
+                   "K-steps skipped; mfma_groups_run_fraction = groups the kernel ran / the dense kernel's, "
+                   "counted on the event-timed frames replayed from the same state; executed_tflops = those "
+                   "groups x 8192 FLOP / the observation launch time; results equal the dense filter's to "
+                   "rounding "
                    "(tests/test_gpu_obs_cutoff.py)"}
     return out
 
