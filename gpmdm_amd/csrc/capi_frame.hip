@@ -517,7 +517,9 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
       pf->oa_pending = oa;             // computed by the resampling launch (or flush_ll)
       pf->ll_pending = true;
     } else {
-      if (pf->bmax && !oa.own && oa.ll_offset == 0) {   // single filter: the maxima for k_norm_exp_scan
+      // single filter (one rank): the maxima for k_norm_exp_scan, in any particle order (the
+      // maximum over the blocks' maxima does not depend on which particles a block holds)
+      if (pf->bmax && oa.ll_offset == 0) {
         oa.bmax = pf->bmax;
         pf->bmax_ready = true;
       }

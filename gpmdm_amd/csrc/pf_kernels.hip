@@ -723,8 +723,22 @@ __device__ __forceinline__ double obs_ll_value(const ObsFinishArgs& a, long long
     const int2 sp = a.cut_split[r / a.cut_pt];
     const int nt = sp.x + a.cut_tm;
     const int r0 = cutoff_chunk_begin(1, nt, a.cut_tpc);
-    for (int i = cutoff_chunk_begin(sp.y, nt, a.cut_tpc); i < nt; ++i) {
-      const double v = a.cut_part[(long long)(i - r0) * a.cut_ld + r];
+    const double* pp = a.cut_part + r;
+    int i = cutoff_chunk_begin(sp.y, nt, a.cut_tpc);
+    for (; i + 8 <= nt; i += 8) {              // eight loads in flight, then the adds in order
+      double v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = pp[(long long)(i + k - r0) * a.cut_ld];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (i + k < sp.x)
+          q += v[k];
+        else
+          S += v[k];
+      }
+    }
+    for (; i < nt; ++i) {
+      const double v = pp[(long long)(i - r0) * a.cut_ld];
       if (i < sp.x)
         q += v;
       else
