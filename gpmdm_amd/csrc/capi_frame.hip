@@ -364,13 +364,25 @@ int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s, bool 
 // _update_weights' likelihoods for this rank's particles (gpmdm_pf.py:170-192): uploads z,
 // runs the observation GP tile and the likelihood finish.
 // Particle tiles of the cutoff launch that run as two workgroups each
-// (gpmdm_pf_set_obs_cutoff_split): by default the tiles past the last full round of resident
-// slots (all of them below one round).
-static int cut_split_tiles(const gpmdm_pf* pf, int tiles, int slots) {
-  if (pf->cut_split_policy == GPMDM_CUT_SPLIT_NONE) return 0;
-  if (pf->cut_split_policy == GPMDM_CUT_SPLIT_ALL) return tiles;
-  if (slots <= 0 || tiles <= slots) return tiles;
-  return tiles % slots;
+// (gpmdm_pf_set_obs_cutoff_split).  AUTO, from the measured policies (DESIGN.md §3 "The grid's
+// tail"): every tile when the launch is at most two rounds of the resident slots or its last
+// round is at most an eighth full (and the partials fit in max_all_bytes), none at whole
+// rounds, otherwise the last round's tiles.
+static int cut_split_tiles(const gpmdm_pf* pf, int tiles, int slots, size_t all_bytes) {
+  constexpr size_t kMaxAllBytes = size_t(2) << 30;
+  const int rem = slots > 0 ? tiles % slots : 0;
+  switch (pf->cut_split_policy) {
+    case GPMDM_CUT_SPLIT_NONE: return 0;
+    case GPMDM_CUT_SPLIT_ALL: return tiles;
+    case GPMDM_CUT_SPLIT_TAIL: return slots <= 0 || tiles <= slots ? tiles : rem;
+    default: break;
+  }
+  if (slots <= 0) return 0;
+  const bool all_fits = all_bytes <= kMaxAllBytes;
+  if (tiles <= 2 * slots) return all_fits ? tiles : std::min(tiles, rem ? rem : tiles);
+  if (rem == 0) return 0;
+  if (rem <= slots / 8 && all_fits) return tiles;
+  return rem;
 }
 
 int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
@@ -445,9 +457,9 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
       const int PT = cutoff_tile_particles(d), TPC = cutoff_tile_list_chunk();
       const int tiles = (int)cdiv(nl, PT);
       const int slots = cutoff_slots(d);
-      int n_split = cut_split_tiles(pf, tiles, slots);
       // list entries a second part can hold (all but the first chunk's, at least one)
       const long long entries = (long long)ci.T_R + ci.T_M - 1;
+      int n_split = cut_split_tiles(pf, tiles, slots, (size_t)entries * tiles * PT * sizeof(double));
       if (ci.T_R + ci.T_M <= TPC) n_split = 0;   // one chunk: nothing to split
       if (n_split > 0) TRY(pf->ensure_cut_split((size_t)entries * n_split * PT, n_split));
       cp.n_whole = tiles - n_split;

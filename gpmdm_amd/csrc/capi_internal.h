@@ -211,7 +211,7 @@ struct gpmdm_pf {
   bool sp_stats_on = false;
   // the cutoff kernel's split tiles (capi_frame.hip): second parts' partials, (n_act, c*) per
   // split tile; grown on demand
-  int cut_split_policy = GPMDM_CUT_SPLIT_TAIL;
+  int cut_split_policy = GPMDM_CUT_SPLIT_AUTO;
   double* cut_part = nullptr;
   size_t cut_part_cap = 0;
   int2* cut_split = nullptr;

@@ -618,8 +618,9 @@ int gpmdm_pf_set_obs_cutoff(gpmdm_pf_t pf, int mode) {
 
 int gpmdm_pf_set_obs_cutoff_split(gpmdm_pf_t pf, int policy) {
   CHECK(pf, "null handle");
-  CHECK(policy == GPMDM_CUT_SPLIT_TAIL || policy == GPMDM_CUT_SPLIT_NONE || policy == GPMDM_CUT_SPLIT_ALL,
-        "policy: GPMDM_CUT_SPLIT_TAIL, _NONE or _ALL");
+  CHECK(policy == GPMDM_CUT_SPLIT_AUTO || policy == GPMDM_CUT_SPLIT_NONE || policy == GPMDM_CUT_SPLIT_ALL ||
+            policy == GPMDM_CUT_SPLIT_TAIL,
+        "policy: GPMDM_CUT_SPLIT_AUTO, _NONE, _ALL or _TAIL");
   if (pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "set_obs_cutoff_split between propagate and resample");
   pf->cut_split_policy = policy;
   return GPMDM_OK;

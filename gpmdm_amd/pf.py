@@ -530,14 +530,14 @@ class GPMDM_PF:
         self.load_state(st["states"], st["classes"], ll=st["ll"], log_w=st["log_w"], w=st["w"],
                         resample_idx=st.get("resample_idx"), frame=st.get("frame"))
 
-    _CUT_SPLIT = {"tail": 0, "none": 1, "all": 2}
+    _CUT_SPLIT = {"auto": 0, "none": 1, "all": 2, "tail": 3}
 
     def set_obs_cutoff(self, on: bool = True, stats: bool = False, split: str | None = None):
         """Run the observation GP with the model's kernel-value cutoff (GPMDM.enable_obs_cutoff,
         built here if needed) or the dense kernel; ``stats`` also counts the MFMA groups run
-        (obs_cutoff_stats); ``split`` ("tail" default, "none", "all") schedules the particle
-        tiles run as two workgroups each (gpmdm_pf_set_obs_cutoff_split; the same results
-        under every policy).  Between frames only."""
+        (obs_cutoff_stats); ``split`` ("auto" default, "none", "all", "tail") schedules the
+        particle tiles run as two workgroups each (gpmdm_pf_set_obs_cutoff_split; the same
+        results under every policy).  Between frames only."""
         if split is not None and split not in self._CUT_SPLIT:
             raise ValueError(f"split: one of {sorted(self._CUT_SPLIT)}")
         if on:

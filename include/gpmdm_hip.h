@@ -377,12 +377,15 @@ int gpmdm_model_obs_cutoff(gpmdm_model_t model, double* tau);
 int gpmdm_pf_set_obs_cutoff(gpmdm_pf_t pf, int mode);
 int gpmdm_pf_obs_cutoff_stats(gpmdm_pf_t pf, int64_t* run, int64_t* dense, int reset, void* stream);
 /* Scheduling of the cutoff kernel's particle tiles (results are identical under every
- * policy): GPMDM_CUT_SPLIT_TAIL (default) runs the tiles past the last full round of resident
- * workgroups -- every tile below one round -- as two workgroups each, _NONE none, _ALL every
- * tile.  Between frames only. */
-#define GPMDM_CUT_SPLIT_TAIL 0
+ * policy): a split tile runs as two workgroups.  GPMDM_CUT_SPLIT_AUTO (default): every tile
+ * when the launch is at most two rounds of resident workgroups or its last round holds at
+ * most an eighth of a round, none at whole rounds, otherwise the tiles of the last round
+ * (measured, DESIGN.md §3 "The grid's tail"); _NONE, _ALL, _TAIL (the last round's tiles).
+ * Between frames only. */
+#define GPMDM_CUT_SPLIT_AUTO 0
 #define GPMDM_CUT_SPLIT_NONE 1
 #define GPMDM_CUT_SPLIT_ALL 2
+#define GPMDM_CUT_SPLIT_TAIL 3
 int gpmdm_pf_set_obs_cutoff_split(gpmdm_pf_t pf, int policy);
 
 /* Failure detection.  The filter keeps the reference's arithmetic: a

@@ -201,7 +201,7 @@ def test_cutoff_logical_shards_match_one_rank(m2c, world, P):
 @pytest.mark.parametrize("P", [100_000, 20_000])
 def test_cutoff_split_policies_bitwise(m2c, P):
     """The cutoff kernel's tile scheduling (set_obs_cutoff(split=...)): whole tiles, the grid's
-    tail as two workgroups per tile (the default), every tile as two -- the same states,
+    tail as two workgroups per tile, every tile as two, the default's choice -- the same states,
     classes, log-likelihoods and ancestors bit for bit over 4 frames of the bench's stream: the
     second workgroup's per-tile partials, chained on in list order by the likelihood finish,
     are the whole tile's running sums."""
@@ -210,7 +210,7 @@ def test_cutoff_split_policies_bitwise(m2c, P):
     zs = data.observation_stream(6, seed=1)
     T = torch.tensor(synthetic.markov_matrix(2))
     out = {}
-    for split in ("none", "tail", "all"):
+    for split in ("none", "tail", "all", "auto"):
         torch.manual_seed(4)                 # (the initial cloud)
         pf = GPMDM_PF(m2c, T, P, rng="philox", seed=11, obs_cutoff=True)
         pf.set_obs_cutoff(True, split=split)
@@ -220,7 +220,7 @@ def test_cutoff_split_policies_bitwise(m2c, P):
             out[split].append(pf.export_state())
     with pytest.raises(ValueError):
         pf.set_obs_cutoff(True, split="half")
-    for split in ("tail", "all"):
+    for split in ("tail", "all", "auto"):
         for k in range(4):
             for key in ("states", "classes", "ll", "log_w", "resample_idx"):
                 assert np.array_equal(out["none"][k][key], out[split][k][key]), (split, k, key)
