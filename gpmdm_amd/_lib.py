@@ -93,6 +93,7 @@ _SIGS = {
     "gpmdm_comm_init": (c_int, [c_int, c_int, c_void_p, c_int, POINTER(c_void_p)]),
     "gpmdm_comm_destroy": (c_int, [c_void_p]),
     "gpmdm_comm_init_all": (c_int, [c_int, POINTER(c_int), POINTER(c_void_p)]),
+    "gpmdm_comm_init_loopback": (c_int, [c_int, POINTER(c_int), POINTER(c_void_p)]),
     "gpmdm_pf_propagate_multi": (c_int, [POINTER(c_void_p), c_int, _dp, _dp, POINTER(c_void_p)]),
     "gpmdm_gp_factor": (c_int, [c_int, _dp, c_int64, c_int32, _dp, _dp, c_double, c_double, c_double,
                                 _dp, c_int64, _dp, _dp]),

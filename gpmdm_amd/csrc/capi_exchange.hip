@@ -2,6 +2,8 @@
 // rows, the library-driven exchange over an RCCL communicator (gpmdm_pf_set_comm,
 // gpmdm_comm_*), the staged calls propagate_dynamics / weigh, and rows read in place by the
 // resample (replaces the single-process hand-over of gpmdm_pf.py:194-213).
+#include <condition_variable>
+
 #include "capi_internal.h"
 
 namespace gpmdm::capi {
@@ -73,11 +75,157 @@ static int nccl_fail(ncclResult_t r, const char* what) {
   return fail(GPMDM_E_HIP, std::string(what) + ": " + (rccl().ok ? rccl().GetErrorString(r) : "RCCL missing"));
 }
 
+// ---- In-process loopback transport (gpmdm_comm_init_loopback; tests only) ----------------
+// The exchange's collectives with the same call pattern and stream semantics as RCCL's, for
+// R ranks held by one process -- also R ranks on ONE device, which RCCL refuses -- so the
+// library's multi-rank exchange (uneven shards, staging + copy-down, grouped collectives,
+// several streams) runs at R > 1 on a one-GPU box.  An all-gather registers each rank's
+// (send, recv, stream) and an event on that stream (its send rows are final there); the last
+// rank to arrive enqueues, on every rank's stream, a wait for every rank's event, the R
+// device copies into that rank's recv, and an event; then every stream waits for every
+// other rank's copies, so no rank's stream runs past the collective before all rows have
+// landed everywhere (RCCL's completion semantics).  A rank that arrives earlier returns at
+// once inside a group (loop_group_start/end: one thread driving every rank) and otherwise
+// blocks on the host until the last rank has enqueued the copies (one thread per rank).
+struct LoopGroup {
+  int n = 0;
+  std::vector<int> dev;
+  std::vector<hipEvent_t> ready, done;
+  struct Slot {
+    const void* send = nullptr;
+    void* recv = nullptr;
+    hipStream_t s = nullptr;
+    bool in = false;
+  };
+  std::vector<Slot> slot;
+  size_t bytes = 0;
+  int arrived = 0, refs = 0, err = GPMDM_OK;
+  unsigned long long gen = 0;
+  std::string why;
+  std::mutex mu;
+  std::condition_variable cv;
+};
+struct LoopComm {
+  LoopGroup* g;
+  int rank;
+};
+
+static std::mutex g_loop_mu;
+static std::vector<LoopComm*> g_loop_live;   // the live loopback communicators
+static thread_local int t_loop_depth = 0;   // loop_group_start nesting on this thread
+static thread_local std::vector<std::pair<LoopGroup*, unsigned long long>> t_loop_pending;
+
+static LoopComm* as_loop(void* comm) {
+  std::lock_guard<std::mutex> lk(g_loop_mu);
+  for (LoopComm* c : g_loop_live)
+    if (c == comm) return c;
+  return nullptr;
+}
+
+// until collective `gen` of g has been enqueued by its last rank (120 s: an error, not a hang)
+static int loop_wait(LoopGroup& g, std::unique_lock<std::mutex>& lk, unsigned long long gen) {
+  if (!g.cv.wait_for(lk, std::chrono::seconds(120), [&] { return g.gen != gen; }))
+    return fail(GPMDM_E_STATE, "loopback all-gather: not every rank joined the collective within 120 s");
+  return g.err == GPMDM_OK ? GPMDM_OK : fail(g.err, g.why);
+}
+
+// the last rank's half: copies and completion edges on every rank's stream (lock held)
+static int loop_run(LoopGroup& g) {
+  auto hip = [&](hipError_t e, const char* what) {
+    if (e == hipSuccess) return GPMDM_OK;
+    g.why = std::string("loopback all-gather: ") + what + ": " + hipGetErrorString(e);
+    return GPMDM_E_HIP;
+  };
+  int rc = GPMDM_OK;
+  for (int j = 0; j < g.n && rc == GPMDM_OK; ++j) {
+    if ((rc = hip(hipSetDevice(g.dev[(size_t)j]), "hipSetDevice"))) break;
+    const LoopGroup::Slot& dj = g.slot[(size_t)j];
+    for (int k = 0; k < g.n && rc == GPMDM_OK; ++k)
+      rc = hip(hipStreamWaitEvent(dj.s, g.ready[(size_t)k], 0), "hipStreamWaitEvent");
+    for (int k = 0; k < g.n && rc == GPMDM_OK && g.bytes; ++k)
+      rc = hip(hipMemcpyAsync(static_cast<char*>(dj.recv) + (size_t)k * g.bytes, g.slot[(size_t)k].send, g.bytes,
+                              hipMemcpyDefault, dj.s),
+               "hipMemcpyAsync");
+    if (rc == GPMDM_OK) rc = hip(hipEventRecord(g.done[(size_t)j], dj.s), "hipEventRecord");
+  }
+  for (int j = 0; j < g.n && rc == GPMDM_OK; ++j) {
+    if ((rc = hip(hipSetDevice(g.dev[(size_t)j]), "hipSetDevice"))) break;
+    for (int k = 0; k < g.n && rc == GPMDM_OK; ++k)
+      if (k != j) rc = hip(hipStreamWaitEvent(g.slot[(size_t)j].s, g.done[(size_t)k], 0), "hipStreamWaitEvent");
+  }
+  return rc;
+}
+
+static int loop_all_gather(LoopComm* c, const void* send, void* recv, size_t bytes, hipStream_t s) {
+  LoopGroup& g = *c->g;
+  int cur = 0;
+  HIPCHK(hipGetDevice(&cur));
+  std::unique_lock<std::mutex> lk(g.mu);
+  LoopGroup::Slot& me = g.slot[(size_t)c->rank];
+  if (me.in) return fail(GPMDM_E_STATE, "loopback all-gather: a rank entered a collective twice");
+  if (g.arrived > 0 && bytes != g.bytes) return fail(GPMDM_E_INVALID, "loopback all-gather: ranks differ in size");
+  g.bytes = bytes;
+  HIPCHK(hipSetDevice(g.dev[(size_t)c->rank]));
+  HIPCHK(hipEventRecord(g.ready[(size_t)c->rank], s));
+  me = {send, recv, s, true};
+  const unsigned long long gen = g.gen;
+  if (++g.arrived == g.n) {
+    g.err = loop_run(g);
+    for (auto& sl : g.slot) sl = LoopGroup::Slot{};
+    g.arrived = 0;
+    ++g.gen;
+    g.cv.notify_all();
+    (void)hipSetDevice(cur);
+    return g.err == GPMDM_OK ? GPMDM_OK : fail(g.err, g.why);
+  }
+  (void)hipSetDevice(cur);
+  if (t_loop_depth > 0) {
+    t_loop_pending.emplace_back(&g, gen);
+    return GPMDM_OK;
+  }
+  return loop_wait(g, lk, gen);
+}
+
+static void loop_group_start() { ++t_loop_depth; }
+
+static int loop_group_end() {
+  if (t_loop_depth > 0 && --t_loop_depth > 0) return GPMDM_OK;
+  std::vector<std::pair<LoopGroup*, unsigned long long>> pend;
+  pend.swap(t_loop_pending);
+  int rc = GPMDM_OK;
+  for (auto& [g, gen] : pend) {
+    std::unique_lock<std::mutex> lk(g->mu);
+    const int r = loop_wait(*g, lk, gen);
+    if (rc == GPMDM_OK) rc = r;
+  }
+  return rc;
+}
+
+static void loop_unref(LoopGroup* g) {
+  bool last = false;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    last = --g->refs == 0;
+  }
+  if (!last) return;
+  for (int k = 0; k < g->n; ++k) {
+    (void)hipSetDevice(g->dev[(size_t)k]);
+    if (g->ready[(size_t)k]) (void)hipEventDestroy(g->ready[(size_t)k]);
+    if (g->done[(size_t)k]) (void)hipEventDestroy(g->done[(size_t)k]);
+  }
+  delete g;
+}
+
+// ---- the exchange's collectives, through RCCL or the loopback ------------------------------
+
 // rows [0, pad) of every rank's send buffer -> recv (even shards) or the staging buffer
 // (uneven shards), on cstream: the collective only (inside an ncclGroupStart/End a
 // host-driven copy would be enqueued before the grouped collective itself)
 static int gather_rows(gpmdm_pf* pf, const double* send, double* recv, double* stage, int width) {
   const size_t cnt = (size_t)pf->pad * width;
+  if (pf->comm_loop)
+    return loop_all_gather(reinterpret_cast<LoopComm*>(pf->comm), send, pf->padded ? stage : recv,
+                           sizeof(double) * cnt, pf->cstream);
   const ncclResult_t r = rccl().AllGather(send, pf->padded ? stage : recv, cnt, ncclDouble, pf->comm, pf->cstream);
   if (r != ncclSuccess) return nccl_fail(r, "ncclAllGather");
   return GPMDM_OK;
@@ -141,15 +289,24 @@ int propagate_exchange(gpmdm_pf* pf, const double* zh, const double* normals, hi
 // One stage's all-gathers of every rank's filter driven by this thread, grouped (a single
 // thread that drives several ranks must group their collectives), then the copy-downs.
 static int group_gather(gpmdm_pf* const* pfs, int n, bool states) {
-  ncclResult_t e = rccl().GroupStart();
-  if (e != ncclSuccess) return nccl_fail(e, "ncclGroupStart");
+  const bool loop = pfs[0]->comm_loop;
+  ncclResult_t e = ncclSuccess;
+  if (loop)
+    loop_group_start();
+  else if ((e = rccl().GroupStart()) != ncclSuccess)
+    return nccl_fail(e, "ncclGroupStart");
   int rc = GPMDM_OK;
   for (int i = 0; i < n && rc == GPMDM_OK; ++i) {
     gpmdm_pf* pf = pfs[i];
     rc = states ? gather_rows(pf, pf->xs_send, pf->xs_recv, pf->xs_stage, pf->m->d + 1)
                 : gather_rows(pf, pf->xl_send, pf->xl_recv, pf->xl_stage, 1);
   }
-  e = rccl().GroupEnd();
+  if (loop) {
+    const int r = loop_group_end();
+    if (rc == GPMDM_OK) rc = r;
+  } else {
+    e = rccl().GroupEnd();
+  }
   if (rc != GPMDM_OK) return rc;
   if (e != ncclSuccess) return nccl_fail(e, "ncclGroupEnd");
   for (int i = 0; i < n; ++i) {
@@ -244,11 +401,13 @@ extern "C" {
 int gpmdm_pf_propagate_multi(gpmdm_pf_t* pfs, int n, const double* zh, const double* normals,
                              void* const* streams) {
   CHECK(pfs && zh && streams && n >= 1, "null argument");
-  RCCL_OR_FAIL();
+  CHECK(pfs[0], "null handle");
+  if (!pfs[0]->comm_loop) RCCL_OR_FAIL();
   for (int i = 0; i < n; ++i) {
     gpmdm_pf* pf = pfs[i];
     CHECK(pf, "null handle");
     CHECK(pf->comm, "gpmdm_pf_propagate_multi needs every filter's communicator (gpmdm_pf_set_comm)");
+    CHECK(pf->comm_loop == pfs[0]->comm_loop, "gpmdm_pf_propagate_multi: every filter's communicator of one kind");
     CHECK(pf->n_ranks == n && pf->rank == i, "filter i must be rank i of n");
     if (!pf->switched || pf->preswitched) return fail(GPMDM_E_STATE, "propagate called before switch");
     if (pf->rng_mode == GPMDM_RNG_REPLAY) CHECK(normals, "replay mode needs the dynamics normals");
@@ -279,15 +438,22 @@ int gpmdm_pf_set_comm(gpmdm_pf_t pf, void* rccl_comm, int flags) {
   pf->release_comm();
   if (!rccl_comm) return GPMDM_OK;
   CHECK(pf->F == 1, "filter banks shard filters, not particles: no communicator");
-  RCCL_OR_FAIL();
   ncclComm_t comm = (ncclComm_t)rccl_comm;
   int n = 0, r = 0, dev = -1;
-  ncclResult_t e = rccl().CommCount(comm, &n);
-  if (e != ncclSuccess) return nccl_fail(e, "ncclCommCount");
-  e = rccl().CommUserRank(comm, &r);
-  if (e != ncclSuccess) return nccl_fail(e, "ncclCommUserRank");
-  e = rccl().CommCuDevice(comm, &dev);
-  if (e != ncclSuccess) return nccl_fail(e, "ncclCommCuDevice");
+  LoopComm* lc = as_loop(rccl_comm);
+  if (lc) {
+    n = lc->g->n;
+    r = lc->rank;
+    dev = lc->g->dev[(size_t)r];
+  } else {
+    RCCL_OR_FAIL();
+    ncclResult_t e = rccl().CommCount(comm, &n);
+    if (e != ncclSuccess) return nccl_fail(e, "ncclCommCount");
+    e = rccl().CommUserRank(comm, &r);
+    if (e != ncclSuccess) return nccl_fail(e, "ncclCommUserRank");
+    e = rccl().CommCuDevice(comm, &dev);
+    if (e != ncclSuccess) return nccl_fail(e, "ncclCommCuDevice");
+  }
   CHECK(n == pf->n_ranks && r == pf->rank, "communicator size/rank differ from the filter's n_ranks/rank");
   CHECK(dev == pf->m->device, "communicator is on another device than the model");
   const int d = pf->m->d;
@@ -312,6 +478,7 @@ int gpmdm_pf_set_comm(gpmdm_pf_t pf, void* rccl_comm, int flags) {
     if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
       return fail_out(fail(GPMDM_E_HIP, "communicator events"));
   pf->comm = comm;
+  pf->comm_loop = lc != nullptr;
   return GPMDM_OK;
 }
 
@@ -350,8 +517,48 @@ int gpmdm_comm_init_all(int n, const int* devices, void** comms) {
   return GPMDM_OK;
 }
 
+int gpmdm_comm_init_loopback(int n, const int* devices, void** comms) {
+  CHECK(n >= 1 && devices && comms, "bad argument");
+  int cur = 0;
+  HIPCHK(hipGetDevice(&cur));
+  auto* g = new LoopGroup();
+  g->n = n;
+  g->dev.assign(devices, devices + n);
+  g->ready.assign((size_t)n, nullptr);
+  g->done.assign((size_t)n, nullptr);
+  g->slot.assign((size_t)n, LoopGroup::Slot{});
+  g->refs = n;
+  for (int k = 0; k < n; ++k) {
+    if (hipSetDevice(devices[k]) != hipSuccess ||
+        hipEventCreateWithFlags(&g->ready[(size_t)k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g->done[(size_t)k], hipEventDisableTiming) != hipSuccess) {
+      g->refs = 1;
+      loop_unref(g);
+      (void)hipSetDevice(cur);
+      return fail(GPMDM_E_HIP, "loopback communicator: device / events");
+    }
+  }
+  (void)hipSetDevice(cur);
+  std::lock_guard<std::mutex> lk(g_loop_mu);
+  for (int k = 0; k < n; ++k) {
+    auto* c = new LoopComm{g, k};
+    g_loop_live.push_back(c);
+    comms[k] = c;
+  }
+  return GPMDM_OK;
+}
+
 int gpmdm_comm_destroy(void* comm) {
   if (!comm) return GPMDM_OK;
+  if (LoopComm* lc = as_loop(comm)) {
+    {
+      std::lock_guard<std::mutex> lk(g_loop_mu);
+      g_loop_live.erase(std::find(g_loop_live.begin(), g_loop_live.end(), lc));
+    }
+    loop_unref(lc->g);
+    delete lc;
+    return GPMDM_OK;
+  }
   RCCL_OR_FAIL();
   const ncclResult_t e = rccl().CommDestroy((ncclComm_t)comm);
   return e == ncclSuccess ? GPMDM_OK : nccl_fail(e, "ncclCommDestroy");

@@ -424,6 +424,7 @@ struct gpmdm_pf {
   // shards are uneven (or GPMDM_COMM_PAD_ROWS asks for it) the gather lands in *_stage and
   // each rank's rows are copied down to their shard offset.
   ncclComm_t comm = nullptr;
+  bool comm_loop = false;            // comm is an in-process loopback communicator (tests)
   hipStream_t cstream = nullptr;
   hipEvent_t cev[3] = {nullptr, nullptr, nullptr};
   long long pad = 0;
@@ -442,6 +443,7 @@ struct gpmdm_pf {
     if (cstream) (void)hipStreamDestroy(cstream);
     cstream = nullptr;
     comm = nullptr;                    // the caller owns the communicator
+    comm_loop = false;
   }
   // Pre-switch (Philox filters): the next frame's class switch needs no host input (its
   // draws are keyed by the frame counter), so the resample launches it right behind the

@@ -149,3 +149,35 @@ class RcclComm:
         if self.ptr:
             _lib.check(_lib.load().gpmdm_comm_destroy(self.ptr), "gpmdm_comm_destroy")
             self.ptr = None
+
+
+class LoopbackComms:
+    """TEST ONLY: the library's in-process loopback communicators (gpmdm_comm_init_loopback),
+    ``comms[r]`` = rank r of ``len(devices)`` on ``devices[r]`` (a device may repeat).  They
+    take the place of RCCL communicators in ``GPMDM_PF.set_comm``: R filters of
+    ``shard=(R, r)``, each stepped on a thread of its own, run the library's exchange among
+    themselves in this process.  ``destroy()`` after the filters using them."""
+
+    def __init__(self, devices):
+        import ctypes
+        from . import _lib
+        devs = [int(x) for x in devices]
+        n = len(devs)
+        out = (ctypes.c_void_p * n)()
+        _lib.check(_lib.load().gpmdm_comm_init_loopback(n, (ctypes.c_int * n)(*devs), out),
+                   "gpmdm_comm_init_loopback")
+        self.ptrs = [int(p) for p in out]
+        self.devices = devs
+
+    def __getitem__(self, r: int) -> int:
+        return self.ptrs[r]
+
+    def __len__(self) -> int:
+        return len(self.ptrs)
+
+    def destroy(self) -> None:
+        from . import _lib
+        for p in self.ptrs:
+            if p:
+                _lib.check(_lib.load().gpmdm_comm_destroy(p), "gpmdm_comm_destroy")
+        self.ptrs = []

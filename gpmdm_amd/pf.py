@@ -22,7 +22,9 @@ every per-frame computation runs in the HIP library.  Extra keyword options:
   (``gpmdm_comm_init_all``), and per frame every rank's stages with their all-gathers grouped
   (``gpmdm_pf_propagate_multi``); rank r owns ``device_shard_plan``'s particle range.  The
   read-outs and exports come from rank 0 (the filter is replicated).  ``devices=[0]`` is the
-  plain filter bit for bit;
+  plain filter bit for bit.  ``transport='loopback'`` (tests) swaps RCCL for the library's
+  in-process loopback communicators (``gpmdm_comm_init_loopback``), which also accept a
+  device repeated, e.g. ``devices=[0] * 8``: the multi-rank exchange on one GPU;
 * ``shard=(world, rank)``: sharding with a caller-driven exchange (``exchange=`` or the
   staged calls); a Philox filter then needs an explicit ``seed`` (nothing to broadcast).
   ``exchange(recv, send)`` is called twice per frame: with the (P x (d+1)) / (P_r x (d+1))
@@ -65,14 +67,15 @@ from .model import GPMDM
 PARALLEL_REPLAY_P = 16384
 
 
-def device_shard_plan(P: int, devices) -> list:
+def device_shard_plan(P: int, devices, repeat: bool = False) -> list:
     """(device, rank, lo, hi) of a one-process multi-device filter (GPMDM_PF(devices=...)):
     rank r runs on devices[r] and owns particles [r P / R, (r + 1) P / R) -- the library's
-    own shard rule (gpmdm_pf_create), so the filter is bitwise the one-rank filter's."""
+    own shard rule (gpmdm_pf_create), so the filter is bitwise the one-rank filter's.
+    ``repeat``: a device may hold several ranks (the loopback transport; tests)."""
     devs = [int(x) for x in devices]
     if not devs:
         raise ValueError("devices must name at least one GPU")
-    if len(set(devs)) != len(devs):
+    if not repeat and len(set(devs)) != len(devs):
         raise ValueError(f"devices must be distinct (one rank per GPU; RCCL refuses two on one device): {devs}")
     if any(x < 0 for x in devs):
         raise ValueError(f"bad device index in {devs}")
@@ -92,7 +95,7 @@ class GPMDM_PF:
     def __init__(self, gpmdm: GPMDM, markov_switching_model, num_particles: int, *,
                  rng: str = "torch", seed=None, resample: str = "multinomial", process_group=None,
                  shard=None, exchange=None, dedup: bool = True, shard_order: bool = True,
-                 dyn_tiles: str = "auto", devices=None, obs_cutoff: bool = False):
+                 dyn_tiles: str = "auto", devices=None, obs_cutoff: bool = False, transport: str = "rccl"):
         self._gpmdm = gpmdm
         self._gpmdm.set_evaluation_mode()
         self._markov_switching_model = torch.as_tensor(markov_switching_model).type(self.dtype)
@@ -114,7 +117,10 @@ class GPMDM_PF:
         if devices is not None:                 # one process, one handle per device (device_shard_plan)
             if process_group is not None or shard is not None or exchange is not None:
                 raise ValueError("devices= drives every rank itself: no process_group, shard or exchange")
-            self._devices = [p[0] for p in device_shard_plan(self._num_particles, devices)]
+            if transport not in ("rccl", "loopback"):
+                raise ValueError("transport must be 'rccl' or 'loopback'")
+            self._devices = [p[0] for p in device_shard_plan(self._num_particles, devices,
+                                                             repeat=transport == "loopback")]
             self._world, self._rank = len(self._devices), 0
         elif process_group is not None:
             import torch.distributed as dist
@@ -171,9 +177,12 @@ class GPMDM_PF:
             self._h, self._dev_index = hs[0], self._devices[0]
             self._peers = list(zip(hs[1:], self._devices[1:]))
             # one communicator per device, made together (ncclCommInitAll); rank r on devices[r]
+            # (transport='loopback': the library's in-process test transport, several ranks
+            # per device allowed -- gpmdm_comm_init_loopback)
             n = len(self._devices)
             comms = (ctypes.c_void_p * n)()
-            _lib.check(lib.gpmdm_comm_init_all(n, (ctypes.c_int * n)(*self._devices), comms), "gpmdm_comm_init_all")
+            init = lib.gpmdm_comm_init_loopback if transport == "loopback" else lib.gpmdm_comm_init_all
+            _lib.check(init(n, (ctypes.c_int * n)(*self._devices), comms), "gpmdm_comm_init")
             self._comms = [ctypes.c_void_p(c) for c in comms]
             for h, c in zip(hs, self._comms):
                 _lib.check(lib.gpmdm_pf_set_comm(h, c, 0), "set_comm")

@@ -260,6 +260,17 @@ int gpmdm_comm_destroy(void* comm);
  * host arrays for every rank (the filter is replicated).  RCCL is resolved at run time
  * (librccl.so.1) by these and the calls above; GPMDM_E_HIP when it is missing. */
 int gpmdm_comm_init_all(int n, const int* devices, void** comms);
+
+/* TEST ONLY: n in-process loopback communicators, comms[i] = rank i of n on devices[i]
+ * (devices may repeat: R ranks on one GPU, which RCCL refuses).  They stand in for RCCL
+ * communicators everywhere above (gpmdm_pf_set_comm, gpmdm_pf_propagate_multi,
+ * gpmdm_comm_destroy): each all-gather is R x R stream-ordered device copies made when the
+ * last rank joins, with RCCL's completion semantics (no rank's stream passes the collective
+ * before every rank's rows have landed).  Ranks joined by one thread inside
+ * gpmdm_pf_propagate_multi are grouped; ranks on threads of their own block on the host in
+ * each collective until all have joined (an error after 120 s).  Not a transport for
+ * production: every byte goes through this process's device copies. */
+int gpmdm_comm_init_loopback(int n, const int* devices, void** comms);
 int gpmdm_pf_propagate_multi(gpmdm_pf_t* pfs, int n, const double* z, const double* normals,
                              void* const* streams);
 
