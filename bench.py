@@ -76,12 +76,14 @@ METRIC = "particle-steps/sec (P×timesteps) + achieved HBM GB/s, N=2000 D=62 d=3
 FP64_MFMA_PEAK_TFLOPS = 78.6          # MI355X spec (dense FP64 matrix); measured 77.1 (profiles/)
 # The reference's only published throughput for this path: P = 100 particles
 # at 12.78 frames/s on the author's laptop CPU (test_gpmdm_pf.ipynb:79, 259-260).  It is the
-# notebook's own configuration, not configs[1]'s N/P; vs_baseline divides by it and says so.
+# notebook's own configuration, not configs[1]'s N/P, so it is NOT this metric's baseline:
+# vs_baseline stays null and the figure is reported beside the line (published_reference);
+# cpu_baseline is the same-box, same-configuration comparison.
 PUBLISHED_PARTICLE_STEPS = 100 * 12.78
-PUBLISHED_BASIS = ("value / 1.278e3 particle-steps/s: the reference's published frame rate (12.78 FPS x P=100, "
-                   "author's laptop CPU, test_gpmdm_pf.ipynb:259-260; BASELINE.md §1) -- the only published "
-                   "throughput for this path, quoted at the notebook's own model and P, not configs[1]'s; "
-                   "cpu_baseline is the same-box comparison")
+PUBLISHED_BASIS = ("the reference's published frame rate, 12.78 FPS x P=100 = 1.278e3 particle-steps/s "
+                   "(author's laptop CPU, test_gpmdm_pf.ipynb:259-260; BASELINE.md §1), quoted at the "
+                   "notebook's own model (N=500) and P=100, not configs[1]'s: a different workload, so no "
+                   "vs_baseline; cpu_baseline is the same-box comparison on this configuration")
 # per-GPU particles: configs 4 and 5 are quoted on 8 GPUs
 P_PER_GPU = {1: 100, 2: 100_000, 3: 100_000, 4: 125_000, 5: 125_000}
 WORKLOAD = None
@@ -426,6 +428,75 @@ def cutoff_line(model, T, P, zs, warmup, steps, headline_ms=None, headline_obs_m
                    "rounding "
                    "(tests/test_gpu_obs_cutoff.py)"}
     return out
+
+
+def cutoff_spread_line(model, T, P, zs, spreads=(0.05, 0.2, 0.5), n_anc=2000, reps=4):
+    """The cutoff on clouds that are NOT one ancestor: n_anc distinct training
+    latents as ancestors (each with its class), P / n_anc particles around each, offset by
+    spread x the observation GP's lengthscale x N(0, 1) per coordinate, contiguous per ancestor
+    (a resampled cloud's order).  Per spread: the dense filter and the cutoff filter load the
+    same cloud (load_state) and run the same Philox step (same frame: same draws) ``reps``
+    times, each from the loaded cloud again; the observation launch is event-timed, then one
+    more step from the same cloud counts the cutoff's MFMA groups (gpmdm.py:923-963 either
+    way; the cutoff's results equal the dense kernel's to rounding)."""
+    import torch
+    from gpmdm_amd import GPMDM_PF
+    model.enable_obs_cutoff(True)
+    X = model.X.detach().cpu().numpy()
+    N, d = X.shape
+    ell = np.exp(model.y_log_lengthscales.detach().cpu().numpy())
+    cls_of = np.concatenate([np.full(model.get_X_for_class(c).shape[0], c) for c in range(model.n_classes)])
+    g = np.random.RandomState(23)
+    anc = np.sort(g.choice(N, min(n_anc, N), replace=False))
+    g.shuffle(anc)                               # ancestors in no spatial order
+    owner = anc[(np.arange(P) * anc.size) // P]  # contiguous runs per ancestor
+    base = X[owner]
+    classes = cls_of[owner].astype(np.int64)
+    filt = {cut: GPMDM_PF(model, T, P, rng="philox", seed=11, obs_cutoff=cut) for cut in (False, True)}
+    rows = []
+    for sp in spreads:
+        states = np.ascontiguousarray(base + sp * ell[None, :] * g.randn(P, d))
+        r = {"spread_ell": sp, "distinct_ancestors": int(anc.size), "P": P}
+        for cut, pf in filt.items():
+            pf.stage_times()
+            ms = []
+            for k in range(reps + 1):
+                pf.load_state(states, classes, frame=7)
+                torch.cuda.synchronize()
+                if k > 0:                        # (the first step is a warm-up)
+                    pf.enable_timing(True, stages=("obs_gemm",))
+                pf.update(zs[7])
+                torch.cuda.synchronize()
+                if k > 0:
+                    pf.enable_timing(False)
+                    t, n = pf.stage_times()["obs_gemm"]
+                    ms.append(t / max(n, 1))
+            key = "cutoff" if cut else "dense"
+            r[f"{key}_obs_launch_ms"] = float(np.median(ms))
+            r[f"{key}_obs_launch_ms_all"] = [round(x, 4) for x in ms]
+            if not cut:
+                w = pf.export_state()["w"]
+                r["ess_fraction"] = float(1.0 / np.sum(w * w) / P)
+            else:
+                pf.load_state(states, classes, frame=7)
+                pf.set_obs_cutoff(True, stats=True)
+                pf.obs_cutoff_stats(reset=True)
+                pf.update(zs[7])
+                st = pf.obs_cutoff_stats()
+                pf.set_obs_cutoff(True, stats=False)
+                r["mfma_groups_run_fraction"] = st["fraction_run"]
+                flop = st["run"] * 16 * 16 * 16 * 2
+                r["executed_tflops"] = flop / (r["cutoff_obs_launch_ms"] * 1e-3) / 1e12
+                r["executed_frac_of_peak"] = r["executed_tflops"] / FP64_MFMA_PEAK_TFLOPS
+        r["obs_speedup"] = r["dense_obs_launch_ms"] / r["cutoff_obs_launch_ms"]
+        rows.append(r)
+        log(f"[bench] cutoff spread {sp}: {json.dumps(r)}")
+    return {"rows": rows,
+            "note": "clouds of distinct_ancestors training latents (their classes) with P/n particles each, "
+                    "offset by spread_ell x l_y x N(0,1); dense and cutoff filters run the same Philox step "
+                    "from the same loaded cloud; obs launch = median over the timed repeats (HIP events on the "
+                    "launch stream); mfma_groups_run_fraction counted by the cutoff kernel on one more step "
+                    "from the same cloud; executed_tflops = groups x 8192 FLOP / the cutoff launch time"}
 
 
 def nodedup_line(model, T, P_total, group, dist, device, zs, steps, rng, dyn_tiles="auto"):
@@ -829,6 +900,9 @@ def main():
     ap.add_argument("--cutoff-steps", type=int, default=None,
                     help="frames of the observation-GP cutoff line (obs_cutoff=True; configs 2, 3, 5 on one GPU: "
                          "default 20, 0 = off)")
+    ap.add_argument("--cutoff-spread", action="store_true",
+                    help="only the cutoff-vs-dense observation launch on spread clouds of >= 1000 ancestors "
+                         "(cutoff_spread_line; one GPU), one JSON line with its rows; not a headline run")
     ap.add_argument("--dyn-tiles", default="auto", choices=("auto", "narrow", "wide"),
                     help="dynamics tile shape of the headline filter (gpmdm_pf_set_dyn_tiles)")
     argv = sys.argv[1:]
@@ -920,6 +994,16 @@ def main():
         zs, stream_check = predictive_stream(new_filter(), model, args.warmup + args.steps + n_breakdown)
     else:
         zs = data.observation_stream(n_frames, seed=1)
+    if args.cutoff_spread:
+        if world > 1:
+            log("[bench] --cutoff-spread runs on one GPU")
+            sys.exit(2)
+        res = cutoff_spread_line(model, T, P_total, zs)
+        print(json.dumps({"metric": "observation launch ms, dense vs cutoff, spread clouds",
+                          "config": {"workload": f"configs[{WORKLOAD['cfg'] - 1}]", "N": int(model.X.shape[0]),
+                                     "D": WORKLOAD["D"], "d": WORKLOAD["d"], "C": WORKLOAD["C"], "P": P_total},
+                          "cutoff_spread": res}), flush=True)
+        return
     pf = new_filter()
     log(f"[bench] rank {rank}/{world} setup {time.perf_counter() - t_setup:.1f}s, P_total={P_total}")
 
@@ -1051,8 +1135,9 @@ def main():
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": P_total * args.steps / elapsed / PUBLISHED_PARTICLE_STEPS,
-        "vs_baseline_basis": PUBLISHED_BASIS,
+        "vs_baseline": None,
+        "published_reference": {"value": PUBLISHED_PARTICLE_STEPS, "unit": "particle-steps/s",
+                                "basis": PUBLISHED_BASIS},
         "dtype": "f64",
         "data": "synthetic (SURVEY §8(d) generator; random-phase sinusoid mocap surrogate, PCA latents)",
         "config": {"workload": f"configs[{WORKLOAD['cfg'] - 1}]: N={N} D={D} d={d} C={model.n_classes}, "

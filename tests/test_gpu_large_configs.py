@@ -24,6 +24,8 @@ gpmdm.py:923-963, 1032-1068; gpmdm_pf.py:137-262):
   single-rank Philox step at P = 10^6 against the oracle (classes exact, ll and states on a
   random subset, every resample index, read-outs).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -45,9 +47,21 @@ def _synthetic(cfg):
     return _MODELS[cfg]
 
 
+def _progress(msg):
+    """A line on stdout (seen with -s) and in gpurun_out/progress.log: long host-side oracle
+    work must not look like a hung GPU command."""
+    import os
+    import time
+    print(f"[{time.strftime('%H:%M:%S')}] {msg}", flush=True)
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/progress.log", "a") as fh:
+        fh.write(f"{time.time():.1f} {msg}\n")
+
+
 def _build_synthetic(cfg):
     from gpmdm_amd import GPMDM, synthetic
     from oracle import gpmdm_oracle as O
+    _progress(f"building config {cfg} (device model + Cholesky oracle)")
     c = synthetic.CONFIGS[cfg]
     data = synthetic.make_sequences(c["C"], c["S"], c["L"], c["D"], c["d"], seed=0)
     hp = synthetic.default_hyperparameters(c["D"], c["d"], 0.1)
@@ -61,6 +75,7 @@ def _build_synthetic(cfg):
                     "x_log_lambdas", "x_log_sigma_n", "x_log_lin_coeff")}
     om = O.OracleModel(X=m.X.detach().numpy().copy(), Y=m.get_Y().astype(np.float64),
                        seq_lengths=[[c["L"]] * c["S"]] * c["C"], **lp).precompute("cholesky")
+    _progress(f"config {cfg} built")
     return m, om, data, c
 
 
@@ -233,7 +248,71 @@ def _philox_step_vs_oracle(m, om, T, P, seed, z_warm, z, what, sub_n=2000, **pf_
     assert nrel(pf.current_state_mean().numpy(), O.current_state_mean(post["states"], post["w"])) < 1e-6, what
     assert abs(pf.log_likelihood() - O.log_likelihood_readout(post["ll"], post["log_w"])) <= 1e-9 * pf.log_likelihood()
     assert pf.health() == {k: 0 for k in pf.health()}, what
-    return pf, post
+    return pf, post, pre, frame
+
+
+def _full_cloud_vs_oracle(om, T, pre, post, pf, seed, frame, z, what, chunk=8192):
+    """The same resynced Philox step evaluated by the oracle for EVERY particle (VERDICT r5
+    #3: independent of the GPU's own outputs): the oracle's switch, dynamics GP, observation
+    GP (Cholesky solves, chunks of ``chunk`` particles), its own normalisation, its own
+    inverse-CDF resample with the restated uniforms and its own read-outs
+    (gpmdm_pf.py:137-262), against the device's:
+      * every particle's ll: 1e-5 normwise and 1e-5 of its terms' magnitude;
+      * every weight: 1e-5 normwise (BASELINE's figure);
+      * resample indices: the oracle's search of the ORACLE's weights; the slots whose ancestor
+        differs are counted (a 1e-6 weight difference moves a CDF boundary across a uniform
+        with probability ~1e-6 per slot) and held to <= 2;
+      * posterior (1e-5 abs), state mean (1e-5 normwise) and the likelihood read-out (1e-5
+        relative) from the oracle's own weights and ancestors.
+    Returns the check's figures (recorded in gpurun_out/full_cloud_oracle.json)."""
+    import json
+    import os
+    import time
+    from oracle import gpmdm_oracle as O
+    from oracle import philox as X
+    t0 = time.time()
+    P, C, d = post["ll"].shape[0], T.shape[0], pre["states"].shape[1]
+    cls1 = O.switch_classes(pre["classes"], T, X.switch_draws(seed, frame, P, C))
+    nrm = X.dynamics_normals(seed, frame, P, d)
+    st1 = np.empty((P, d))
+    for c in range(C):
+        idx_c = np.nonzero(cls1 == c)[0]
+        for i in range(0, idx_c.size, chunk):
+            sel = idx_c[i:i + chunk]
+            mu, var = om.map_x_dynamics_for_class(pre["states"][sel], c)
+            st1[sel] = nrm[sel] * np.sqrt(var) + mu
+        _progress(f"{what}: oracle dynamics, class {c} ({idx_c.size} particles)")
+    ll = np.empty(P)
+    terms = np.empty(P)
+    zz = np.asarray(z, dtype=np.float64)
+    for i in range(0, P, chunk):
+        mu_s, var_s = om.map_x_to_y(st1[i:i + chunk])
+        ll[i:i + chunk] = (-0.5 * np.sum((zz[None, :] - mu_s) ** 2 / var_s + np.log(var_s), axis=1)
+                           + np.sum(-np.log(np.sqrt(var_s)), axis=1) - O.loglik_const(zz.shape[0]))
+        terms[i:i + chunk] = (np.sum((zz[None, :] - mu_s) ** 2 / var_s + 2.0 * np.abs(np.log(var_s)), axis=1)
+                              + abs(O.loglik_const(zz.shape[0])))
+        _progress(f"{what}: oracle observation GP, particles [{i}, {min(P, i + chunk)})")
+    log_w, w = O.normalise(ll)
+    idx = O.multinomial_resample_indices(w, X.resample_uniforms(seed, frame, P))
+    post_o = O.class_probabilities(ll, log_w, cls1[idx], C)
+    mean_o = O.current_state_mean(st1[idx], w)
+    lik_o = O.log_likelihood_readout(ll, log_w)
+    fig = {"what": what, "P": P, "oracle_s": time.time() - t0,
+           "ll_nrel": nrel(post["ll"], ll), "ll_term_scaled": float(np.max(np.abs(post["ll"] - ll) / terms)),
+           "w_nrel": nrel(post["w"], w), "idx_mismatch": int(np.sum(post["resample_idx"] != idx)),
+           "posterior_abs": float(np.max(np.abs(pf.class_probabilities().numpy() - post_o))),
+           "mean_nrel": nrel(pf.current_state_mean().numpy(), mean_o),
+           "lik_rel": abs(pf.log_likelihood() - lik_o) / abs(lik_o),
+           "ess": float(1.0 / np.sum(w * w)), "posterior_oracle": post_o.tolist()}
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/full_cloud_oracle.json", "a") as fh:
+        fh.write(json.dumps(fig) + "\n")
+    assert np.array_equal(post["classes"], cls1[post["resample_idx"]]), what
+    assert fig["ll_nrel"] < 1e-5 and fig["ll_term_scaled"] < 1e-5, fig
+    assert fig["w_nrel"] < 1e-5, fig
+    assert fig["idx_mismatch"] <= 2, fig
+    assert fig["posterior_abs"] < 1e-5 and fig["mean_nrel"] < 1e-5 and fig["lik_rel"] < 1e-5, fig
+    return fig
 
 
 @pytest.mark.timeout(600)
@@ -262,6 +341,28 @@ def test_large_config_benchmarked_particles_vs_oracle(cfg):
     _philox_step_vs_oracle(m, om_t, T, P, 11, zs[0], zs[1], f"config {cfg} at P={P}")
 
 
+@pytest.mark.timeout(1200)
+@pytest.mark.parametrize("cfg", [3, pytest.param(5, marks=pytest.mark.skipif(
+    not os.environ.get("GPMDM_FULL_ORACLE_C5"),
+    reason="~5 min of host Cholesky solves (5e13 FLOP): opt-in, GPMDM_FULL_ORACLE_C5=1; "
+           "the run's figures are in profiles/r06/full_oracle/"))])
+def test_large_config_benchmarked_particles_full_oracle(cfg):
+    """configs[2] / [4] at the benchmarked P = 100k / 125k: the resynced step of
+    test_large_config_benchmarked_particles_vs_oracle, with the oracle evaluating every
+    particle and forming the read-outs from its own weights (_full_cloud_vs_oracle; ~1e13 /
+    5e13 FLOP of Cholesky solves on the host cores).  The posterior of this stream is
+    saturated (one class holds all the mass), so the figures that carry the check are every
+    particle's ll and weight; the read-outs are compared as well."""
+    from gpmdm_amd import synthetic
+    m, om, om_t, data, c = _synthetic(cfg)
+    T = synthetic.markov_matrix(c["C"])
+    zs = data.observation_stream(2, seed=1)
+    P = {3: 100_000, 5: 125_000}[cfg]
+    pf, post, pre, frame = _philox_step_vs_oracle(m, om_t, T, P, 11, zs[0], zs[1], f"config {cfg} at P={P}")
+    fig = _full_cloud_vs_oracle(om_t, T, pre, post, pf, 11, frame, zs[1], f"config {cfg} at P={P}, full cloud")
+    print(fig)
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("cfg", [3, 5])
 def test_large_config_cutoff_vs_oracle(cfg):
@@ -272,13 +373,17 @@ def test_large_config_cutoff_vs_oracle(cfg):
     from gpmdm_amd import synthetic
     m, om, om_t, data, c = _synthetic(cfg)
     m.enable_obs_cutoff(True)
-    assert m.obs_cutoff_tau > 0
-    T = synthetic.markov_matrix(c["C"])
-    zs = data.observation_stream(2, seed=1)
-    P = {3: 100_000, 5: 125_000}[cfg]
-    pf, _ = _philox_step_vs_oracle(m, om_t, T, P, 11, zs[0], zs[1], f"config {cfg} at P={P}, cutoff",
-                                   obs_cutoff=True)
-    pf.set_obs_cutoff(True, stats=True)
-    pf.update(zs[0])
-    st = pf.obs_cutoff_stats()
-    assert 0 < st["run"] < 0.5 * st["dense"], st
+    try:
+        assert m.obs_cutoff_tau > 0
+        T = synthetic.markov_matrix(c["C"])
+        zs = data.observation_stream(2, seed=1)
+        P = {3: 100_000, 5: 125_000}[cfg]
+        pf, *_ = _philox_step_vs_oracle(m, om_t, T, P, 11, zs[0], zs[1], f"config {cfg} at P={P}, cutoff",
+                                        obs_cutoff=True)
+        pf.set_obs_cutoff(True, stats=True)
+        pf.update(zs[0])
+        st = pf.obs_cutoff_stats()
+        assert 0 < st["run"] < 0.5 * st["dense"], st
+        del pf
+    finally:
+        m.enable_obs_cutoff(False)      #  the session-cached model goes back to dense only

@@ -272,3 +272,69 @@ def test_cutoff_far_cloud_has_no_reachable_kstep(m2c):
     # out of reach: only the mean tiles ran
     assert st["dense"] > 0 and st["run"] < 0.05 * st["dense"], st
     assert np.max(np.abs(a["ll"] - b["ll"]) / np.maximum(np.abs(a["ll"]), 1.0)) < 1e-12
+
+
+@pytest.fixture(scope="module", params=[5, 12])
+def synth_cut(request):
+    """Synthetic models at d = 5 (the 32 x 512 cutoff tile with the particle coordinates read
+    from LDS, d = 4..8) and d = 12 (the 8-wave 64 x 512 tile of 9 <= d <= 16), N = 3000."""
+    from conftest import synthetic_model
+    m, T, Y = synthetic_model(C=2, d=request.param, D=24, L=500, S=3, seed=31 + request.param)
+    return request.param, m, T, Y
+
+
+def test_cutoff_vs_dense_other_latent_dims(synth_cut):
+    """the cutoff kernel's d = 4..7 LDS-coordinate path and its 64-particle
+    instantiations (9 <= d <= 15) against the dense kernel from one state with the same draws:
+    classes exact, log-likelihoods and weights 1e-5 normwise (gpmdm.py:923-963,
+    gpmdm_pf.py:170-204), one step from each of two states of the dense filter's trajectory
+    (b is reloaded with a's state before each step: a flipped resampling index would otherwise
+    compare different clouds)."""
+    from gpmdm_amd import GPMDM_PF
+    d, m, T, Y = synth_cut
+    P = 5000
+    torch.manual_seed(3)
+    a = GPMDM_PF(m, T, P, rng="torch")
+    a.update(Y[40])
+    b = GPMDM_PF(m, T, P, rng="torch", obs_cutoff=True)
+    b.set_obs_cutoff(True, stats=True)
+    rng = np.random.RandomState(5)
+    for k in range(2):
+        st = a.export_state()
+        b.load_state(st["states"], st["classes"], ll=st["ll"], log_w=st["log_w"], w=st["w"],
+                     resample_idx=st["resample_idx"], frame=st.get("frame"))
+        E, nrm, u = rng.exponential(size=(P, 2)), rng.randn(P, d), rng.rand(P)
+        a.update_with_draws(Y[41 + k], E, nrm, u)
+        b.update_with_draws(Y[41 + k], E, nrm, u)
+        sa, sb = a.export_state(), b.export_state()
+        assert np.array_equal(sa["classes"], sb["classes"]), (d, k)
+        assert nrel(sb["ll"], sa["ll"]) < 1e-5, (d, k, nrel(sb["ll"], sa["ll"]))
+        assert nrel(sb["w"], sa["w"]) < 1e-5, (d, k, nrel(sb["w"], sa["w"]))
+    st = b.obs_cutoff_stats()
+    assert st["dense"] > 0 and 0 < st["run"] <= st["dense"], st
+
+
+def test_cutoff_logical_shards_other_latent_dims(synth_cut):
+    """4 logical shards of a d = 5 / d = 12 cutoff filter (another particle tiling) are bitwise
+    the one-rank cutoff filter over 3 frames."""
+    from gpmdm_amd import GPMDM_PF
+    d, m, T, Y = synth_cut
+    P, world = 6_007, 4
+    torch.manual_seed(4)
+    ref = GPMDM_PF(m, T, P, rng="philox", seed=91, obs_cutoff=True)
+    ranks = []
+    for r in range(world):
+        torch.manual_seed(4)
+        ranks.append(GPMDM_PF(m, T, P, rng="philox", seed=91, shard=(world, r), obs_cutoff=True))
+    for k in range(3):
+        z = np.ascontiguousarray(np.asarray(Y[60 + 3 * k], dtype=np.float64))
+        ref.update(z)
+        full = torch.cat([pf._stage_propagate(z) for pf in ranks], 0)
+        for pf in ranks:
+            pf._recv.copy_(full)
+            pf._stage_resample()
+        a = ref.export_state()
+        for pf in ranks:
+            b = pf.export_state()
+            for key in ("states", "classes", "ll", "resample_idx"):
+                assert np.array_equal(a[key], b[key]), (d, k, key)
