@@ -453,6 +453,7 @@ def cutoff_spread_line(model, T, P, zs, spreads=(0.05, 0.2, 0.5), n_anc=2000, re
     base = X[owner]
     classes = cls_of[owner].astype(np.int64)
     filt = {cut: GPMDM_PF(model, T, P, rng="philox", seed=11, obs_cutoff=cut) for cut in (False, True)}
+    zero, unif = np.zeros(P), np.full(P, 1.0 / P)   # the reference's initial weights (gpmdm_pf.py:100-104)
     rows = []
     for sp in spreads:
         states = np.ascontiguousarray(base + sp * ell[None, :] * g.randn(P, d))
@@ -461,7 +462,7 @@ def cutoff_spread_line(model, T, P, zs, spreads=(0.05, 0.2, 0.5), n_anc=2000, re
             pf.stage_times()
             ms = []
             for k in range(reps + 1):
-                pf.load_state(states, classes, frame=7)
+                pf.load_state(states, classes, ll=zero, log_w=zero, w=unif, frame=7)
                 torch.cuda.synchronize()
                 if k > 0:                        # (the first step is a warm-up)
                     pf.enable_timing(True, stages=("obs_gemm",))
@@ -478,7 +479,7 @@ def cutoff_spread_line(model, T, P, zs, spreads=(0.05, 0.2, 0.5), n_anc=2000, re
                 w = pf.export_state()["w"]
                 r["ess_fraction"] = float(1.0 / np.sum(w * w) / P)
             else:
-                pf.load_state(states, classes, frame=7)
+                pf.load_state(states, classes, ll=zero, log_w=zero, w=unif, frame=7)
                 pf.set_obs_cutoff(True, stats=True)
                 pf.obs_cutoff_stats(reset=True)
                 pf.update(zs[7])
