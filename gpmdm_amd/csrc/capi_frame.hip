@@ -461,7 +461,7 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
       const long long entries = (long long)ci.T_R + ci.T_M - 1;
       int n_split = cut_split_tiles(pf, tiles, slots, (size_t)entries * tiles * PT * sizeof(double));
       if (ci.T_R + ci.T_M <= TPC) n_split = 0;   // one chunk: nothing to split
-      if (n_split > 0) TRY(pf->ensure_cut_split((size_t)entries * n_split * PT, n_split));
+      if (n_split > 0) TRY(pf->ensure_cut_split((size_t)entries * n_split * PT, n_split, s));
       cp.n_whole = tiles - n_split;
       cp.n_split = n_split;
       cp.part = pf->cut_part;

@@ -141,7 +141,39 @@ struct gpmdm_model {
     obs_cut = CutImage{};
   }
 
+  // Lifecycle (DESIGN.md §1 "Lifecycle waits"): the filters built on the model --
+  // gpmdm_model_set_obs_cutoff waits for each one's own last frame (quiesce) before it
+  // replaces the cutoff image -- and one event per stream the predictive maps ran on, so the
+  // images' release at the last reference is ordered after those launches on the lifecycle
+  // stream (no device-wide wait either way).
+  std::mutex life_mu;
+  std::vector<gpmdm_pf*> users;
+  std::vector<std::pair<hipStream_t, hipEvent_t>> uses;
+  void add_user(gpmdm_pf* pf) {
+    std::lock_guard<std::mutex> lk(life_mu);
+    users.push_back(pf);
+  }
+  void remove_user(gpmdm_pf* pf) {
+    std::lock_guard<std::mutex> lk(life_mu);
+    users.erase(std::remove(users.begin(), users.end(), pf), users.end());
+  }
+  hipError_t note_use(hipStream_t s) {   // after a predictive map's launches on s
+    std::lock_guard<std::mutex> lk(life_mu);
+    for (auto& u : uses)
+      if (u.first == s) return hipEventRecord(u.second, s);
+    hipEvent_t ev = nullptr;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+    uses.emplace_back(s, ev);
+    return hipEventRecord(ev, s);
+  }
+
   ~gpmdm_model() {
+    (void)hipSetDevice(device);
+    if (hipStream_t life = life_stream(device)) {
+      for (auto& u : uses) (void)hipStreamWaitEvent(life, u.second, 0);
+    }
+    for (auto& u : uses) (void)hipEventDestroy(u.second);
     obs.release();
     obs_small.release();
     for (auto& g : dyn) g.release();
@@ -216,15 +248,16 @@ struct gpmdm_pf {
   size_t cut_part_cap = 0;
   int2* cut_split = nullptr;
   int cut_split_cap = 0;
-  int ensure_cut_split(size_t n_part, int n_split) {
+  // (grown inside a frame: the old buffers are released after the frame stream's earlier work)
+  int ensure_cut_split(size_t n_part, int n_split, hipStream_t s) {
     if (n_part > cut_part_cap) {
-      dfree(cut_part);
+      dfree_after(cut_part, s);
       cut_part_cap = 0;
       if (dalloc(&cut_part, n_part)) return fail(GPMDM_E_NOMEM, "cutoff split partials");
       cut_part_cap = n_part;
     }
     if (n_split > cut_split_cap) {
-      dfree(cut_split);
+      dfree_after(cut_split, s);
       cut_split_cap = 0;
       if (dalloc(&cut_split, (size_t)n_split)) return fail(GPMDM_E_NOMEM, "cutoff split table");
       cut_split_cap = n_split;
@@ -527,7 +560,9 @@ struct gpmdm_pf {
   const int* own_order() const { return own_valid ? own : nullptr; }
 
   ~gpmdm_pf() {
-    if (preswitched) (void)hipDeviceSynchronize();   // a pre-switch may still use the buffers
+    // (gpmdm_pf_destroy has waited for the filter's own work: quiesce, capi_pf.hip; a handle
+    // deleted by a failed create has launched nothing)
+    if (m) (void)hipSetDevice(m->device);
     if (up_stream) (void)hipStreamSynchronize(up_stream);
     release_comm();
     double* ds[] = {T, X, X_prop, ll, qdyn, mudyn, qobs, sobs, z, E, normals, U,
@@ -548,11 +583,11 @@ struct gpmdm_pf {
     dfree(health);
     for (auto& r : recs) { pool.push_back(r.a); pool.push_back(r.b); }
     for (auto ev : pool) (void)hipEventDestroy(ev);
-    if (rpin) (void)hipHostFree(rpin);
-    if (cnt_pin) (void)hipHostFree(cnt_pin);
-    if (cseq_pin) (void)hipHostFree(cseq_pin);
-    if (rows_pin) (void)hipHostFree(rows_pin);
-    if (cls_pin) (void)hipHostFree(cls_pin);
+    hfree(rpin);
+    hfree(cnt_pin);
+    hfree(cseq_pin);
+    hfree(rows_pin);
+    hfree(cls_pin);
     if (cls_ev) (void)hipEventDestroy(cls_ev);
     if (cnt_ev) (void)hipEventDestroy(cnt_ev);
     if (sw_ev) (void)hipEventDestroy(sw_ev);
@@ -561,16 +596,17 @@ struct gpmdm_pf {
     if (up_ev) (void)hipEventDestroy(up_ev);
     if (ndev_ev) (void)hipEventDestroy(ndev_ev);
     if (up_stream) (void)hipStreamDestroy(up_stream);
-    if (ro_pin) (void)hipHostFree(ro_pin);
-    if (seq_pin) (void)hipHostFree(seq_pin);
+    hfree(ro_pin);
+    hfree(seq_pin);
     for (int k = 0; k < 2; ++k) {
-      if (zpin[k]) (void)hipHostFree(zpin[k]);
+      hfree(zpin[k]);
       if (zev[k]) (void)hipEventDestroy(zev[k]);
     }
     for (int k = 0; k < 3; ++k) {
-      if (rep_pin[k]) (void)hipHostFree(rep_pin[k]);
+      hfree(rep_pin[k]);
       if (rep_ev[k]) (void)hipEventDestroy(rep_ev[k]);
     }
+    if (m) m->remove_user(this);
     model_release(m);
   }
 
@@ -602,6 +638,7 @@ ResampleArgs resample_args(gpmdm_pf* pf);
 NormArgs norm_args(gpmdm_pf* pf);
 int flush_ll(gpmdm_pf* pf, hipStream_t s);
 int drop_preswitch(gpmdm_pf* pf, hipStream_t s, bool host_wait);
+int quiesce(gpmdm_pf* pf);
 int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipStream_t s, bool order_ahead = false, bool counts_ahead = false, bool e_uploaded = false);
 int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s, bool zstage = false);
 int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s);

@@ -18,10 +18,32 @@ int fail(int code, const std::string& msg) {
 
 namespace gpmdm::capi {
 
+// host -> device on the current device's lifecycle stream (memory.hip): not ordered behind the
+// legacy null stream's users
+static int h2d(void* dst, const void* src, size_t bytes) {
+  hipStream_t ls = life_stream_current();
+  CHECK(ls, "the library's lifecycle stream");
+  HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ls));
+  HIPCHK(hipStreamSynchronize(ls));
+  return GPMDM_OK;
+}
+
 template <typename T>
 int upload(T** dst, const std::vector<T>& v) {
   TRY(dalloc(dst, v.size()));
-  HIPCHK(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return h2d(*dst, v.data(), v.size() * sizeof(T));
+}
+
+// Wait for the last frame of every filter built on the model (not for the device): the
+// caller guarantees none of them is inside a frame or stepping on another thread.
+static int quiesce_users(gpmdm_model* m) {
+  std::vector<gpmdm_pf*> us;
+  {
+    std::lock_guard<std::mutex> lk(m->life_mu);
+    us = m->users;
+  }
+  for (gpmdm_pf* pf : us) TRY(quiesce(pf));
+  HIPCHK(hipSetDevice(m->device));
   return GPMDM_OK;
 }
 
@@ -47,7 +69,7 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
   for (int J = 0; J < g.n_j; ++J) {
     buf.assign((size_t)pk.block_doubles(J), 0.0);
     pk.pack_block(J, buf.data());
-    HIPCHK(hipMemcpy(g.Bf + off, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice));
+    TRY(h2d(g.Bf + off, buf.data(), buf.size() * sizeof(double)));
     off += (long long)buf.size();
   }
   return GPMDM_OK;
@@ -164,7 +186,7 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
   }
   rc = dalloc(&m->y_il2_dev, m->D);
   if (rc) { delete m; return rc; }
-  if (hipMemcpy(m->y_il2_dev, m->y_il2.data(), m->D * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+  if (h2d(m->y_il2_dev, m->y_il2.data(), m->D * sizeof(double)) != GPMDM_OK) {
     delete m;
     return fail(GPMDM_E_HIP, "upload y_inv_lambda2");
   }
@@ -176,7 +198,7 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
     }
     rc = dalloc(&m->y_lam2_dev, m->D);
     if (rc) { delete m; return rc; }
-    if (hipMemcpy(m->y_lam2_dev, lam2.data(), m->D * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+    if (h2d(m->y_lam2_dev, lam2.data(), m->D * sizeof(double)) != GPMDM_OK) {
       delete m;
       return fail(GPMDM_E_HIP, "upload lambda^2");
     }
@@ -194,7 +216,7 @@ int gpmdm_model_set_obs_cutoff(gpmdm_model_t m, const double* K_inv, const doubl
   CHECK(m, "null model");
   HIPCHK(hipSetDevice(m->device));
   if (!K_inv) {
-    HIPCHK(hipDeviceSynchronize());   // filters' launches may still read the image
+    TRY(quiesce_users(m));            // the filters' own launches may still read the image
     m->release_cutoff();
     return GPMDM_OK;
   }
@@ -213,7 +235,7 @@ int gpmdm_model_set_obs_cutoff(gpmdm_model_t m, const double* K_inv, const doubl
   std::vector<double> sph, rec;
   kstep_spheres(m->X.data(), m->y_ls.data(), perm.data(), N, d, sph);
   pk.records(rec);
-  HIPCHK(hipDeviceSynchronize());
+  TRY(quiesce_users(m));              // the filters' own launches may still read the old image
   m->release_cutoff();
   auto& ci = m->obs_cut;
   int rc = upload(&ci.sph, sph);
@@ -227,7 +249,7 @@ int gpmdm_model_set_obs_cutoff(gpmdm_model_t m, const double* K_inv, const doubl
     while (t1 < pk.tiles() && toff[(size_t)t1 + 1] - toff[(size_t)t0] <= (1LL << 22)) ++t1;
     buf.assign((size_t)(toff[(size_t)t1] - toff[(size_t)t0]), 0.0);
     for (int t = t0; t < t1; ++t) pk.pack_tile(t, buf.data() + (toff[(size_t)t] - toff[(size_t)t0]));
-    if (hipMemcpy(ci.Bt + toff[(size_t)t0], buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)
+    if (h2d(ci.Bt + toff[(size_t)t0], buf.data(), buf.size() * sizeof(double)) != GPMDM_OK)
       rc = fail(GPMDM_E_HIP, "upload of the cutoff image");
     t0 = t1;
   }
@@ -299,7 +321,9 @@ int gpmdm_predict_obs(gpmdm_model_t m, const double* Xs, int64_t n, double* mu, 
   fa.il2 = m->y_il2_dev;
   fa.var_out = var;
   launch_obs_finish(fa, s);
-  return finish_scratch(q, s);
+  TRY(finish_scratch(q, s));
+  HIPCHK(m->note_use(s));   // the model's release is ordered after this map (lifecycle waits)
+  return GPMDM_OK;
 }
 
 int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, double* mu, double* var, void* stream) {
@@ -347,7 +371,9 @@ int gpmdm_predict_dyn(gpmdm_model_t m, int c, const double* Xs, int64_t n, doubl
   for (int j = 0; j < m->d; ++j) fa.il2[j] = m->x_il2[j];
   fa.var_out = var;
   launch_dyn_finish(fa, s);
-  return finish_scratch(q, s);
+  TRY(finish_scratch(q, s));
+  HIPCHK(m->note_use(s));   // the model's release is ordered after this map (lifecycle waits)
+  return GPMDM_OK;
 }
 
 }  // extern "C"

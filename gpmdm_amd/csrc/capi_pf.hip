@@ -98,8 +98,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
 #undef ALLOC
   for (int k = 0; k < 2; ++k) {
     void* zv = nullptr;
-    if (hipHostMalloc((void**)&pf->zpin[k], sizeof(double) * F * D, hipHostMallocMapped | hipHostMallocCoherent) !=
-            hipSuccess ||
+    if (halloc(&pf->zpin[k], (size_t)(F * D), hipHostMallocMapped | hipHostMallocCoherent) != GPMDM_OK ||
         hipEventCreateWithFlags(&pf->zev[k], hipEventDisableTiming) != hipSuccess ||
         hipHostGetDevicePointer(&zv, pf->zpin[k], 0) != hipSuccess) {
       delete pf;
@@ -107,22 +106,20 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
     }
     pf->zdev[k] = (const double*)zv;
   }
-  if (hipHostMalloc((void**)&pf->rpin, sizeof(double) * F * (C + d + 1)) != hipSuccess) {
+  if (halloc(&pf->rpin, (size_t)(F * (C + d + 1)), 0) != GPMDM_OK) {
     delete pf;
     return fail(GPMDM_E_NOMEM, "pinned read-out buffer");
   }
   if (sizeof(double) * F * (C + d + 1) <= 32768) {
     void* rv = nullptr;
-    if (hipHostMalloc((void**)&pf->ro_pin, sizeof(double) * F * (C + d + 1),
-                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+    if (halloc(&pf->ro_pin, (size_t)(F * (C + d + 1)), hipHostMallocMapped | hipHostMallocCoherent) != GPMDM_OK ||
         hipHostGetDevicePointer(&rv, pf->ro_pin, 0) != hipSuccess) {
       delete pf;
       return fail(GPMDM_E_NOMEM, "mapped read-out buffer");
     }
     pf->ro_dev = (double*)rv;
     void* sv = nullptr;
-    if (hipHostMalloc((void**)&pf->seq_pin, sizeof(long long) * F, hipHostMallocMapped | hipHostMallocCoherent) !=
-            hipSuccess ||
+    if (halloc(&pf->seq_pin, (size_t)(F), hipHostMallocMapped | hipHostMallocCoherent) != GPMDM_OK ||
         hipHostGetDevicePointer(&sv, pf->seq_pin, 0) != hipSuccess) {
       delete pf;
       return fail(GPMDM_E_NOMEM, "mapped read-out number");
@@ -132,7 +129,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   }
   {
     void* rv = nullptr;
-    if (hipHostMalloc((void**)&pf->rows_pin, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+    if (halloc(&pf->rows_pin, 1, hipHostMallocMapped | hipHostMallocCoherent) != GPMDM_OK ||
         hipHostGetDevicePointer(&rv, pf->rows_pin, 0) != hipSuccess) {
       delete pf;
       return fail(GPMDM_E_NOMEM, "mapped row-count buffer");
@@ -146,7 +143,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
     const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
     for (int k = 0; k < 3; ++k) {
       void* dv = nullptr;
-      if (hipHostMalloc((void**)&pf->rep_pin[k], sizeof(double) * n[k], fl) != hipSuccess ||
+      if (halloc(&pf->rep_pin[k], (size_t)(n[k]), fl) != GPMDM_OK ||
           hipEventCreateWithFlags(&pf->rep_ev[k], hipEventDisableTiming) != hipSuccess ||
           hipHostGetDevicePointer(&dv, pf->rep_pin[k], 0) != hipSuccess) {
         delete pf;
@@ -155,14 +152,14 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
       pf->rep_dev[k] = (const double*)dv;
     }
     void* cv = nullptr;
-    if (hipHostMalloc((void**)&pf->cnt_pin, sizeof(int) * kMaxClasses, fl) != hipSuccess ||
+    if (halloc(&pf->cnt_pin, (size_t)(kMaxClasses), fl) != GPMDM_OK ||
         hipHostGetDevicePointer(&cv, pf->cnt_pin, 0) != hipSuccess) {
       delete pf;
       return fail(GPMDM_E_NOMEM, "pinned class-count buffer");
     }
     pf->cnt_dev = (int*)cv;
     void* qv = nullptr;
-    if (hipHostMalloc((void**)&pf->cseq_pin, sizeof(long long), fl) != hipSuccess ||
+    if (halloc(&pf->cseq_pin, 1, fl) != GPMDM_OK ||
         hipHostGetDevicePointer(&qv, pf->cseq_pin, 0) != hipSuccess) {
       delete pf;
       return fail(GPMDM_E_NOMEM, "mapped class-count number");
@@ -171,7 +168,7 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
     pf->cseq_dev = (long long*)qv;
     if (F == 1 && n_ranks == 1 && P <= kHostCountsMaxP) {
       void* lv = nullptr;
-      if (hipHostMalloc((void**)&pf->cls_pin, sizeof(int) * P, fl) != hipSuccess ||
+      if (halloc(&pf->cls_pin, (size_t)(P), fl) != GPMDM_OK ||
           hipHostGetDevicePointer(&lv, pf->cls_pin, 0) != hipSuccess ||
           hipEventCreateWithFlags(&pf->cls_ev, hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&pf->cnt_ev, hipEventDisableTiming) != hipSuccess) {
@@ -194,13 +191,15 @@ static int pf_create(gpmdm_model_t m, const double* T, int64_t F, int64_t Pf, in
   pf->preswitch = rng_mode == GPMDM_RNG_PHILOX && std::getenv("GPMDM_NO_PRESWITCH") == nullptr;
   pf->obs_img = &obs_pick(m, pf->Pf, pf->nloc, pf->obs_geo);
   const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, pf->obs_geo.pt())};
-  if (hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(pf->T, T, sizeof(double) * C * C, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(pf->health, 0, sizeof(unsigned) * kHealthN) != hipSuccess ||
-      hipMemset(pf->small, 0, sizeof(int) * 512) != hipSuccess) {
+  hipStream_t life = life_stream(m->device);   // (the lifecycle stream: no null-stream ordering)
+  if (!life || hipMemcpyAsync(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice, life) != hipSuccess ||
+      hipMemcpyAsync(pf->T, T, sizeof(double) * C * C, hipMemcpyHostToDevice, life) != hipSuccess ||
+      hipMemsetAsync(pf->health, 0, sizeof(unsigned) * kHealthN, life) != hipSuccess ||
+      hipMemsetAsync(pf->small, 0, sizeof(int) * 512, life) != hipSuccess || hipStreamSynchronize(life) != hipSuccess) {
     delete pf;
     return fail(GPMDM_E_HIP, "upload of particle-filter tables failed");
   }
+  m->add_user(pf);
   *out = pf;
   return GPMDM_OK;
 }
@@ -282,6 +281,28 @@ int drop_preswitch(gpmdm_pf* pf, hipStream_t s, bool host_wait) {
   return GPMDM_OK;
 }
 
+// Wait for everything this filter has launched, and nothing else (DESIGN.md §1 "Lifecycle
+// waits"): its pending pre-switch, its last read-out -- every stage of a frame precedes the
+// read-out on the frame's stream, which publishes a sequence number in mapped memory (or
+// records ro_ev) -- and its own side streams (replay uploads, the exchange's collectives).
+// Calls between frames that launch work (export, health, predict, dyn_rows) wait for it
+// themselves.  A filter stopped inside a frame (switched or propagated, not yet resampled)
+// has no such marker: then, and only then, the device is synchronised.
+int quiesce(gpmdm_pf* pf) {
+  HIPCHK(hipSetDevice(pf->m->device));
+  TRY(drop_preswitch(pf, nullptr, true));
+  if (pf->switched || pf->propagated || pf->dyn_done) {
+    HIPCHK(hipDeviceSynchronize());
+  } else if (pf->seq_pin && pf->ro_seq.load() > 0) {
+    HIPCHK(pf->wait_readout(pf->ro_seq.load()));
+  } else if (pf->ro_ev_ok) {
+    HIPCHK(hipEventSynchronize(pf->ro_ev));
+  }
+  if (pf->up_stream) HIPCHK(hipStreamSynchronize(pf->up_stream));
+  if (pf->cstream) HIPCHK(hipStreamSynchronize(pf->cstream));
+  return GPMDM_OK;
+}
+
 }  // namespace gpmdm::capi
 
 extern "C" {
@@ -304,43 +325,49 @@ int gpmdm_pf_shape(gpmdm_pf_t pf, int64_t* n_filters, int64_t* P) {
 }
 
 int gpmdm_pf_destroy(gpmdm_pf_t pf) {
-  delete pf;
-  return GPMDM_OK;
+  if (!pf) return GPMDM_OK;
+  const int rc = quiesce(pf);   // the filter's own launches only: its buffers are then released
+  delete pf;                    // in the lifecycle stream's order (memory.hip)
+  return rc;
 }
 
 int gpmdm_pf_init(gpmdm_pf_t pf, const double* states, const int64_t* classes) {
   CHECK(pf && states && classes, "null argument");
   gpmdm_model* m = pf->m;
   HIPCHK(hipSetDevice(m->device));
-  TRY(drop_preswitch(pf, nullptr, true));
-  pf->bmax_ready = false;
   const long long P = pf->P;
   std::vector<int> c32(P);
   for (long long i = 0; i < P; ++i) {
     CHECK(classes[i] >= 0 && classes[i] < m->C, "class id out of range");
     c32[i] = (int)classes[i];
   }
-  HIPCHK(hipMemcpy(pf->X, states, sizeof(double) * P * m->d, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(pf->cls, c32.data(), sizeof(int) * P, hipMemcpyHostToDevice));
+  TRY(quiesce(pf));                    // the filter's own frames, not the device
+  pf->bmax_ready = false;
+  // the uploads and the read-out of the initial state on the lifecycle stream (memory.hip)
+  hipStream_t ls = life_stream(m->device);
+  CHECK(ls, "the library's lifecycle stream");
+  std::vector<int> r32(P);
+  for (long long i = 0; i < P; ++i) r32[i] = (int)(i % pf->Pf);   // no shared ancestors yet
+  const std::vector<unsigned long long> neg(pf->F, 0x000fffffffffffffull);   // ord_enc(-inf)
+  HIPCHK(hipMemcpyAsync(pf->X, states, sizeof(double) * P * m->d, hipMemcpyHostToDevice, ls));
+  HIPCHK(hipMemcpyAsync(pf->cls, c32.data(), sizeof(int) * P, hipMemcpyHostToDevice, ls));
+  HIPCHK(hipMemcpyAsync(pf->ridx, r32.data(), sizeof(int) * P, hipMemcpyHostToDevice, ls));
+  HIPCHK(hipMemsetAsync(pf->ll, 0, sizeof(double) * P, ls));
+  HIPCHK(hipMemcpyAsync(pf->gmax, neg.data(), sizeof(unsigned long long) * pf->F, hipMemcpyHostToDevice, ls));
   if (pf->cls_pin) {
     std::memcpy(pf->cls_pin, c32.data(), sizeof(int) * P);
     pf->cls_host_ok = true;
     pf->cls_ev_pending = false;
   }
-  for (long long i = 0; i < P; ++i) c32[i] = (int)(i % pf->Pf);   // no shared ancestors yet
-  HIPCHK(hipMemcpy(pf->ridx, c32.data(), sizeof(int) * P, hipMemcpyHostToDevice));
-  HIPCHK(hipMemset(pf->ll, 0, sizeof(double) * P));
-  const std::vector<unsigned long long> neg(pf->F, 0x000fffffffffffffull);   // ord_enc(-inf)
-  HIPCHK(hipMemcpy(pf->gmax, neg.data(), sizeof(unsigned long long) * pf->F, hipMemcpyHostToDevice));
   // read-outs of the initial state: ll = log_w = 0, w = 1/P (gpmdm_pf.py:102-104)
   ResampleArgs ra = resample_args(pf);
   ra.identity = 1;
   ra.cls_src = pf->cls;
   ra.X_src = pf->X;
-  launch_normalise_resample(norm_args(pf), ra, nullptr);
+  launch_normalise_resample(norm_args(pf), ra, ls);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipEventRecord(pf->ro_ev, nullptr));
-  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipEventRecord(pf->ro_ev, ls));
+  HIPCHK(hipStreamSynchronize(ls));
   pf->ro_ev_ok = true;
   if (pf->seq_pin) pf->ro_seq = pf->seq_min();   // (synchronised: nothing to wait for)
   pf->initialised = true;
@@ -363,6 +390,7 @@ int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes,
   HIPCHK(hipSetDevice(m->device));
   TRY(drop_preswitch(pf, nullptr, true));
   if (pf->switched || pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "import between switch and resample");
+  TRY(quiesce(pf));                    // the filter's own frames, not the device
   CHECK(frame < (1ll << 32), "frame out of range");
   const long long P = pf->P, Pf = pf->Pf;
   const int F = pf->F;
@@ -388,13 +416,15 @@ int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes,
     gm[f] = (u >> 63) ? ~u : (u | 0x8000000000000000ull);   // ord_enc (common.h)
   }
   const std::vector<double> ones(F, 1.0);
-  HIPCHK(hipMemcpy(pf->X, states, sizeof(double) * P * m->d, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(pf->cls, c32.data(), sizeof(int) * P, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(pf->ridx, r32.data(), sizeof(int) * P, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(pf->ll, ll, sizeof(double) * P, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(pf->e, w, sizeof(double) * P, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(pf->total, ones.data(), sizeof(double) * F, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(pf->gmax, gm.data(), sizeof(unsigned long long) * F, hipMemcpyHostToDevice));
+  hipStream_t ls = life_stream(m->device);   // uploads and read-outs on the lifecycle stream
+  CHECK(ls, "the library's lifecycle stream");
+  HIPCHK(hipMemcpyAsync(pf->X, states, sizeof(double) * P * m->d, hipMemcpyHostToDevice, ls));
+  HIPCHK(hipMemcpyAsync(pf->cls, c32.data(), sizeof(int) * P, hipMemcpyHostToDevice, ls));
+  HIPCHK(hipMemcpyAsync(pf->ridx, r32.data(), sizeof(int) * P, hipMemcpyHostToDevice, ls));
+  HIPCHK(hipMemcpyAsync(pf->ll, ll, sizeof(double) * P, hipMemcpyHostToDevice, ls));
+  HIPCHK(hipMemcpyAsync(pf->e, w, sizeof(double) * P, hipMemcpyHostToDevice, ls));
+  HIPCHK(hipMemcpyAsync(pf->total, ones.data(), sizeof(double) * F, hipMemcpyHostToDevice, ls));
+  HIPCHK(hipMemcpyAsync(pf->gmax, gm.data(), sizeof(unsigned long long) * F, hipMemcpyHostToDevice, ls));
   if (pf->cls_pin) {
     std::memcpy(pf->cls_pin, c32.data(), sizeof(int) * P);
     pf->cls_host_ok = true;
@@ -408,14 +438,14 @@ int gpmdm_pf_import(gpmdm_pf_t pf, const double* states, const int64_t* classes,
   ra.identity = 1;
   ra.cls_src = pf->cls;
   ra.X_src = pf->X;
-  launch_resample(ra, nullptr);
+  launch_resample(ra, ls);
   HIPCHK(hipGetLastError());
   // the next frame's shards: the identity order (the exporter's uniforms are not part of the
   // state; the ownership order changes which rank evaluates a particle, never its values)
   pf->own_valid = false;
   pf->rows_st = pf->rows_ll = nullptr;
-  HIPCHK(hipEventRecord(pf->ro_ev, nullptr));
-  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipEventRecord(pf->ro_ev, ls));
+  HIPCHK(hipStreamSynchronize(ls));
   pf->ro_ev_ok = true;
   if (pf->seq_pin) pf->ro_seq = pf->seq_min();   // (synchronised: nothing to wait for)
   pf->initialised = true;
@@ -431,26 +461,23 @@ int gpmdm_pf_export(gpmdm_pf_t pf, double* states, int64_t* classes, double* ll,
   hipStream_t s = (hipStream_t)stream;
   TRY(flush_ll(pf, s));
   TRY(flush_rows(pf, s));
-  HIPCHK(hipStreamSynchronize(s));
+  // the copies in the caller's stream order, one wait at the end (not the null stream's)
   const long long P = pf->P;
-  if (states) HIPCHK(hipMemcpy(states, pf->X, sizeof(double) * P * m->d, hipMemcpyDeviceToHost));
-  std::vector<int> tmp(P);
-  if (classes) {
-    HIPCHK(hipMemcpy(tmp.data(), pf->cls, sizeof(int) * P, hipMemcpyDeviceToHost));
-    for (long long i = 0; i < P; ++i) classes[i] = tmp[i];
-  }
-  if (ridx) {
-    HIPCHK(hipMemcpy(tmp.data(), pf->ridx, sizeof(int) * P, hipMemcpyDeviceToHost));
-    for (long long i = 0; i < P; ++i) ridx[i] = tmp[i];
-  }
+  std::vector<int> tc(classes ? P : 0), tr(ridx ? P : 0);
   std::vector<double> l(P);
-  HIPCHK(hipMemcpy(l.data(), pf->ll, sizeof(double) * P, hipMemcpyDeviceToHost));
-  if (ll) std::memcpy(ll, l.data(), sizeof(double) * P);
   std::vector<unsigned long long> gm(pf->F);
   std::vector<double> S(pf->F);
-  HIPCHK(hipMemcpy(gm.data(), pf->gmax, sizeof(unsigned long long) * pf->F, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(S.data(), pf->total, sizeof(double) * pf->F, hipMemcpyDeviceToHost));
-  if (w) HIPCHK(hipMemcpy(w, pf->e, sizeof(double) * P, hipMemcpyDeviceToHost));
+  if (states) HIPCHK(hipMemcpyAsync(states, pf->X, sizeof(double) * P * m->d, hipMemcpyDeviceToHost, s));
+  if (classes) HIPCHK(hipMemcpyAsync(tc.data(), pf->cls, sizeof(int) * P, hipMemcpyDeviceToHost, s));
+  if (ridx) HIPCHK(hipMemcpyAsync(tr.data(), pf->ridx, sizeof(int) * P, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(l.data(), pf->ll, sizeof(double) * P, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(gm.data(), pf->gmax, sizeof(unsigned long long) * pf->F, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(S.data(), pf->total, sizeof(double) * pf->F, hipMemcpyDeviceToHost, s));
+  if (w) HIPCHK(hipMemcpyAsync(w, pf->e, sizeof(double) * P, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (long long i = 0; i < (classes ? P : 0); ++i) classes[i] = tc[i];
+  for (long long i = 0; i < (ridx ? P : 0); ++i) ridx[i] = tr[i];
+  if (ll) std::memcpy(ll, l.data(), sizeof(double) * P);
   for (int f = 0; f < pf->F; ++f) {
     const unsigned long long v = (gm[f] >> 63) ? (gm[f] & 0x7fffffffffffffffull) : ~gm[f];
     double M;
@@ -558,16 +585,24 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
   if (!rc) rc = dalloc(&sobs, (size_t)obs_blocks_max(m) * nl);
   TileGeo og{};
   const GpImage* oimg = &obs_pick(m, pf->Pf, pf->nloc, og);
-  const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, og.pt())};
-  if (!rc && hipMemcpy(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess)
-    rc = fail(GPMDM_E_HIP, "upload of the observation tile table");
   if (rc) {
     dfree(qdyn);
     dfree(qobs);
     dfree(sobs);
     return rc;
   }
-  HIPCHK(hipDeviceSynchronize());    // launches in flight may still read the old buffers
+  // the filter's own launches in flight may still read the old buffers and obs_tab: wait for
+  // them (not for the device), then release the old buffers in the lifecycle stream's order
+  TRY(quiesce(pf));
+  const int tab[5] = {(int)pf->lo, (int)pf->hi, 0, 0, (int)cdiv(pf->nloc, og.pt())};
+  hipStream_t ls = life_stream(m->device);
+  if (!ls || hipMemcpyAsync(pf->obs_tab, tab, sizeof(tab), hipMemcpyHostToDevice, ls) != hipSuccess ||
+      hipStreamSynchronize(ls) != hipSuccess) {
+    dfree(qdyn);
+    dfree(qobs);
+    dfree(sobs);
+    return fail(GPMDM_E_HIP, "upload of the observation tile table");
+  }
   dfree(pf->qdyn);
   dfree(pf->qobs);
   dfree(pf->sobs);
@@ -580,6 +615,8 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
   pf->obs_geo = og;
   pf->obs_img = oimg;
   m->refs.fetch_add(1);
+  old->remove_user(pf);
+  m->add_user(pf);
   pf->m = m;
   model_release(old);
   return GPMDM_OK;

@@ -24,8 +24,8 @@
 //    (mu = the mean tiles' V) are summed per column tile (its 16 columns by a DPP row
 //    reduction) and then over the tiles in list order, by one thread per particle.  An R
 //    tile's last list position is its own diagonal K-step, whose K* in the LDS ring are the
-//    tile's k_j: its partial is formed there, with no regeneration; mean tiles after the
-//    chunk's K loop.
+//    tile's k_j: its retired accumulators take the products V_j k_j there (no regeneration),
+//    and every tile of the chunk is reduced after the chunk's K loop.
 // Invariance: a K-step or R tile dropped for one tile composition contributes exact zeros to
 // every particle of another composition that includes it (its values are flushed for that
 // particle), and the sums run in increasing tile order, so a particle's q and S do not
@@ -258,10 +258,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
 #pragma unroll
     for (int j = 0; j < NTW; ++j) acc[i][j] = (d4){0.0, 0.0, 0.0, 0.0};
   __shared__ double qrun[PT], srun[PT];                       // running sums per particle
-  // per-position R-tile partials: the tile retiring at list position i writes slot i & 3; wave 0
-  // adds slots to qrun in position order after each barrier (a slot is rewritten two barriers
-  // after it was written, by which time wave 0 has added it)
-  __shared__ double ptq[4][PT];
   if (tid < PT) {
     qrun[tid] = 0.0;
     srun[tid] = 0.0;
@@ -317,22 +313,6 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
         bb[(2 * h + 1) * NTW + nt] = __builtin_bit_cast(double, (unsigned long long)x.z | ((unsigned long long)x.w << 32));
       }
     };
-    // R tiles of this chunk retire at list positions [c0, rlim), one per position, in list
-    // order: their partials are added in that order, as the sum over tiles requires
-    const int rlim = min(cend, n_act);
-    auto consume = [&](int i0, int i1) {                     // positions i0 .. i1 (wave 0)
-      if (tid < PT) {
-        if (second) {                                        // a second part: the partials
-          for (int q = i0; q <= i1; ++q)
-            if (q >= c0 && q < rlim) prm.part[pbase + (long long)(q - r0) * prm.ld_part + tid] = ptq[q & 3][tid];
-        } else {
-          double qa = qrun[tid];
-          for (int q = i0; q <= i1; ++q)
-            if (q >= c0 && q < rlim) qa += ptq[q & 3][tid];
-          qrun[tid] = qa;
-        }
-      }
-    };
     auto step = [&](auto t0c, auto t1c, int i, bool retire, double (&bb)[4 * NTW]) {
       constexpr int T0 = decltype(t0c)::value, T1c = decltype(t1c)::value;
       const int buf = i & (ASL - 1);
@@ -355,23 +335,19 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
       }
       if (retire) {
         // tile T0's diagonal position: this K-step's rows are the tile's columns, so the K*
-        // just multiplied are its k_j (the flushed values, as generated): the tile's partial
-        // sum_j V_j k_j per particle, reduced over its 16 columns (lanes li)
+        // just multiplied are its k_j (the flushed values, as generated).  The tile's
+        // accumulators are final from here on (it has retired), so they take the products
+        // V_j k_j in place; their reduction over the 16 columns waits for the chunk's end,
+        // with every other tile's (no reduction, no LDS partials, no extra barrier work
+        // inside the K loop)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int pr = mt * 16 + lk + 4 * r;
-            const double v = row16_sum(acc[mt][T0][r] * As[buf][li][pr]);
-            if (li == 0) ptq[i & 3][pr] = v;
-          }
+          for (int r = 0; r < 4; ++r) acc[mt][T0][r] *= As[buf][li][mt * 16 + lk + 4 * r];
       }
       store((i + LOOK) & (ASL - 1), v);
       store_rows((i + RA) & (RXS - 1), rr);
-      if (i % SB == SB - 1) {
-        __syncthreads();
-        consume(i - 1, i);
-      }
+      if (i % SB == SB - 1) __syncthreads();
     };
 
     double bb[4 * NTW];
@@ -418,10 +394,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
       gen((i + LOOK) & (RXS - 1), v);
       store((i + LOOK) & (ASL - 1), v);
       store_rows((i + RA) & (RXS - 1), rr);
-      if (i % SB == SB - 1) {
-        __syncthreads();
-        consume(i - 1, i);
-      }
+      if (i % SB == SB - 1) __syncthreads();
     }
     if (prm.sp_stats && lane == 0) {
       unsigned run = 0;
@@ -431,16 +404,24 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
     }
 
     __syncthreads();                                         // every wave is done with As
-    if (npos % SB == 1) consume(npos - 1, npos - 1);          // the last position's partial
-    // ---- mean tiles: per-tile sums into LDS (aliasing the K* ring), then in list order ------
-    if (last >= n_act) {                                     // (uniform) the chunk holds mean tiles
+    // ---- the chunk's per-tile sums into LDS (aliasing the K* ring), then in list order ------
+    // R tiles: sum_j V_j k_j (the products formed at the diagonal); mean tiles:
+    // (z_j - mu_j)^2 lam2_j over the tile's columns (gpmdm_pf.py:188-192 with var_j = vc / lam2_j
+    // factored out; k_obs_ll finishes the likelihood); each reduced over its 16 columns (lanes li)
 #pragma unroll
-      for (int nt = 0; nt < NTW; ++nt) {
-        const int i2 = c0 + NW * nt + w;
-        if (i2 < n_act || i2 >= cend) continue;              // (wave-uniform)
-        // (z_j - mu_j)^2 lam2_j over the tile's columns (gpmdm_pf.py:188-192 with var_j =
-        // vc / lam2_j factored out; k_obs_ll finishes the likelihood), reduced over its 16
-        // columns (lanes li)
+    for (int nt = 0; nt < NTW; ++nt) {
+      const int i2 = c0 + NW * nt + w;
+      if (i2 >= cend) continue;                              // (wave-uniform)
+      if (i2 < n_act) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int pr = mt * 16 + lk + 4 * r;
+            const double v = row16_sum(acc[mt][nt][r]);
+            if (li == 0) ptile[(NW * nt + w) * PT + pr] = v;
+          }
+      } else {
         const int jm = 16 * (i2 - n_act) + li;
         const bool real = jm < prm.n_m;
         const double lam = real ? prm.lam2[jm] : 0.0;
@@ -454,17 +435,22 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
             if (li == 0) ptile[(NW * nt + w) * PT + pr] = v;
           }
       }
-      __syncthreads();
-      if (tid < PT) {
-        const int ns = cend - c0;
-        if (second) {
-          for (int s = n_act - c0 > 0 ? n_act - c0 : 0; s < ns; ++s)
-            prm.part[pbase + (long long)(c0 + s - r0) * prm.ld_part + tid] = ptile[s * PT + tid];
-        } else {
-          double sa = srun[tid];
-          for (int s = n_act - c0 > 0 ? n_act - c0 : 0; s < ns; ++s) sa += ptile[s * PT + tid];
-          srun[tid] = sa;
+    }
+    __syncthreads();
+    if (tid < PT) {
+      const int ns = cend - c0;
+      if (second) {                                          // a second part: the partials
+        for (int s = 0; s < ns; ++s) prm.part[pbase + (long long)(c0 + s - r0) * prm.ld_part + tid] = ptile[s * PT + tid];
+      } else {
+        double qa = qrun[tid], sa = srun[tid];
+        for (int s = 0; s < ns; ++s) {
+          if (c0 + s < n_act)
+            qa += ptile[s * PT + tid];
+          else
+            sa += ptile[s * PT + tid];
         }
+        qrun[tid] = qa;
+        srun[tid] = sa;
       }
     }
 #pragma unroll

@@ -98,7 +98,9 @@ struct Handle {
 struct DevBufs {
   double *Xs = nullptr, *sq = nullptr, *X = nullptr, *c2 = nullptr, *K = nullptr, *B0 = nullptr, *B1 = nullptr;
   int* info = nullptr;
+  hipStream_t s = nullptr;   // the stream the buffers were used on (released after its work)
   ~DevBufs() {
+    (void)hipStreamSynchronize(s);   // (an early error return may leave launches in flight)
     dfree(Xs); dfree(sq); dfree(X); dfree(c2); dfree(K); dfree(B0); dfree(B1); dfree(info);
   }
 };
@@ -194,6 +196,7 @@ extern "C" int gpmdm_spd_inverse(int device, double* A, int64_t n, double* logde
   RBCHK(rocblas_set_stream(h, s));
   const int N = (int)n;
   DevBufs b;
+  b.s = s;
   TRY(dalloc(&b.info, 1));
   TRY(dalloc(&b.sq, 1));                                    // logdet scratch
   int info = 0;

@@ -260,8 +260,9 @@ def _full_cloud_vs_oracle(om, T, pre, post, pf, seed, frame, z, what, chunk=8192
       * every particle's ll: 1e-5 normwise and 1e-5 of its terms' magnitude;
       * every weight: 1e-5 normwise (BASELINE's figure);
       * resample indices: the oracle's search of the ORACLE's weights; the slots whose ancestor
-        differs are counted (a 1e-6 weight difference moves a CDF boundary across a uniform
-        with probability ~1e-6 per slot) and held to <= 2;
+        differs are counted (a 1e-7 weight difference moves a CDF boundary across a uniform
+        with probability ~1e-7 per boundary and slot) and each must be a boundary case: its
+        uniform within 1e-6 of the oracle CDF's interval for the GPU's ancestor;
       * posterior (1e-5 abs), state mean (1e-5 normwise) and the likelihood read-out (1e-5
         relative) from the oracle's own weights and ancestors.
     Returns the check's figures (recorded in gpurun_out/full_cloud_oracle.json)."""
@@ -293,13 +294,26 @@ def _full_cloud_vs_oracle(om, T, pre, post, pf, seed, frame, z, what, chunk=8192
                               + abs(O.loglik_const(zz.shape[0])))
         _progress(f"{what}: oracle observation GP, particles [{i}, {min(P, i + chunk)})")
     log_w, w = O.normalise(ll)
-    idx = O.multinomial_resample_indices(w, X.resample_uniforms(seed, frame, P))
+    u = X.resample_uniforms(seed, frame, P)
+    idx = O.multinomial_resample_indices(w, u)
+    # slots whose ancestor differs: each must be a boundary case -- its uniform within 1e-6 of
+    # the oracle CDF's interval for the GPU's ancestor (the CDF is accurate to the weights'
+    # tolerance; two correct fp64 CDFs put a uniform on different sides of a boundary when it
+    # falls between them)
+    cum = np.cumsum(w)
+    cum = cum / cum[-1]
+    cum[-1] = 1.0
+    bad = np.nonzero(post["resample_idx"] != idx)[0]
+    j = post["resample_idx"][bad]
+    lo = np.where(j > 0, cum[np.maximum(j - 1, 0)], 0.0)
+    gap = np.maximum(np.maximum(lo - u[bad], u[bad] - cum[j]), 0.0)
     post_o = O.class_probabilities(ll, log_w, cls1[idx], C)
     mean_o = O.current_state_mean(st1[idx], w)
     lik_o = O.log_likelihood_readout(ll, log_w)
     fig = {"what": what, "P": P, "oracle_s": time.time() - t0,
            "ll_nrel": nrel(post["ll"], ll), "ll_term_scaled": float(np.max(np.abs(post["ll"] - ll) / terms)),
-           "w_nrel": nrel(post["w"], w), "idx_mismatch": int(np.sum(post["resample_idx"] != idx)),
+           "w_nrel": nrel(post["w"], w), "idx_mismatch": int(bad.size),
+           "idx_mismatch_max_gap": float(gap.max()) if bad.size else 0.0,
            "posterior_abs": float(np.max(np.abs(pf.class_probabilities().numpy() - post_o))),
            "mean_nrel": nrel(pf.current_state_mean().numpy(), mean_o),
            "lik_rel": abs(pf.log_likelihood() - lik_o) / abs(lik_o),
@@ -310,7 +324,7 @@ def _full_cloud_vs_oracle(om, T, pre, post, pf, seed, frame, z, what, chunk=8192
     assert np.array_equal(post["classes"], cls1[post["resample_idx"]]), what
     assert fig["ll_nrel"] < 1e-5 and fig["ll_term_scaled"] < 1e-5, fig
     assert fig["w_nrel"] < 1e-5, fig
-    assert fig["idx_mismatch"] <= 2, fig
+    assert fig["idx_mismatch"] <= max(2, P // 1000) and fig["idx_mismatch_max_gap"] <= 1e-6, fig
     assert fig["posterior_abs"] < 1e-5 and fig["mean_nrel"] < 1e-5 and fig["lik_rel"] < 1e-5, fig
     return fig
 
@@ -358,6 +372,7 @@ def test_large_config_benchmarked_particles_full_oracle(cfg):
     T = synthetic.markov_matrix(c["C"])
     zs = data.observation_stream(2, seed=1)
     P = {3: 100_000, 5: 125_000}[cfg]
+    torch.manual_seed(70 + cfg)          # (the initial cloud: independent of the tests before)
     pf, post, pre, frame = _philox_step_vs_oracle(m, om_t, T, P, 11, zs[0], zs[1], f"config {cfg} at P={P}")
     fig = _full_cloud_vs_oracle(om_t, T, pre, post, pf, 11, frame, zs[1], f"config {cfg} at P={P}, full cloud")
     print(fig)

@@ -11,6 +11,9 @@
 #   bash tools/gpu_pass.sh spread <tag> [configs...]
 #        the cutoff on spread clouds (bench.py --cutoff-spread): dense vs cutoff launches from
 #        resynced >= 1000-ancestor clouds at three spreads (default configs 2 3 5)
+#   bash tools/gpu_pass.sh cutoff-ab <tag> [configs...]
+#        same-box A/B of the cutoff kernel: the working tree against tools/ab_prev (spread clouds
+#        at each config, the config-2 cutoff line, and the bits of a 5-frame cutoff trajectory)
 #   bash tools/gpu_pass.sh cutoff-pmc <tag>
 #        PMC passes of the config-2 bench with its cutoff line (dense and cutoff kernels)
 #   bash tools/gpu_pass.sh configs <tag> [configs...]
@@ -87,6 +90,34 @@ spread)
     timeout -k 10 $lim python -u bench.py --config $c --cutoff-spread --no-cpu-baseline > $out/spread_c$c.json 2> $out/spread_c$c.err \
       || { echo "spread config $c failed rc=$?"; tail -8 $out/spread_c$c.err; exit 1; }
     python -c "import json,sys;d=json.load(open(sys.argv[1]));[print('config', sys.argv[2], json.dumps(r)) for r in d['cutoff_spread']['rows']]" $out/spread_c$c.json $c
+  done
+  ;;
+cutoff-ab)
+  mkdir -p tools/ab_prev/tools && cp tools/cutoff_hash.py tools/ab_prev/tools/
+  for c in ${*:-2 3 5}; do
+    for v in new prev; do
+      dir=.; [ $v = prev ] && dir=tools/ab_prev
+      (cd $dir && timeout -k 10 300 python -u tools/cutoff_hash.py --config $c --frames 4) > $out/hash_${v}_c$c.txt 2>&1 \
+        || { echo "hash $v c$c failed"; tail -5 $out/hash_${v}_c$c.txt; exit 1; }
+      echo "hash $v c$c $(tail -1 $out/hash_${v}_c$c.txt)"
+    done
+  done
+  for r in 1 2; do
+    for c in ${*:-2 3 5}; do
+      for v in new prev; do
+        dir=.; [ $v = prev ] && dir=tools/ab_prev
+        lim=600; [ "$c" = 5 ] && lim=1000
+        (cd $dir && timeout -k 10 $lim python -u bench.py --config $c --cutoff-spread --no-cpu-baseline) > $out/spread_${v}_c${c}_$r.json 2> $out/spread_${v}_c${c}_$r.err \
+          || { echo "spread $v c$c failed"; tail -8 $out/spread_${v}_c${c}_$r.err; exit 1; }
+        python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], [(r['spread_ell'], round(r['cutoff_obs_launch_ms'],3), round(r['dense_obs_launch_ms'],3), round(r['executed_frac_of_peak'],3)) for r in d['cutoff_spread']['rows']])" $out/spread_${v}_c${c}_$r.json "spread $v c$c r$r"
+      done
+    done
+    for v in new prev; do
+      dir=.; [ $v = prev ] && dir=tools/ab_prev
+      (cd $dir && timeout -k 10 300 python -u bench.py --steps 40 --cutoff-steps 20 $HEAD_ARGS) > $out/c2_${v}_$r.json 2> $out/c2_${v}_$r.err \
+        || { echo "c2 $v failed"; tail -5 $out/c2_${v}_$r.err; exit 1; }
+      show $out/c2_${v}_$r.json "c2 $v r$r"
+    done
   done
   ;;
 cutoff-pmc)
