@@ -84,8 +84,11 @@ _SIGS = {
     "gpmdm_pf_health": (c_int, [c_void_p, _i64p, c_int, c_void_p]),
     "gpmdm_model_set_obs_cutoff": (c_int, [c_void_p, c_void_p, c_void_p, ctypes.c_double, c_void_p]),
     "gpmdm_model_obs_cutoff": (c_int, [c_void_p, POINTER(ctypes.c_double)]),
+    "gpmdm_model_build_obs_cutoff": (c_int, [c_void_p, ctypes.c_double, c_void_p, c_void_p, c_void_p]),
+    "gpmdm_model_obs_cutoff_image": (c_int, [c_void_p, _i64p, c_void_p]),
     "gpmdm_pf_set_obs_cutoff": (c_int, [c_void_p, c_int]),
     "gpmdm_pf_set_obs_cutoff_split": (c_int, [c_void_p, c_int]),
+    "gpmdm_pf_obs_cutoff_auto": (c_int, [c_void_p, POINTER(c_int), POINTER(ctypes.c_double)]),
     "gpmdm_pf_obs_cutoff_stats": (c_int, [c_void_p, _i64p, _i64p, c_int, c_void_p]),
     "gpmdm_pf_predict": (c_int, [c_void_p, _dp, c_void_p]),
     "gpmdm_pf_set_comm": (c_int, [c_void_p, c_void_p, c_int]),

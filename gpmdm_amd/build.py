@@ -23,7 +23,7 @@ LIB = PKG / "libgpmdm_hip.so"
 SOURCES = ["gp_tile.hip", "gp_tile_d1.hip", "gp_tile_d2.hip", "gp_tile_d3.hip", "gp_tile_d4.hip",
            "gp_tile_d5.hip", "pf_kernels.hip", "capi_model.hip", "capi_pf.hip", "capi_frame.hip",
            "capi_exchange.hip", "capi_replay.hip", "precompute.hip", "shard_order.hip", "torch_rng.cpp",
-           "obs_cutoff.hip", "obs_cutoff_d9.hip", "memory.hip"]
+           "obs_cutoff.hip", "obs_cutoff_d9.hip", "memory.hip", "cutoff_image.hip"]
 HEADERS = [CSRC / "common.h", CSRC / "geometry.h", CSRC / "host_image.h", CSRC / "gp_tile.h", CSRC / "pf_kernels.h",
            CSRC / "status.h", CSRC / "capi_internal.h", CSRC / "obs_cutoff.h", ROOT / "include" / "gpmdm_hip.h"]
 ARCH = "gfx950"

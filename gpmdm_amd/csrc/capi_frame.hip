@@ -412,7 +412,25 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     pf->mark_begin(s, GPMDM_STAGE_OBS_GEMM, t0);
     // the opt-in kernel-value cutoff: its own kernel over the cutoff image (obs_cutoff.h),
     // one q and one S partial per particle
-    const bool cut = pf->obs_cutoff && m->has_cutoff();
+    bool cut = pf->obs_cutoff && m->has_cutoff();
+    // AUTO (gpmdm_pf::cut_auto): the cutoff while the reach it last measured is below the
+    // break-even, a cutoff frame at least every kCutAutoProbe frames to measure it again
+    bool auto_frame = false;
+    if (cut && pf->cut_auto_active() && !small_resample_ok(norm_args(pf), resample_args(pf))) {
+      if (pf->cut_auto_pending) {      // the last cutoff frame's counters, published with its read-out
+        HIPCHK(pf->wait_readout(pf->cut_auto_seq));
+        const unsigned long long run = __atomic_load_n(pf->cut_auto_host + 0, __ATOMIC_ACQUIRE);
+        const unsigned long long dense = __atomic_load_n(pf->cut_auto_host + 1, __ATOMIC_ACQUIRE);
+        pf->cut_auto_frac = dense ? (double)run / (double)dense : 0.0;
+        pf->cut_auto_pending = false;
+      }
+      const bool probe = pf->cut_auto_frac < 0.0 || (long long)pf->frame - pf->cut_auto_probe >= gpmdm_pf::kCutAutoProbe;
+      cut = probe || pf->cut_auto_frac <= gpmdm_pf::kCutAutoMaxRun;
+      auto_frame = cut;
+      if (cut) pf->cut_auto_probe = pf->frame;
+    }
+    pf->cut_frame = cut;
+    pf->cut_frame_auto = auto_frame;
     const GpImage& oi = *pf->obs_img;
     // Particle order of the tiles: positions [lo, hi) of the ownership order -- or, for a
     // cutoff filter whose switch grouped exactly this rank's particles (one rank, or a
@@ -449,7 +467,7 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
       cp.z = zsrc;
       cp.lam2 = m->y_lam2_dev;
       cp.Pf = pf->Pf;
-      cp.sp_stats = pf->sp_stats_on ? pf->sp_stats : nullptr;
+      cp.sp_stats = auto_frame ? pf->cut_auto_dev : (pf->sp_stats_on ? pf->sp_stats : nullptr);
       // the grid's tail: equal workgroups run in whole rounds of the resident slots, so the
       // tiles past the last full round are split in two workgroups each (chunks [0, c*) and
       // [c*, nc); bitwise the whole tile's sums, k_obs_ll chains the second part on).  Below
@@ -652,7 +670,17 @@ int gpmdm_pf_resample(gpmdm_pf_t pf, const double* uniforms, void* stream) {
   pf->rows_st = pf->rows_ll = nullptr;
   const bool cls_host = pf->cls_pin && small;
   if (cls_host) ra.cls_host = pf->cls_pdev;
+  const bool auto_stats = pf->cut_frame_auto && !small && pf->seq_pin;
+  if (auto_stats) {                    // this frame's cutoff counters travel with the read-out
+    ra.cut_stats = pf->cut_auto_dev;
+    ra.cut_stats_host = pf->cut_auto_hdev;
+  }
+  pf->cut_frame_auto = false;
   launch_normalise_resample(na, ra, s);
+  if (auto_stats) {
+    pf->cut_auto_pending = true;
+    pf->cut_auto_seq = ra.seq;
+  }
   pf->bmax_ready = false;
   pf->cls_host_ok = cls_host;
   if (cls_host) {

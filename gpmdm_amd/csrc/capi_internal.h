@@ -19,6 +19,7 @@
 #include <vector>
 
 #include <dlfcn.h>
+#include <functional>
 #include <mutex>
 #include <type_traits>
 
@@ -241,6 +242,25 @@ struct gpmdm_pf {
   bool obs_cutoff = false;
   unsigned long long* sp_stats = nullptr;
   bool sp_stats_on = false;
+  // AUTO (gpmdm_pf_set_obs_cutoff mode 3; single-rank filters and banks with mapped
+  // read-outs): the cutoff kernel while the reach it measured is low, the dense kernel
+  // otherwise -- decided per frame from the last cutoff frame's MFMA-group fraction, with a
+  // cutoff frame (a probe) at least every kCutAutoProbe frames.  The counters travel with the
+  // read-out (k_readout -> cut_auto_host), so the decision is a function of the filter's own
+  // trajectory: deterministic, but not rank-count invariant (multi-rank filters run mode 1).
+  static constexpr int kCutAutoProbe = 8;
+  static constexpr double kCutAutoMaxRun = 0.75;   // break-even: cutoff 0.65 vs dense 0.865 of peak
+  bool cut_auto = false;
+  unsigned long long* cut_auto_dev = nullptr;      // device counters {run, dense}
+  unsigned long long* cut_auto_host = nullptr;     // mapped: the last cutoff frame's counters
+  unsigned long long* cut_auto_hdev = nullptr;     // (its device view)
+  bool cut_auto_pending = false;                   // a cutoff frame's counters are on their way
+  long long cut_auto_seq = 0;                      // ... published with this read-out number
+  double cut_auto_frac = -1.0;                     // the last measured fraction (< 0: none)
+  long long cut_auto_probe = -(1LL << 40);         // the frame of the last cutoff frame
+  bool cut_frame = false;                          // this frame's observation GP is the cutoff's
+  bool cut_frame_auto = false;                     // ... an AUTO filter's (its counters go with the read-out)
+  bool cut_auto_active() const { return cut_auto && obs_cutoff && n_ranks == 1 && seq_pin != nullptr; }
   // the cutoff kernel's split tiles (capi_frame.hip): second parts' partials, (n_act, c*) per
   // split tile; grown on demand
   int cut_split_policy = GPMDM_CUT_SPLIT_AUTO;
@@ -575,6 +595,8 @@ struct gpmdm_pf {
     dfree(own_tmp);
     dfree(gmax);
     dfree(sp_stats);
+    dfree(cut_auto_dev);
+    hfree(cut_auto_host);
     dfree(cut_part);
     dfree(cut_split);
     dfree(bmax);
@@ -639,6 +661,17 @@ NormArgs norm_args(gpmdm_pf* pf);
 int flush_ll(gpmdm_pf* pf, hipStream_t s);
 int drop_preswitch(gpmdm_pf* pf, hipStream_t s, bool host_wait);
 int quiesce(gpmdm_pf* pf);
+int quiesce_users(gpmdm_model* m);
+int h2d(void* dst, const void* src, size_t bytes);
+// the observation-GP cutoff image (capi_model.hip; packed on the host or the device)
+struct CutoffPlan {
+  std::vector<long long> perm, toff;
+  std::vector<double> sph, rec;
+  double tau = 0.0;
+  int T_R = 0, T_M = 0;
+};
+int cutoff_plan(gpmdm_model* m, double sigma2, const double* M, const double* y_absmax, CutoffPlan& pl);
+int cutoff_install(gpmdm_model* m, const CutoffPlan& pl, const std::function<int(double*, const long long*)>& fill);
 int do_switch(gpmdm_pf* pf, const double* E, int64_t* class_counts, hipStream_t s, bool order_ahead = false, bool counts_ahead = false, bool e_uploaded = false);
 int propagate_dynamics(gpmdm_pf* pf, const double* normals, hipStream_t s, bool zstage = false);
 int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s);

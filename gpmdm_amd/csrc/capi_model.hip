@@ -20,7 +20,7 @@ namespace gpmdm::capi {
 
 // host -> device on the current device's lifecycle stream (memory.hip): not ordered behind the
 // legacy null stream's users
-static int h2d(void* dst, const void* src, size_t bytes) {
+int h2d(void* dst, const void* src, size_t bytes) {
   hipStream_t ls = life_stream_current();
   CHECK(ls, "the library's lifecycle stream");
   HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ls));
@@ -36,7 +36,7 @@ int upload(T** dst, const std::vector<T>& v) {
 
 // Wait for the last frame of every filter built on the model (not for the device): the
 // caller guarantees none of them is inside a frame or stepping on another thread.
-static int quiesce_users(gpmdm_model* m) {
+int quiesce_users(gpmdm_model* m) {
   std::vector<gpmdm_pf*> us;
   {
     std::lock_guard<std::mutex> lk(m->life_mu);
@@ -72,6 +72,54 @@ int build_image(GpImage& g, int n_rows, int d, int n_m, const double* X, const d
     TRY(h2d(g.Bf + off, buf.data(), buf.size() * sizeof(double)));
     off += (long long)buf.size();
   }
+  return GPMDM_OK;
+}
+
+// The host half of a cutoff image, whichever side packs it: tau (host_image.h
+// obs_cutoff_tau, from M = K^-1 Y and the data's scale), the spatial order of the training
+// rows, the K-step spheres, the row records in that order and the tile offsets.
+int cutoff_plan(gpmdm_model* m, double sigma2, const double* M, const double* y_absmax, CutoffPlan& pl) {
+  CHECK(sigma2 > 0.0 && std::isfinite(sigma2), "sigma2 must be positive (the observation noise variance)");
+  CHECK(ksteps((int)m->N) <= kMaxCutoffKs, "the cutoff image holds at most 65536 training rows");
+  CHECK(m->d <= 16, "the cutoff image is built for latent dimensions d <= 16");
+  const int N = (int)m->N, d = m->d;
+  pl.tau = obs_cutoff_tau(N, sigma2, M, m->D, y_absmax);
+  CHECK(pl.tau > 0.0 && std::isfinite(pl.tau), "no usable cutoff for this model");
+  pl.perm = spatial_order(m->X.data(), m->y_ls.data(), N, d);
+  CutoffPacker pk(N, d, m->D, m->X.data(), m->y_ls.data(), nullptr, nullptr, pl.perm.data());
+  pl.toff = pk.offsets();
+  pl.T_R = pk.T_R;
+  pl.T_M = pk.T_M;
+  // the kernel addresses the image with 32-bit byte offsets (one buffer resource)
+  CHECK(pl.toff.back() * 8 < (1LL << 32), "the cutoff image exceeds 4 GiB (about 32k training rows)");
+  kstep_spheres(m->X.data(), m->y_ls.data(), pl.perm.data(), N, d, pl.sph);
+  pk.records(pl.rec);
+  return GPMDM_OK;
+}
+
+// Replace the model's cutoff image: wait for the filters built on it (their own last frames),
+// release the old image, upload the plan's tables and let `fill` write the image Bt (device,
+// toff.back() doubles; toff_dev: the tile offsets on the device).
+int cutoff_install(gpmdm_model* m, const CutoffPlan& pl, const std::function<int(double*, const long long*)>& fill) {
+  TRY(quiesce_users(m));              // the filters' own launches may still read the old image
+  m->release_cutoff();
+  auto& ci = m->obs_cut;
+  int rc = upload(&ci.sph, pl.sph);
+  if (!rc) rc = upload(&ci.Xrec, pl.rec);
+  if (!rc) rc = upload(&ci.toff, pl.toff);
+  if (!rc) rc = dalloc(&ci.Bt, (size_t)pl.toff.back());
+  if (!rc) rc = fill(ci.Bt, ci.toff);
+  if (rc) {
+    m->release_cutoff();
+    return rc;
+  }
+  ci.n_rows = (int)m->N;
+  ci.n_m = m->D;
+  ci.T_R = pl.T_R;
+  ci.T_M = pl.T_M;
+  m->cut_tau = pl.tau;
+  m->cut2 = -std::log(pl.tau) * (1.0 + 1e-12) + 1e-6;   // margin over both tests' rounding
+  m->t_cut = std::log(pl.tau) * kLog2eX64;
   return GPMDM_OK;
 }
 
@@ -210,7 +258,8 @@ int gpmdm_model_create(const gpmdm_model_desc* desc, int device, gpmdm_model_t* 
 // The observation GP's opt-in kernel-value cutoff (DESIGN.md §3 "Kernel-value cutoff"):
 // the K^-1 image in the symmetric block form over a spatial order of the training rows,
 // tile-major (host_image.h CutoffPacker), the per-K-step bounding spheres and tau.
-// K_inv = NULL removes it.
+// K_inv = NULL removes it.  (gpmdm_model_build_obs_cutoff, cutoff_image.hip, builds the same
+// image on the device from the model's own factor.)
 int gpmdm_model_set_obs_cutoff(gpmdm_model_t m, const double* K_inv, const double* beta, double sigma2,
                                const double* y_absmax) {
   CHECK(m, "null model");
@@ -221,49 +270,38 @@ int gpmdm_model_set_obs_cutoff(gpmdm_model_t m, const double* K_inv, const doubl
     return GPMDM_OK;
   }
   CHECK(beta && y_absmax, "null argument");
-  CHECK(sigma2 > 0.0 && std::isfinite(sigma2), "sigma2 must be positive (the observation noise variance)");
-  CHECK(ksteps((int)m->N) <= kMaxCutoffKs, "the cutoff image holds at most 65536 training rows");
-  CHECK(m->d <= 16, "the cutoff image is built for latent dimensions d <= 16");
-  const int N = (int)m->N, d = m->d;
-  const double tau = obs_cutoff_tau(N, sigma2, beta, m->D, y_absmax);
-  CHECK(tau > 0.0 && std::isfinite(tau), "no usable cutoff for this model");
-  const std::vector<long long> perm = spatial_order(m->X.data(), m->y_ls.data(), N, d);
-  CutoffPacker pk(N, d, m->D, m->X.data(), m->y_ls.data(), K_inv, beta, perm.data());
-  const std::vector<long long> toff = pk.offsets();
-  // the kernel addresses the image with 32-bit byte offsets (one buffer resource)
-  CHECK(toff.back() * 8 < (1LL << 32), "the cutoff image exceeds 4 GiB (about 32k training rows)");
-  std::vector<double> sph, rec;
-  kstep_spheres(m->X.data(), m->y_ls.data(), perm.data(), N, d, sph);
-  pk.records(rec);
-  TRY(quiesce_users(m));              // the filters' own launches may still read the old image
-  m->release_cutoff();
-  auto& ci = m->obs_cut;
-  int rc = upload(&ci.sph, sph);
-  if (!rc) rc = upload(&ci.Xrec, rec);
-  if (!rc) rc = upload(&ci.toff, toff);
-  if (!rc) rc = dalloc(&ci.Bt, (size_t)toff.back());
+  CutoffPlan pl;
+  TRY(cutoff_plan(m, sigma2, beta, y_absmax, pl));
+  const int N = (int)m->N;
+  CutoffPacker pk(N, m->d, m->D, m->X.data(), m->y_ls.data(), K_inv, beta, pl.perm.data());
   // packed and uploaded a group of tiles at a time (the host never holds the whole image)
-  std::vector<double> buf;
-  for (int t0 = 0; !rc && t0 < pk.tiles();) {
-    int t1 = t0 + 1;
-    while (t1 < pk.tiles() && toff[(size_t)t1 + 1] - toff[(size_t)t0] <= (1LL << 22)) ++t1;
-    buf.assign((size_t)(toff[(size_t)t1] - toff[(size_t)t0]), 0.0);
-    for (int t = t0; t < t1; ++t) pk.pack_tile(t, buf.data() + (toff[(size_t)t] - toff[(size_t)t0]));
-    if (h2d(ci.Bt + toff[(size_t)t0], buf.data(), buf.size() * sizeof(double)) != GPMDM_OK)
-      rc = fail(GPMDM_E_HIP, "upload of the cutoff image");
-    t0 = t1;
+  return cutoff_install(m, pl, [&](double* Bt, const long long*) -> int {
+    const std::vector<long long>& toff = pl.toff;
+    std::vector<double> buf;
+    for (int t0 = 0; t0 < pk.tiles();) {
+      int t1 = t0 + 1;
+      while (t1 < pk.tiles() && toff[(size_t)t1 + 1] - toff[(size_t)t0] <= (1LL << 22)) ++t1;
+      buf.assign((size_t)(toff[(size_t)t1] - toff[(size_t)t0]), 0.0);
+      for (int t = t0; t < t1; ++t) pk.pack_tile(t, buf.data() + (toff[(size_t)t] - toff[(size_t)t0]));
+      if (h2d(Bt + toff[(size_t)t0], buf.data(), buf.size() * sizeof(double)) != GPMDM_OK)
+        return fail(GPMDM_E_HIP, "upload of the cutoff image");
+      t0 = t1;
+    }
+    return GPMDM_OK;
+  });
+}
+
+int gpmdm_model_obs_cutoff_image(gpmdm_model_t m, int64_t* n, double* out) {
+  CHECK(m && n, "null argument");
+  HIPCHK(hipSetDevice(m->device));
+  if (!m->has_cutoff()) {
+    *n = 0;
+    return GPMDM_OK;
   }
-  if (rc) {
-    m->release_cutoff();
-    return rc;
-  }
-  ci.n_rows = N;
-  ci.n_m = m->D;
-  ci.T_R = pk.T_R;
-  ci.T_M = pk.T_M;
-  m->cut_tau = tau;
-  m->cut2 = -std::log(tau) * (1.0 + 1e-12) + 1e-6;   // margin over both tests' rounding
-  m->t_cut = std::log(tau) * kLog2eX64;
+  long long cnt = 0;
+  HIPCHK(hipMemcpy(&cnt, m->obs_cut.toff + (m->obs_cut.T_R + m->obs_cut.T_M), sizeof(long long), hipMemcpyDeviceToHost));
+  *n = cnt;
+  if (out) HIPCHK(hipMemcpy(out, m->obs_cut.Bt, sizeof(double) * cnt, hipMemcpyDeviceToHost));
   return GPMDM_OK;
 }
 

@@ -624,7 +624,7 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t m) {
 
 int gpmdm_pf_set_obs_cutoff(gpmdm_pf_t pf, int mode) {
   CHECK(pf, "null handle");
-  CHECK(mode >= 0 && mode <= 2, "mode: 0 off, 1 on, 2 on with skip statistics");
+  CHECK(mode >= 0 && mode <= 3, "mode: 0 off, 1 on, 2 on with skip statistics, 3 auto");
   if (pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "set_obs_cutoff between propagate and resample");
   gpmdm_model* m = pf->m;
   HIPCHK(hipSetDevice(m->device));
@@ -648,8 +648,33 @@ int gpmdm_pf_set_obs_cutoff(gpmdm_pf_t pf, int mode) {
     TRY(dalloc(&pf->sp_stats, 2));
     HIPCHK(hipMemset(pf->sp_stats, 0, 2 * sizeof(unsigned long long)));
   }
+  if (mode == 3 && !pf->cut_auto_dev) {
+    void* hv = nullptr;
+    TRY(dalloc(&pf->cut_auto_dev, 2));
+    HIPCHK(hipMemset(pf->cut_auto_dev, 0, 2 * sizeof(unsigned long long)));
+    TRY(halloc(&pf->cut_auto_host, 2, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer(&hv, pf->cut_auto_host, 0));
+    pf->cut_auto_hdev = (unsigned long long*)hv;
+  }
   pf->obs_cutoff = mode != 0;
   pf->sp_stats_on = mode == 2;
+  pf->cut_auto = mode == 3;
+  pf->cut_auto_pending = false;        // (a fresh measurement: the next frame probes)
+  pf->cut_auto_frac = -1.0;
+  return GPMDM_OK;
+}
+
+int gpmdm_pf_obs_cutoff_auto(gpmdm_pf_t pf, int* last_cut, double* fraction) {
+  CHECK(pf, "null handle");
+  if (pf->cut_auto_pending) {          // the last cutoff frame's counters (as the next frame reads them)
+    HIPCHK(pf->wait_readout(pf->cut_auto_seq));
+    const unsigned long long run = __atomic_load_n(pf->cut_auto_host + 0, __ATOMIC_ACQUIRE);
+    const unsigned long long dense = __atomic_load_n(pf->cut_auto_host + 1, __ATOMIC_ACQUIRE);
+    pf->cut_auto_frac = dense ? (double)run / (double)dense : 0.0;
+    pf->cut_auto_pending = false;
+  }
+  if (last_cut) *last_cut = pf->cut_frame ? 1 : 0;
+  if (fraction) *fraction = pf->cut_auto_frac;
   return GPMDM_OK;
 }
 

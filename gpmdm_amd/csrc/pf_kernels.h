@@ -251,6 +251,11 @@ struct ResampleArgs {
   // (F x nb) scanned; slot s's ancestor = max(local[s], block prefix).  nullptr: search.
   int* sys_mark;
   int* sys_block;
+  // the observation cutoff's AUTO policy (gpmdm_pf_set_obs_cutoff mode 3): the cutoff kernel's
+  // MFMA-group counters of this frame, copied by k_readout into mapped host memory (published
+  // with the read-out) and reset; nullptr: not a cutoff frame of an AUTO filter
+  unsigned long long* cut_stats;
+  unsigned long long* cut_stats_host;
 };
 
 // Guide buckets per filter for the inverse-CDF search (P / 4: a resample search then spans

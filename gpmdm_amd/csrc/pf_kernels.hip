@@ -305,7 +305,10 @@ __global__ __launch_bounds__(kB) void k_lead_compact(LeadArgs a) {
 // row is the sum of the leader counts of blocks 0 .. b-1, which the block adds up itself
 // (integers: any order gives k_lead_tables's prefix); block 0 also scans every block's count
 // and writes the leader segment tables with k_lead_tables's row rule.  Same rows, same tables.
-constexpr int kMaxLeadBlocks = 8192;
+// Up to 1024 blocks (P <= 262,144 per launch): each block's prefix re-sum is O(nb) loads and
+// block 0's table is 4 KB of static LDS in every block; above, the two launches (ADVICE r5:
+// at nb = 8192 the re-sums were ~33M loads and a 32 KB table limited occupancy).
+constexpr int kMaxLeadBlocks = 1024;
 __global__ __launch_bounds__(kB) void k_lead_tables_compact(LeadArgs a) {
   __shared__ int red[kB / 64];
   __shared__ int pre[kMaxLeadBlocks];          // block 0: exclusive prefix of every block's count
@@ -1251,6 +1254,12 @@ __global__ __launch_bounds__(1024) void k_readout(ResampleArgs a) {
     }
     readout[tid] = v;
     if (a.readout_host) a.readout_host[f * nro + tid] = v;
+  }
+  if (a.cut_stats && f == 0 && tid == 0) {   // (thread 0: ordered by its own release store)
+    a.cut_stats_host[0] = a.cut_stats[0];
+    a.cut_stats_host[1] = a.cut_stats[1];
+    a.cut_stats[0] = 0;
+    a.cut_stats[1] = 0;
   }
   publish_readout(a, f, tid, tid < nro);
 }

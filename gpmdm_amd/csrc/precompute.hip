@@ -176,7 +176,7 @@ extern "C" int gpmdm_gp_factor(int device, const double* X, int64_t n, int32_t d
 
 // One rocBLAS handle per device, created on first use (handle creation costs milliseconds;
 // a training step at small N costs a few).  rocBLAS manages its own workspace on it.
-static rocblas_handle cached_handle(int device) {
+rocblas_handle cached_handle(int device) {   // (also cutoff_image.hip)
   static std::mutex mu;
   static std::vector<rocblas_handle> handles;
   std::lock_guard<std::mutex> lock(mu);

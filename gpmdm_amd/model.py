@@ -467,33 +467,26 @@ class GPMDM(torch.nn.Module):
             _lib.check(lib.gpmdm_model_create(ctypes.byref(desc), int(dev), ctypes.byref(h)), "gpmdm_model_create")
             self._extra_handles[dev] = h
         if self._obs_cutoff:
-            self._install_obs_cutoff(Ry, beta)
+            self._install_obs_cutoff()
 
-    def _install_obs_cutoff(self, Ry, beta):
-        """The observation GP's cutoff image (gpmdm_model_set_obs_cutoff) on every device
-        image: K_y^-1 = U^-1 U^-T (gpmdm.py:1286-1290, Ry = U^-1) in fp64 -- torch on the host
-        for N <= 4096 as the reference computes it, on the model's GPU above -- and K_y^-1 Y."""
+    def _install_obs_cutoff(self):
+        """The observation GP's cutoff image on every device image, built on the device from
+        the model's own factor (gpmdm_model_build_obs_cutoff: R and K_y^-1 Y read back out of
+        the device image, K_y^-1 = U^-1 U^-T (gpmdm.py:1286-1290) by rocBLAS dsyrk, the
+        tile-major packing by a device kernel; no N x N matrix on the host)."""
         lib = _lib.load()
-        N = Ry.shape[0]
-        with torch.no_grad():
-            R = torch.as_tensor(Ry, dtype=torch.float64)
-            if N > 4096:
-                R = R.to(self.device)
-            K_inv = np.ascontiguousarray((R @ R.T).cpu().numpy())
-            del R
-        beta = np.ascontiguousarray(beta, dtype=np.float64)
         y_absmax = np.ascontiguousarray(np.max(np.abs(np.asarray(self.get_Y(), dtype=np.float64)), axis=0))
         sigma2 = float(torch.exp(self._host("y_log_sigma_n"))) ** 2 + self.sigma_n_num_Y ** 2
         for h in [self._handle] + [self._extra_handles[d] for d in sorted(self._extra_handles)]:
-            _lib.check(lib.gpmdm_model_set_obs_cutoff(h, _lib.dptr(K_inv), _lib.dptr(beta), ctypes.c_double(sigma2),
-                                                      _lib.dptr(y_absmax)), "gpmdm_model_set_obs_cutoff")
+            _lib.check(lib.gpmdm_model_build_obs_cutoff(h, ctypes.c_double(sigma2), _lib.dptr(y_absmax), None, None),
+                       "gpmdm_model_build_obs_cutoff")
 
     def enable_obs_cutoff(self, on: bool = True):
         """Build (or drop) the observation GP's kernel-value cutoff image, which filters use
         with ``GPMDM_PF(..., obs_cutoff=True)`` (DESIGN.md §3 "Kernel-value cutoff": kernel
         values below a provable tau flushed to 0 and the MFMAs of unreachable training rows
-        skipped; results equal the dense filter's to rounding).  Enabling rebuilds the device
-        model once (the factor is not kept on the host)."""
+        skipped; results equal the dense filter's to rounding).  The image is built on the
+        device from the model's own factor (_install_obs_cutoff), and rebuilt with the model."""
         on = bool(on)
         if on == self._obs_cutoff:
             return
@@ -501,7 +494,10 @@ class GPMDM(torch.nn.Module):
         if self._handle is None:
             return                                  # built with the model
         if on:
-            self._precompute_kernel_inverses()
+            gen = self.generation
+            self._refresh()                         # (a rebuilt model installs the image itself)
+            if self.generation == gen:
+                self._install_obs_cutoff()
         else:
             lib = _lib.load()
             for h in [self._handle] + list(self._extra_handles.values()):

@@ -148,7 +148,9 @@ class GPMDM_PF:
         if dyn_tiles not in _lib.DYN_TILES:
             raise ValueError("dyn_tiles must be 'auto', 'narrow' or 'wide'")
 
-        self._obs_cutoff = 1 if obs_cutoff else 0
+        if isinstance(obs_cutoff, str) and obs_cutoff != "auto":
+            raise ValueError("obs_cutoff: True, False or 'auto'")
+        self._obs_cutoff = 3 if obs_cutoff == "auto" else (1 if obs_cutoff else 0)
         if obs_cutoff:
             gpmdm.enable_obs_cutoff(True)       # the model's cutoff image (built once)
 
@@ -541,24 +543,39 @@ class GPMDM_PF:
 
     _CUT_SPLIT = {"auto": 0, "none": 1, "all": 2, "tail": 3}
 
-    def set_obs_cutoff(self, on: bool = True, stats: bool = False, split: str | None = None):
+    def set_obs_cutoff(self, on=True, stats: bool = False, split: str | None = None):
         """Run the observation GP with the model's kernel-value cutoff (GPMDM.enable_obs_cutoff,
-        built here if needed) or the dense kernel; ``stats`` also counts the MFMA groups run
-        (obs_cutoff_stats); ``split`` ("auto" default, "none", "all", "tail") schedules the
-        particle tiles run as two workgroups each (gpmdm_pf_set_obs_cutoff_split; the same
-        results under every policy).  Between frames only."""
+        built here if needed) or the dense kernel; ``on="auto"``: per frame, the cutoff while
+        the reach it measured on its last frame is below its break-even against the dense
+        kernel, else the dense kernel (re-measured at least every 8 frames; one-rank filters,
+        gpmdm_pf_set_obs_cutoff mode 3); ``stats`` also counts the MFMA groups run
+        (obs_cutoff_stats; not with "auto"); ``split`` ("auto" default, "none", "all", "tail")
+        schedules the particle tiles run as two workgroups each (gpmdm_pf_set_obs_cutoff_split;
+        the same results under every policy).  Between frames only."""
         if split is not None and split not in self._CUT_SPLIT:
             raise ValueError(f"split: one of {sorted(self._CUT_SPLIT)}")
+        if isinstance(on, str) and on != "auto":
+            raise ValueError("on: True, False or 'auto'")
+        if on == "auto" and stats:
+            raise ValueError("stats count the cutoff's work of every frame: not with on='auto'")
         if on:
             self._gpmdm.enable_obs_cutoff(True)
             self._sync_model()
-        mode = (2 if stats else 1) if on else 0
+        mode = 3 if on == "auto" else ((2 if stats else 1) if on else 0)
         lib = _lib.load()
         for h in [self._h] + [p[0] for p in self._peers]:
             _lib.check(lib.gpmdm_pf_set_obs_cutoff(h, mode), "set_obs_cutoff")
             if split is not None:
                 _lib.check(lib.gpmdm_pf_set_obs_cutoff_split(h, self._CUT_SPLIT[split]), "set_obs_cutoff")
         self._obs_cutoff = mode
+
+    def obs_cutoff_auto(self) -> dict:
+        """AUTO cutoff state: whether the last frame ran the cutoff kernel, and the fraction of
+        the dense MFMA work it ran on its last cutoff frame (None: not measured yet)."""
+        last, frac = ctypes.c_int(), ctypes.c_double()
+        _lib.check(_lib.load().gpmdm_pf_obs_cutoff_auto(self._h, ctypes.byref(last), ctypes.byref(frac)),
+                   "obs_cutoff_auto")
+        return {"last_frame_cutoff": bool(last.value), "fraction_run": frac.value if frac.value >= 0 else None}
 
     def obs_cutoff_stats(self, reset: bool = True) -> dict:
         """MFMA groups (16-particle x 16-column tile x 16-row K-step) the cutoff kernel ran since

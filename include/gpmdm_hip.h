@@ -376,7 +376,9 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t model);
  *   beta      N x D row-major, K_y^-1 Y (the mean weights, gpmdm.py:955-957)
  *   sigma2    the noise variance on K_y's diagonal (exp(y_log_sigma_n)^2 + sigma_n_num_Y^2)
  *   y_absmax  D values, max_i |Y_ij|
- * (K_inv = NULL removes it); gpmdm_model_obs_cutoff returns tau (0: none).  A filter uses it
+ * (K_inv = NULL removes it); gpmdm_model_obs_cutoff returns tau (0: none).  The call waits
+ * for the last frame of every filter built on the model, not for the device: none of them
+ * may be inside a frame or stepping on another thread meanwhile.  A filter uses it
  * after gpmdm_pf_set_obs_cutoff(pf, 1) (2: also count the MFMA groups run against the dense
  * kernel's, read and optionally reset by gpmdm_pf_obs_cutoff_stats; 0: the dense kernel).
  * Results are the dense filter's to rounding (not bit for bit), and do not depend on the
@@ -384,8 +386,29 @@ int gpmdm_pf_set_model(gpmdm_pf_t pf, gpmdm_model_t model);
  * rows); GPMDM_E_INVALID otherwise. */
 int gpmdm_model_set_obs_cutoff(gpmdm_model_t model, const double* K_inv, const double* beta, double sigma2,
                                const double* y_absmax);
+/* The same image built on the model's device from the model's own observation factor: R and
+ * K_y^-1 Y are read back out of the device image, K_y^-1 = R R^T is formed by rocBLAS dsyrk
+ * and the image is packed by a device kernel (only tau, the spatial order and the K-step
+ * spheres are computed on the host, from X and the column sums of K_y^-1 Y).  Byte-equal to
+ * gpmdm_model_set_obs_cutoff's image for the same K_y^-1.  kinv_out (N x N) and m_out (N x D)
+ * are optional host copies of the K_y^-1 and K_y^-1 Y it packed (tests).  Like
+ * gpmdm_model_set_obs_cutoff: no filter on the model may be inside a frame or stepping on
+ * another thread during the call (the filters' last frames are waited for, not the device). */
+int gpmdm_model_build_obs_cutoff(gpmdm_model_t model, double sigma2, const double* y_absmax, double* kinv_out,
+                                 double* m_out);
+/* The cutoff image's doubles (*n = their count; out = NULL: the count only).  Tests. */
+int gpmdm_model_obs_cutoff_image(gpmdm_model_t model, int64_t* n, double* out);
 int gpmdm_model_obs_cutoff(gpmdm_model_t model, double* tau);
 int gpmdm_pf_set_obs_cutoff(gpmdm_pf_t pf, int mode);
+/* mode 3 = AUTO: per frame the cutoff kernel while the fraction of the dense MFMA work it ran
+ * on its last frame is at most 0.75 (its break-even against the dense kernel), else the
+ * dense kernel, with a cutoff frame at least every 8 frames to measure again.  The counts
+ * travel with the frame's read-out, so the choice is a function of the filter's own
+ * trajectory (deterministic).  Single-rank filters and banks whose read-outs are mapped (up
+ * to ~800 filters) with more than 1024 particles per filter; others run mode 1 (a rank-local
+ * choice would make a particle's result depend on its rank).  gpmdm_pf_obs_cutoff_auto: did
+ * the last frame run the cutoff, and the last measured fraction (< 0: none yet). */
+int gpmdm_pf_obs_cutoff_auto(gpmdm_pf_t pf, int* last_cut, double* fraction);
 int gpmdm_pf_obs_cutoff_stats(gpmdm_pf_t pf, int64_t* run, int64_t* dense, int reset, void* stream);
 /* Scheduling of the cutoff kernel's particle tiles (results are identical under every
  * policy): a split tile runs as two workgroups.  GPMDM_CUT_SPLIT_AUTO (default): every tile

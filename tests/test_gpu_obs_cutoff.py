@@ -338,3 +338,108 @@ def test_cutoff_logical_shards_other_latent_dims(synth_cut):
             b = pf.export_state()
             for key in ("states", "classes", "ll", "resample_idx"):
                 assert np.array_equal(a[key], b[key]), (d, k, key)
+
+
+@pytest.mark.parametrize("which", ["config1", "config2"])
+def test_device_cutoff_image_is_byte_equal_to_the_host_packer(fx_config1, fx_config2, which):
+    """the cutoff image built on the device (gpmdm_model_build_obs_cutoff: R and
+    K_y^-1 Y read back out of the device image, K_y^-1 = R R^T by dsyrk, the tile-major
+    packing by a kernel) is byte for byte the host packer's image (host_image.h CutoffPacker,
+    gpmdm_model_set_obs_cutoff) of the same K_y^-1 and K_y^-1 Y, with the same tau; the
+    K_y^-1 it formed is the reference's U^-1 U^-T (gpmdm.py:1286-1290) to rounding."""
+    import ctypes
+    from gpmdm_amd import _lib
+    m = product_model(fx_config1 if which == "config1" else fx_config2)
+    lib = _lib.load()
+    h = m.handle
+    N, D = m.X.shape[0], m.D
+    y_absmax = np.ascontiguousarray(np.max(np.abs(np.asarray(m.get_Y(), dtype=np.float64)), axis=0))
+    sigma2 = float(torch.exp(m.y_log_sigma_n.detach().cpu())) ** 2 + m.sigma_n_num_Y ** 2
+    K = np.zeros((N, N))
+    M = np.zeros((N, D))
+    _lib.check(lib.gpmdm_model_build_obs_cutoff(h, ctypes.c_double(sigma2), _lib.dptr(y_absmax), _lib.dptr(K),
+                                                _lib.dptr(M)), "build")
+    tau_dev = m.obs_cutoff_tau
+    n = ctypes.c_int64()
+    _lib.check(lib.gpmdm_model_obs_cutoff_image(h, ctypes.byref(n), None), "image size")
+    img_dev = np.zeros(n.value)
+    _lib.check(lib.gpmdm_model_obs_cutoff_image(h, ctypes.byref(n), _lib.dptr(img_dev)), "image")
+    _lib.check(lib.gpmdm_model_set_obs_cutoff(h, _lib.dptr(K), _lib.dptr(M), ctypes.c_double(sigma2),
+                                              _lib.dptr(y_absmax)), "host packer")
+    img_host = np.zeros(n.value)
+    _lib.check(lib.gpmdm_model_obs_cutoff_image(h, ctypes.byref(n), _lib.dptr(img_host)), "image")
+    assert m.obs_cutoff_tau == tau_dev
+    assert img_dev.tobytes() == img_host.tobytes()
+    # K^-1 against the oracle's explicit inverse of K_y (the reference's recipe)
+    om = oracle_model(fx_config1 if which == "config1" else fx_config2)
+    assert np.max(np.abs(K - om.Ky_inv)) <= 1e-6 * np.max(np.abs(om.Ky_inv))
+    assert np.array_equal(K, K.T)
+    _lib.check(lib.gpmdm_model_set_obs_cutoff(h, None, None, ctypes.c_double(0.0), None), "remove")
+
+
+def _auto_vs_hand_switched(m, T, P, zs, init=None, seed=11):
+    """Run an AUTO filter (obs_cutoff="auto") beside a mode-1 filter switched by hand
+    (set_obs_cutoff) through the AUTO filter's per-frame choices: every choice must follow the
+    rule (a cutoff frame when no fraction is known, 8 frames after the last cutoff frame, or
+    when the last measured fraction is <= 0.75) and every frame must be bitwise equal."""
+    from gpmdm_amd import GPMDM_PF
+    filters = []
+    for mode in ("auto", True):
+        torch.manual_seed(4)
+        pf = GPMDM_PF(m, T, P, rng="philox", seed=seed, obs_cutoff=mode)
+        if init is not None:
+            pf.load_state(*init[:2], ll=init[2], log_w=init[2], w=init[3], frame=0)
+        filters.append(pf)
+    a, b = filters
+    choices, fracs = [], []
+    last_probe, frac = None, None
+    for k, z in enumerate(zs):
+        a.update(z)
+        cut = a.obs_cutoff_auto()["last_frame_cutoff"]
+        expect = frac is None or k - last_probe >= 8 or frac <= 0.75
+        assert cut == expect, (k, cut, frac, last_probe)
+        if cut:
+            last_probe = k
+            frac = a.obs_cutoff_auto()["fraction_run"]
+        choices.append(cut)
+        fracs.append(frac)
+        b.set_obs_cutoff(bool(cut))
+        b.update(z)
+        sa, sb = a.export_state(), b.export_state()
+        for key in ("states", "classes", "ll", "resample_idx"):
+            assert np.array_equal(sa[key], sb[key]), (k, key, choices)
+    return choices, fracs
+
+
+def test_cutoff_auto_on_the_benchmark_stream(m2c):
+    """AUTO (gpmdm_pf_set_obs_cutoff mode 3) on the bench's stream: the initial cloud (drawn
+    from every training latent) reaches every K-step, so after the first probe the dense kernel
+    runs; the next probe (frame 8) finds the collapsed cloud's low reach and the cutoff runs
+    from there on."""
+    from gpmdm_amd import synthetic
+    data = synthetic.make_sequences(2, 5, 200, 62, 3, seed=0)
+    zs = data.observation_stream(12, seed=1)
+    T = torch.tensor(synthetic.markov_matrix(2))
+    choices, fracs = _auto_vs_hand_switched(m2c, T, 100_000, zs)
+    assert choices[0] and not all(choices[1:8]), (choices, fracs)
+    assert all(choices[8:]) and fracs[-1] < 0.75, (choices, fracs)
+
+
+def test_cutoff_auto_on_a_spread_cloud(m2c):
+    """AUTO from a cloud spread over the training set (2000 ancestors, 0.5 l): the probe's
+    reach is above the break-even, so the dense kernel runs until the next probe or until the
+    cloud has collapsed; bitwise a hand-switched filter through the same choices."""
+    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]])
+    P = 20_000
+    X = m2c.X.detach().cpu().numpy()
+    g = np.random.RandomState(23)
+    anc = g.choice(X.shape[0], 2000, replace=False)
+    owner = anc[(np.arange(P) * anc.size) // P]
+    cls_of = np.concatenate([np.full(m2c.get_X_for_class(c).shape[0], c) for c in range(2)])
+    states = np.ascontiguousarray(X[owner] + 0.5 * g.randn(P, X.shape[1]))
+    classes = cls_of[owner].astype(np.int64)
+    Y = m2c.get_Y()
+    zs = [np.asarray(Y[100 + 5 * k], dtype=np.float64) for k in range(12)]
+    choices, fracs = _auto_vs_hand_switched(m2c, T, P, zs, init=(states, classes, np.zeros(P), np.full(P, 1.0 / P)),
+                                            seed=5)
+    assert choices[0] and fracs[0] > 0.75 and not all(choices), (choices, fracs)
