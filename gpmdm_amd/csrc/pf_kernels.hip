@@ -1255,13 +1255,13 @@ __global__ __launch_bounds__(1024) void k_readout(ResampleArgs a) {
     readout[tid] = v;
     if (a.readout_host) a.readout_host[f * nro + tid] = v;
   }
-  if (a.cut_stats && f == 0 && tid == 0) {   // (thread 0: ordered by its own release store)
-    a.cut_stats_host[0] = a.cut_stats[0];
-    a.cut_stats_host[1] = a.cut_stats[1];
-    a.cut_stats[0] = 0;
-    a.cut_stats[1] = 0;
+  // the AUTO cutoff's counters of this frame, one per lane (8-byte stores: the ISA guard)
+  const bool cst = a.cut_stats && f == 0 && tid < 2;
+  if (cst) {
+    a.cut_stats_host[tid] = a.cut_stats[tid];
+    a.cut_stats[tid] = 0;
   }
-  publish_readout(a, f, tid, tid < nro);
+  publish_readout(a, f, tid, tid < nro || cst);
 }
 
 
