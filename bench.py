@@ -151,7 +151,7 @@ def obs_model_bytes(N, D):
 def pmc_traffic(cfg):
     """(HBM bytes per launch of the obs tile kernel, source note) from the committed
     rocprofv3 PMC summary of this bench command (tools/pmc_passes.sh + tools/pmc_summary.py)."""
-    for name in ("r05_pmc_summary.json", "r04_pmc_summary.json", "r03_pmc_summary.json", "r02_pmc_summary.json", "pmc_summary.json"):
+    for name in ("r06_pmc_summary.json", "r05_pmc_summary.json", "r04_pmc_summary.json", "r03_pmc_summary.json", "r02_pmc_summary.json", "pmc_summary.json"):
         p = ROOT / "profiles" / name
         if not p.exists():
             continue
