@@ -627,8 +627,18 @@ def library_comm(world, rank, local, group, device):
     broadcast over the process group."""
     from gpmdm_amd import _lib
     from gpmdm_amd.distributed import RcclComm, broadcast_array
-    uid = RcclComm.unique_id() if rank == 0 else bytes(_lib.GPMDM_COMM_ID_BYTES)
+    uid = bytes(_lib.GPMDM_COMM_ID_BYTES)
+    err = None
+    if rank == 0:
+        try:
+            uid = RcclComm.unique_id()
+        except Exception as e:  # noqa: BLE001  (the others still get the broadcast: all zeros)
+            err = e
     uid = broadcast_array(np.frombuffer(uid, dtype=np.uint8).copy(), group, device).tobytes()
+    if err is not None:
+        raise err
+    if not any(uid):
+        raise RuntimeError("rank 0 could not make an RCCL unique id")
     return RcclComm(world, rank, uid, local)
 
 
@@ -1090,6 +1100,13 @@ def main():
                 comm = library_comm(world, rank, local, group, device)
             except Exception as e:  # noqa: BLE001
                 libx = {"exchange": "gpmdm_pf_set_comm", "error": repr(e)[:400]}
+        # every rank must hold a communicator before any enters the library's collectives (a
+        # rank that failed alone would leave the others waiting in RCCL, which has no timeout)
+        ok = torch.tensor([1 if comm is not None else 0], dtype=torch.int32, device=device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if int(ok.item()) == 0 and comm is not None:
+            libx = {"exchange": "gpmdm_pf_set_comm", "error": "another rank could not make its communicator"}
+            comm = None
         if comm is not None:
             try:    # an error here is reported in the line, not in place of the headline
                 libx = library_exchange_line(new_filter, zs, min(args.steps, args.library_steps), dist, device,
