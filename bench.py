@@ -42,7 +42,7 @@ Prints ONE JSON line (rank 0) with the contract fields plus:
                 per particle; SURVEY §8(d)'s dense 2N^2 + 2ND is reported beside it) / mean
                 launch time from HIP events on the launch stream; traffic = HBM bytes per
                 launch of the same kernel from the committed rocprofv3 PMC passes of this
-                bench command (profiles/r05_pmc_summary.json; its "commit" field names the
+                bench command (profiles/r06_pmc_summary.json; its "commit" field names the
                 build it measured -- the driver's bench run has no profiler attached), or null
   cpu_baseline  the CPU oracle (numpy fp64) on this configuration's own particle count
                 for N <= 2000 (a bounded sample of frames), a 1000-particle sample above;
