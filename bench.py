@@ -914,6 +914,10 @@ def main():
     ap.add_argument("--cutoff-spread", action="store_true",
                     help="only the cutoff-vs-dense observation launch on spread clouds of >= 1000 ancestors "
                          "(cutoff_spread_line; one GPU), one JSON line with its rows; not a headline run")
+    ap.add_argument("--cutoff-spread-at", type=float, nargs="+", default=[0.05, 0.2, 0.5],
+                    help="the spreads (x the observation lengthscale) of --cutoff-spread")
+    ap.add_argument("--cutoff-spread-reps", type=int, default=4,
+                    help="timed launches per spread and kernel of --cutoff-spread (after one warm-up)")
     ap.add_argument("--dyn-tiles", default="auto", choices=("auto", "narrow", "wide"),
                     help="dynamics tile shape of the headline filter (gpmdm_pf_set_dyn_tiles)")
     argv = sys.argv[1:]
@@ -1009,7 +1013,8 @@ def main():
         if world > 1:
             log("[bench] --cutoff-spread runs on one GPU")
             sys.exit(2)
-        res = cutoff_spread_line(model, T, P_total, zs)
+        res = cutoff_spread_line(model, T, P_total, zs, spreads=tuple(args.cutoff_spread_at),
+                                 reps=args.cutoff_spread_reps)
         print(json.dumps({"metric": "observation launch ms, dense vs cutoff, spread clouds",
                           "config": {"workload": f"configs[{WORKLOAD['cfg'] - 1}]", "N": int(model.X.shape[0]),
                                      "D": WORKLOAD["D"], "d": WORKLOAD["d"], "C": WORKLOAD["C"], "P": P_total},

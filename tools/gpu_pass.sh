@@ -16,6 +16,8 @@
 #        at each config, the config-2 cutoff line, and the bits of a 5-frame cutoff trajectory)
 #   bash tools/gpu_pass.sh cutoff-pmc <tag>
 #        PMC passes of the config-2 bench with its cutoff line (dense and cutoff kernels)
+#   bash tools/gpu_pass.sh spread-pmc <tag> [config] [spread]
+#        PMC passes of one dense and one cutoff launch from a spread cloud (default config 5, 0.2 l)
 #   bash tools/gpu_pass.sh configs <tag> [configs...]
 #        bench.py on the other BASELINE configurations with their cpu_baseline (default 3 4 5)
 # Output under gpurun_out/<tag>/; COMMIT (the evidence commit) stamps the summaries.
@@ -125,6 +127,16 @@ cutoff-pmc)
     "$COUNTERS_A" "$COUNTERS_B" || exit 1
   python tools/pmc_summary.py $out/pmc --commit "$commit" \
     --command "bench.py --steps 2 --warmup 1 --no-cpu-baseline --spread-steps 0 --replay-steps 0 --no-nodedup --cutoff-steps 2" \
+    --out $out/pmc_summary.json > $out/pmc_summary.txt 2>&1 || { echo "pmc summary failed"; exit 1; }
+  ;;
+spread-pmc)
+  # PMC passes of one spread-cloud dense + cutoff launch pair: spread-pmc <tag> <config> [spread]
+  c=${1:-5}; sp=${2:-0.2}
+  args="--config $c --cutoff-spread --cutoff-spread-at $sp --cutoff-spread-reps 1"
+  BENCH_ARGS="$args" bash tools/pmc_passes.sh $out/pmc "FETCH_SIZE" "WRITE_SIZE" \
+    "$COUNTERS_A" "$COUNTERS_B" || exit 1
+  python tools/pmc_summary.py $out/pmc --commit "$commit" \
+    --command "bench.py --steps 2 --warmup 1 --no-cpu-baseline $args" \
     --out $out/pmc_summary.json > $out/pmc_summary.txt 2>&1 || { echo "pmc summary failed"; exit 1; }
   ;;
 configs)
