@@ -350,7 +350,7 @@ def spread_line(device, steps, warmup=5, y_lambda=SPREAD_LAMBDA, dyn_tiles="auto
                     "(ms_per_step includes them)"}
 
 
-def cutoff_line(model, T, P, zs, warmup, steps, headline_ms=None, headline_obs_ms=None):
+def cutoff_line(model, T, P, zs, warmup, steps, headline_ms=None, headline_obs_ms=None, split=None):
     """The same step with the observation GP's opt-in kernel-value cutoff
     (GPMDM_PF(obs_cutoff=True)): kernel values below the model's tau flushed to
     0 and the unreachable 16-row K-steps skipped.  A timed pass (the roofline kernel's events
@@ -365,6 +365,8 @@ def cutoff_line(model, T, P, zs, warmup, steps, headline_ms=None, headline_obs_m
     setup_s = time.perf_counter() - t0
     torch.manual_seed(11)
     pf = GPMDM_PF(model, T, P, rng="philox", seed=11, obs_cutoff=True)
+    if split is not None:
+        pf.set_obs_cutoff(True, split=split)
 
     def frame(k):
         pf.update(zs[k])
@@ -430,7 +432,7 @@ def cutoff_line(model, T, P, zs, warmup, steps, headline_ms=None, headline_obs_m
     return out
 
 
-def cutoff_spread_line(model, T, P, zs, spreads=(0.05, 0.2, 0.5), n_anc=2000, reps=4):
+def cutoff_spread_line(model, T, P, zs, spreads=(0.05, 0.2, 0.5), n_anc=2000, reps=4, split=None):
     """The cutoff on clouds that are NOT one ancestor: n_anc distinct training
     latents as ancestors (each with its class), P / n_anc particles around each, offset by
     spread x the observation GP's lengthscale x N(0, 1) per coordinate, contiguous per ancestor
@@ -453,6 +455,8 @@ def cutoff_spread_line(model, T, P, zs, spreads=(0.05, 0.2, 0.5), n_anc=2000, re
     base = X[owner]
     classes = cls_of[owner].astype(np.int64)
     filt = {cut: GPMDM_PF(model, T, P, rng="philox", seed=11, obs_cutoff=cut) for cut in (False, True)}
+    if split is not None:
+        filt[True].set_obs_cutoff(True, split=split)
     zero, unif = np.zeros(P), np.full(P, 1.0 / P)   # the reference's initial weights (gpmdm_pf.py:100-104)
     rows = []
     for sp in spreads:
@@ -916,6 +920,8 @@ def main():
                          "(cutoff_spread_line; one GPU), one JSON line with its rows; not a headline run")
     ap.add_argument("--cutoff-spread-at", type=float, nargs="+", default=[0.05, 0.2, 0.5],
                     help="the spreads (x the observation lengthscale) of --cutoff-spread")
+    ap.add_argument("--cutoff-split", default=None, choices=("auto", "none", "all", "tail", "chunks"),
+                    help="the cutoff filters' tile scheduling (gpmdm_pf_set_obs_cutoff_split; default auto)")
     ap.add_argument("--cutoff-spread-reps", type=int, default=4,
                     help="timed launches per spread and kernel of --cutoff-spread (after one warm-up)")
     ap.add_argument("--dyn-tiles", default="auto", choices=("auto", "narrow", "wide"),
@@ -1014,7 +1020,7 @@ def main():
             log("[bench] --cutoff-spread runs on one GPU")
             sys.exit(2)
         res = cutoff_spread_line(model, T, P_total, zs, spreads=tuple(args.cutoff_spread_at),
-                                 reps=args.cutoff_spread_reps)
+                                 reps=args.cutoff_spread_reps, split=args.cutoff_split)
         print(json.dumps({"metric": "observation launch ms, dense vs cutoff, spread clouds",
                           "config": {"workload": f"configs[{WORKLOAD['cfg'] - 1}]", "N": int(model.X.shape[0]),
                                      "D": WORKLOAD["D"], "d": WORKLOAD["d"], "C": WORKLOAD["C"], "P": P_total},
@@ -1133,7 +1139,7 @@ def main():
     if args.cutoff_steps and world == 1 and len(zs) >= args.warmup + args.cutoff_steps + 10:
         try:   # reported beside the headline, never in place of it
             cut = cutoff_line(model, T, P_total, zs, args.warmup, args.cutoff_steps, elapsed / args.steps * 1e3,
-                              obs_launch_s * 1e3)
+                              obs_launch_s * 1e3, split=args.cutoff_split)
         except Exception as e:  # noqa: BLE001
             cut = {"error": repr(e)[:400]}
     achieved = alg * P_local / obs_launch_s / 1e12

@@ -415,8 +415,9 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
     bool cut = pf->obs_cutoff && m->has_cutoff();
     // AUTO (gpmdm_pf::cut_auto): the cutoff while the reach it last measured is below the
     // break-even, a cutoff frame at least every kCutAutoProbe frames to measure it again
+    // (mode 1 measures its reach the same way, for the split policy's chunk grid)
     bool auto_frame = false;
-    if (cut && pf->cut_auto_active() && !small_resample_ok(norm_args(pf), resample_args(pf))) {
+    if (cut && pf->cut_measure_active() && !small_resample_ok(norm_args(pf), resample_args(pf))) {
       if (pf->cut_auto_pending) {      // the last cutoff frame's counters, published with its read-out
         HIPCHK(pf->wait_readout(pf->cut_auto_seq));
         const unsigned long long run = __atomic_load_n(pf->cut_auto_host + 0, __ATOMIC_ACQUIRE);
@@ -424,10 +425,12 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
         pf->cut_auto_frac = dense ? (double)run / (double)dense : 0.0;
         pf->cut_auto_pending = false;
       }
-      const bool probe = pf->cut_auto_frac < 0.0 || (long long)pf->frame - pf->cut_auto_probe >= gpmdm_pf::kCutAutoProbe;
-      cut = probe || pf->cut_auto_frac <= gpmdm_pf::kCutAutoMaxRun;
+      if (pf->cut_auto) {
+        const bool probe = pf->cut_auto_frac < 0.0 || (long long)pf->frame - pf->cut_auto_probe >= gpmdm_pf::kCutAutoProbe;
+        cut = probe || pf->cut_auto_frac <= gpmdm_pf::kCutAutoMaxRun;
+        if (cut) pf->cut_auto_probe = pf->frame;
+      }
       auto_frame = cut;
-      if (cut) pf->cut_auto_probe = pf->frame;
     }
     pf->cut_frame = cut;
     pf->cut_frame_auto = auto_frame;
@@ -477,11 +480,19 @@ int weigh(gpmdm_pf* pf, const double* zh, hipStream_t s) {
       const int slots = cutoff_slots(d);
       // list entries a second part can hold (all but the first chunk's, at least one)
       const long long entries = (long long)ci.T_R + ci.T_M - 1;
-      int n_split = cut_split_tiles(pf, tiles, slots, (size_t)entries * tiles * PT * sizeof(double));
+      // the chunk grid by request, or under AUTO when the filter's last measured reach is high
+      // (every tile's list then spans several chunks: measured 4-7 % faster at reaches 0.68-0.91,
+      // 2 % slower at 0.07-0.23, where most chunk workgroups find no chunk)
+      const bool grid = (pf->cut_split_policy == GPMDM_CUT_SPLIT_CHUNKS ||
+                         (pf->cut_split_policy == GPMDM_CUT_SPLIT_AUTO && pf->cut_auto_frac >= gpmdm_pf::kCutChunksMin)) &&
+                        ci.T_R + ci.T_M > TPC;
+      int n_split = grid ? tiles : cut_split_tiles(pf, tiles, slots, (size_t)entries * tiles * PT * sizeof(double));
       if (ci.T_R + ci.T_M <= TPC) n_split = 0;   // one chunk: nothing to split
       if (n_split > 0) TRY(pf->ensure_cut_split((size_t)entries * n_split * PT, n_split, s));
       cp.n_whole = tiles - n_split;
       cp.n_split = n_split;
+      cp.chunk_grid = grid ? 1 : 0;
+      cp.n_chunk_max = (int)cdiv(ci.T_R + ci.T_M, TPC);
       cp.part = pf->cut_part;
       cp.ld_part = (long long)n_split * PT;
       cp.split = pf->cut_split;

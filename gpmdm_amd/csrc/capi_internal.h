@@ -260,7 +260,13 @@ struct gpmdm_pf {
   long long cut_auto_probe = -(1LL << 40);         // the frame of the last cutoff frame
   bool cut_frame = false;                          // this frame's observation GP is the cutoff's
   bool cut_frame_auto = false;                     // ... an AUTO filter's (its counters go with the read-out)
-  bool cut_auto_active() const { return cut_auto && obs_cutoff && n_ranks == 1 && seq_pin != nullptr; }
+  // the counters run on every cutoff frame of a one-rank filter with mapped read-outs (modes 1
+  // and 3): AUTO's choice of kernel, and the split policy's choice of the chunk grid
+  bool cut_measure_active() const {
+    return obs_cutoff && !sp_stats_on && n_ranks == 1 && seq_pin != nullptr && cut_auto_dev != nullptr;
+  }
+  bool cut_auto_active() const { return cut_auto && cut_measure_active(); }
+  static constexpr double kCutChunksMin = 0.5;     // GPMDM_CUT_SPLIT_AUTO: the chunk grid from this reach
   // the cutoff kernel's split tiles (capi_frame.hip): second parts' partials, (n_act, c*) per
   // split tile; grown on demand
   int cut_split_policy = GPMDM_CUT_SPLIT_AUTO;

@@ -648,7 +648,7 @@ int gpmdm_pf_set_obs_cutoff(gpmdm_pf_t pf, int mode) {
     TRY(dalloc(&pf->sp_stats, 2));
     HIPCHK(hipMemset(pf->sp_stats, 0, 2 * sizeof(unsigned long long)));
   }
-  if (mode == 3 && !pf->cut_auto_dev) {
+  if ((mode == 1 || mode == 3) && !pf->cut_auto_dev) {
     void* hv = nullptr;
     TRY(dalloc(&pf->cut_auto_dev, 2));
     HIPCHK(hipMemset(pf->cut_auto_dev, 0, 2 * sizeof(unsigned long long)));
@@ -681,8 +681,8 @@ int gpmdm_pf_obs_cutoff_auto(gpmdm_pf_t pf, int* last_cut, double* fraction) {
 int gpmdm_pf_set_obs_cutoff_split(gpmdm_pf_t pf, int policy) {
   CHECK(pf, "null handle");
   CHECK(policy == GPMDM_CUT_SPLIT_AUTO || policy == GPMDM_CUT_SPLIT_NONE || policy == GPMDM_CUT_SPLIT_ALL ||
-            policy == GPMDM_CUT_SPLIT_TAIL,
-        "policy: GPMDM_CUT_SPLIT_AUTO, _NONE, _ALL or _TAIL");
+            policy == GPMDM_CUT_SPLIT_TAIL || policy == GPMDM_CUT_SPLIT_CHUNKS,
+        "policy: GPMDM_CUT_SPLIT_AUTO, _NONE, _ALL, _TAIL or _CHUNKS");
   if (pf->dyn_done || pf->propagated) return fail(GPMDM_E_STATE, "set_obs_cutoff_split between propagate and resample");
   pf->cut_split_policy = policy;
   return GPMDM_OK;

@@ -75,6 +75,9 @@ struct CutoffParams {
   double* part;
   long long ld_part;
   int2* split;               // per split tile: (n_act, c*), written by its first workgroup
+  // chunk grid (GPMDM_CUT_SPLIT_CHUNKS): every tile split at c* = 1 and every chunk its own
+  // workgroup, n_chunk_max x n_split of them, chunk-major from each list's end (heavy first)
+  int chunk_grid, n_chunk_max;
 };
 bool launch_obs_cutoff(const CutoffParams& p, int d, hipStream_t stream);   // false: bad shape
 int cutoff_tile_particles(int d);   // PT of the cutoff kernel at d

@@ -97,7 +97,11 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
   // the workgroup's particle tile and part: whole tiles first, then the split tiles' second
   // parts (the longer ones in the balanced split's usual case), then their first parts
   int tile = (int)blockIdx.x, part = -1;                      // -1: the whole tile
-  if (tile >= prm.n_whole) {
+  int cfe = 0;                                                // chunk grid: chunk from the list's end
+  if (prm.chunk_grid) {
+    cfe = tile / prm.n_split;
+    tile -= cfe * prm.n_split;
+  } else if (tile >= prm.n_whole) {
     const int r = tile - prm.n_whole;
     part = r < prm.n_split ? 1 : 0;
     tile = prm.n_whole + (r < prm.n_split ? r : r - prm.n_split);
@@ -193,7 +197,15 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
   // the chunks [c_lo, c_hi) of the tile list this workgroup runs (none: a second part of a
   // tile below two chunks; no early exit, which costs the K loop registers)
   int c_lo = 0, c_hi = (n_tiles + TPC - 1) / TPC;
-  if (part >= 0) {
+  if (prm.chunk_grid) {
+    // chunk c = nc - 1 - cfe alone: chunk 0 as a split tile's first part (q, S and the split
+    // record (n_act, 1)), a later one as a second part writing its entries; none past the list
+    const int c = c_hi - 1 - cfe;
+    part = c == 0 ? 0 : 1;
+    c_lo = c < 0 ? 0 : c;
+    c_hi = c < 0 ? 0 : c + 1;
+    if (c == 0 && tid == 0) prm.split[tile] = make_int2(n_act, 1);
+  } else if (part >= 0) {
     const int cs = __builtin_amdgcn_readfirstlane(cutoff_split_chunk(n_act, prm.T_M, TPC));
     if (part == 0) {
       c_hi = cs;
@@ -483,9 +495,12 @@ bool launch_cut_d(const CutoffParams& p, hipStream_t s) {
   constexpr int PT = DI <= 8 ? 32 : 64;
   // grid: the whole tiles, then two workgroups per split tile (capi_frame.hip sets n_whole +
   // n_split = the tile count)
-  const unsigned grid = (unsigned)(p.n_whole + 2 * p.n_split);
+  const unsigned grid = p.chunk_grid ? (unsigned)(p.n_chunk_max * p.n_split) : (unsigned)(p.n_whole + 2 * p.n_split);
   if (p.n_whole < 0 || p.n_split < 0 || (long long)(p.n_whole + p.n_split) * PT < n ||
       (long long)(p.n_whole + p.n_split - 1) * PT >= n || (p.n_split > 0 && (!p.part || !p.split)))
+    return false;
+  if (p.chunk_grid && (p.n_whole != 0 || p.n_split <= 0 || p.n_chunk_max <= 0 ||
+                       (long long)p.n_chunk_max * cutoff_tile_list_chunk() < p.T_R + p.T_M))
     return false;
   if constexpr (DI <= 8)
     hipLaunchKernelGGL((k_obs_cutoff<DI, 4, 2, 8>), dim3(grid), dim3(256), 0, s, p);

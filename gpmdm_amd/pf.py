@@ -541,7 +541,7 @@ class GPMDM_PF:
         self.load_state(st["states"], st["classes"], ll=st["ll"], log_w=st["log_w"], w=st["w"],
                         resample_idx=st.get("resample_idx"), frame=st.get("frame"))
 
-    _CUT_SPLIT = {"auto": 0, "none": 1, "all": 2, "tail": 3}
+    _CUT_SPLIT = {"auto": 0, "none": 1, "all": 2, "tail": 3, "chunks": 4}
 
     def set_obs_cutoff(self, on=True, stats: bool = False, split: str | None = None):
         """Run the observation GP with the model's kernel-value cutoff (GPMDM.enable_obs_cutoff,
@@ -549,7 +549,7 @@ class GPMDM_PF:
         the reach it measured on its last frame is below its break-even against the dense
         kernel, else the dense kernel (re-measured at least every 8 frames; one-rank filters,
         gpmdm_pf_set_obs_cutoff mode 3); ``stats`` also counts the MFMA groups run
-        (obs_cutoff_stats; not with "auto"); ``split`` ("auto" default, "none", "all", "tail")
+        (obs_cutoff_stats; not with "auto"); ``split`` ("auto" default, "none", "all", "tail", "chunks")
         schedules the particle tiles run as two workgroups each (gpmdm_pf_set_obs_cutoff_split;
         the same results under every policy).  Between frames only."""
         if split is not None and split not in self._CUT_SPLIT:

@@ -406,20 +406,25 @@ int gpmdm_pf_set_obs_cutoff(gpmdm_pf_t pf, int mode);
  * travel with the frame's read-out, so the choice is a function of the filter's own
  * trajectory (deterministic).  Single-rank filters and banks whose read-outs are mapped (up
  * to ~800 filters) with more than 1024 particles per filter; others run mode 1 (a rank-local
- * choice would make a particle's result depend on its rank).  gpmdm_pf_obs_cutoff_auto: did
- * the last frame run the cutoff, and the last measured fraction (< 0: none yet). */
+ * choice would make a particle's result depend on its rank).  Mode 1 filters of that kind
+ * count the same way (for the split policy below).  gpmdm_pf_obs_cutoff_auto: did the last
+ * frame run the cutoff, and the last measured fraction (< 0: none yet). */
 int gpmdm_pf_obs_cutoff_auto(gpmdm_pf_t pf, int* last_cut, double* fraction);
 int gpmdm_pf_obs_cutoff_stats(gpmdm_pf_t pf, int64_t* run, int64_t* dense, int reset, void* stream);
 /* Scheduling of the cutoff kernel's particle tiles (results are identical under every
- * policy): a split tile runs as two workgroups.  GPMDM_CUT_SPLIT_AUTO (default): every tile
- * when the launch is at most two rounds of resident workgroups or its last round holds at
+ * policy): a split tile runs as two workgroups.  GPMDM_CUT_SPLIT_AUTO (default): the
+ * _CHUNKS grid below when the filter's last measured fraction (modes 1 and 3, above) is at
+ * least 0.5; otherwise every tile when the launch is at most two rounds of resident workgroups or its last round holds at
  * most an eighth of a round, none at whole rounds, otherwise the tiles of the last round
- * (measured, DESIGN.md §3 "The grid's tail"); _NONE, _ALL, _TAIL (the last round's tiles).
- * Between frames only. */
+ * (measured, DESIGN.md §3 "The grid's tail"); _NONE, _ALL, _TAIL (the last round's tiles);
+ * _CHUNKS: every 32-tile chunk of every tile's list its own workgroup, the chunks at the
+ * lists' ends first (the dense kernel's heavy-first column blocks, for clouds that reach most
+ * K-steps).  Between frames only. */
 #define GPMDM_CUT_SPLIT_AUTO 0
 #define GPMDM_CUT_SPLIT_NONE 1
 #define GPMDM_CUT_SPLIT_ALL 2
 #define GPMDM_CUT_SPLIT_TAIL 3
+#define GPMDM_CUT_SPLIT_CHUNKS 4
 int gpmdm_pf_set_obs_cutoff_split(gpmdm_pf_t pf, int policy);
 
 /* Failure detection.  The filter keeps the reference's arithmetic: a

@@ -210,7 +210,7 @@ def test_cutoff_split_policies_bitwise(m2c, P):
     zs = data.observation_stream(6, seed=1)
     T = torch.tensor(synthetic.markov_matrix(2))
     out = {}
-    for split in ("none", "tail", "all", "auto"):
+    for split in ("none", "tail", "all", "auto", "chunks"):
         torch.manual_seed(4)                 # (the initial cloud)
         pf = GPMDM_PF(m2c, T, P, rng="philox", seed=11, obs_cutoff=True)
         pf.set_obs_cutoff(True, split=split)
@@ -220,8 +220,49 @@ def test_cutoff_split_policies_bitwise(m2c, P):
             out[split].append(pf.export_state())
     with pytest.raises(ValueError):
         pf.set_obs_cutoff(True, split="half")
-    for split in ("tail", "all", "auto"):
+    for split in ("tail", "all", "auto", "chunks"):
         for k in range(4):
+            for key in ("states", "classes", "ll", "log_w", "resample_idx"):
+                assert np.array_equal(out["none"][k][key], out[split][k][key]), (split, k, key)
+
+
+def test_cutoff_chunk_grid_on_a_spread_cloud_bitwise(m2c):
+    """A cloud of 2000 distinct ancestors (the bench's --cutoff-spread cloud, 0.2 l): the
+    default split policy measures the reach on its first frame (mode 1 counts like AUTO) and
+    takes the chunk grid on the second (reach >= 0.5; the resampled cloud then collapses and
+    the third frame goes back to whole tiles); every frame is bitwise the whole-tile
+    scheduling's (split="none") and the explicit chunk grid's (split="chunks")."""
+    from gpmdm_amd import GPMDM_PF, synthetic
+    P = 100_000
+    data = synthetic.make_sequences(2, 5, 200, 62, 3, seed=0)
+    zs = data.observation_stream(6, seed=1)
+    T = torch.tensor(synthetic.markov_matrix(2))
+    X = m2c.X.detach().cpu().numpy()
+    N, d = X.shape
+    ell = np.exp(m2c.y_log_lengthscales.detach().cpu().numpy())
+    cls_of = np.concatenate([np.full(m2c.get_X_for_class(c).shape[0], c) for c in range(2)])
+    g = np.random.RandomState(23)
+    anc = np.sort(g.choice(N, 2000, replace=False))
+    g.shuffle(anc)
+    owner = anc[(np.arange(P) * anc.size) // P]
+    states = np.ascontiguousarray(X[owner] + 0.2 * ell[None, :] * g.randn(P, d))
+    classes = cls_of[owner].astype(np.int64)
+    zero, unif = np.zeros(P), np.full(P, 1.0 / P)
+    out, fr = {}, {}
+    for split in ("none", "auto", "chunks"):
+        pf = GPMDM_PF(m2c, T, P, rng="philox", seed=11, obs_cutoff=True)
+        pf.set_obs_cutoff(True, split=split)
+        pf.load_state(states, classes, ll=zero, log_w=zero, w=unif, frame=7)
+        out[split] = []
+        for k in range(3):
+            pf.update(zs[k])
+            pf.class_probabilities()
+            out[split].append(pf.export_state())
+            if k == 0:              # the reach the second frame's split choice reads
+                fr[split] = pf.obs_cutoff_auto()["fraction_run"]
+    assert fr["auto"] is not None and fr["auto"] >= 0.5, fr
+    for split in ("auto", "chunks"):
+        for k in range(3):
             for key in ("states", "classes", "ll", "log_w", "resample_idx"):
                 assert np.array_equal(out["none"][k][key], out[split][k][key]), (split, k, key)
 
@@ -315,8 +356,9 @@ def test_cutoff_vs_dense_other_latent_dims(synth_cut):
 
 
 def test_cutoff_logical_shards_other_latent_dims(synth_cut):
-    """4 logical shards of a d = 5 / d = 12 cutoff filter (another particle tiling) are bitwise
-    the one-rank cutoff filter over 3 frames."""
+    """4 logical shards of a d = 5 / d = 12 cutoff filter (another particle tiling; shards 0 and
+    2 with every list chunk its own workgroup, split="chunks") are bitwise the one-rank cutoff
+    filter over 3 frames."""
     from gpmdm_amd import GPMDM_PF
     d, m, T, Y = synth_cut
     P, world = 6_007, 4
@@ -326,6 +368,8 @@ def test_cutoff_logical_shards_other_latent_dims(synth_cut):
     for r in range(world):
         torch.manual_seed(4)
         ranks.append(GPMDM_PF(m, T, P, rng="philox", seed=91, shard=(world, r), obs_cutoff=True))
+        if r % 2 == 0:
+            ranks[-1].set_obs_cutoff(True, split="chunks")
     for k in range(3):
         z = np.ascontiguousarray(np.asarray(Y[60 + 3 * k], dtype=np.float64))
         ref.update(z)

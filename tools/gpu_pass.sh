@@ -16,6 +16,8 @@
 #        at each config, the config-2 cutoff line, and the bits of a 5-frame cutoff trajectory)
 #   bash tools/gpu_pass.sh cutoff-pmc <tag>
 #        PMC passes of the config-2 bench with its cutoff line (dense and cutoff kernels)
+#   bash tools/gpu_pass.sh spread-split <tag> [spread] [policies...]
+#        the cutoff on a spread cloud at configs 2 / 3 / 5 under each tile scheduling policy
 #   bash tools/gpu_pass.sh spread-pmc <tag> [config] [spread]
 #        PMC passes of one dense and one cutoff launch from a spread cloud (default config 5, 0.2 l)
 #   bash tools/gpu_pass.sh configs <tag> [configs...]
@@ -128,6 +130,19 @@ cutoff-pmc)
   python tools/pmc_summary.py $out/pmc --commit "$commit" \
     --command "bench.py --steps 2 --warmup 1 --no-cpu-baseline --spread-steps 0 --replay-steps 0 --no-nodedup --cutoff-steps 2" \
     --out $out/pmc_summary.json > $out/pmc_summary.txt 2>&1 || { echo "pmc summary failed"; exit 1; }
+  ;;
+spread-split)
+  # the cutoff's tile scheduling policies on spread clouds: spread-split <tag> <spread> <policies...>
+  sp=${1:-0.2}; shift
+  for c in 2 3 5; do
+    for pol in ${*:-auto chunks}; do
+      lim=300; [ "$c" = 5 ] && lim=600
+      timeout -k 10 $lim python -u bench.py --config $c --cutoff-spread --no-cpu-baseline --cutoff-spread-at $sp \
+          --cutoff-spread-reps 2 --cutoff-split $pol > $out/spread_c${c}_$pol.json 2> $out/spread_c${c}_$pol.err \
+        || { echo "spread c$c $pol failed"; tail -8 $out/spread_c${c}_$pol.err; exit 1; }
+      python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[2], [(r['spread_ell'], round(r['cutoff_obs_launch_ms'],3), round(r['dense_obs_launch_ms'],3), round(r['mfma_groups_run_fraction'],3), round(r['executed_frac_of_peak'],3)) for r in d['cutoff_spread']['rows']])" $out/spread_c${c}_$pol.json "c$c $pol"
+    done
+  done
   ;;
 spread-pmc)
   # PMC passes of one spread-cloud dense + cutoff launch pair: spread-pmc <tag> <config> [spread]
