@@ -97,10 +97,9 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
   // the workgroup's particle tile and part: whole tiles first, then the split tiles' second
   // parts (the longer ones in the balanced split's usual case), then their first parts
   int tile = (int)blockIdx.x, part = -1;                      // -1: the whole tile
-  int cfe = 0;                                                // chunk grid: chunk from the list's end
   if (prm.chunk_grid) {
-    cfe = tile / prm.n_split;
-    tile -= cfe * prm.n_split;
+    part = 2 + tile / prm.n_split;
+    tile -= (part - 2) * prm.n_split;
   } else if (tile >= prm.n_whole) {
     const int r = tile - prm.n_whole;
     part = r < prm.n_split ? 1 : 0;
@@ -197,21 +196,19 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
   // the chunks [c_lo, c_hi) of the tile list this workgroup runs (none: a second part of a
   // tile below two chunks; no early exit, which costs the K loop registers)
   int c_lo = 0, c_hi = (n_tiles + TPC - 1) / TPC;
-  if (prm.chunk_grid) {
-    // chunk c = nc - 1 - cfe alone: chunk 0 as a split tile's first part (q, S and the split
-    // record (n_act, 1)), a later one as a second part writing its entries; none past the list
-    const int c = c_hi - 1 - cfe;
-    part = c == 0 ? 0 : 1;
-    c_lo = c < 0 ? 0 : c;
-    c_hi = c < 0 ? 0 : c + 1;
-    if (c == 0 && tid == 0) prm.split[tile] = make_int2(n_act, 1);
-  } else if (part >= 0) {
-    const int cs = __builtin_amdgcn_readfirstlane(cutoff_split_chunk(n_act, prm.T_M, TPC));
+  if (part >= 0) {
+    // chunk grid (part 2 + cfe): chunk c = nc - 1 - cfe alone, as a split at c* = 1 -- chunk 0
+    // the first part, a later one a second part; none past the list
+    const bool cg = part >= 2;
+    const int c = c_hi - 1 - (part - 2);
+    const int cs = cg ? 1 : __builtin_amdgcn_readfirstlane(cutoff_split_chunk(n_act, prm.T_M, TPC));
+    if (cg) part = c == 0 ? 0 : 1;
     if (part == 0) {
       c_hi = cs;
       if (tid == 0) prm.split[tile - prm.n_whole] = make_int2(n_act, cs);
     } else {
-      c_lo = cs;
+      c_lo = cg ? (c < 0 ? c_hi : c) : cs;
+      if (cg && c >= 0) c_hi = c + 1;
     }
   }
   // (the second part's partials: list entry i of particle m at part[(i - r0) ld + o], r0 the
