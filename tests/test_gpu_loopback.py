@@ -54,10 +54,10 @@ def _assert_same(ref_out, ref_state, out, pf, what):
         assert np.array_equal(ref_state[key], st[key]), f"{what}: {key}"
 
 
-def _reference(m, T, P, rng, resample, draws=None):
+def _reference(m, T, P, rng, resample, draws=None, cutoff=False):
     from gpmdm_amd import GPMDM_PF
     torch.manual_seed(5)
-    pf = GPMDM_PF(m, T, P, rng=rng, seed=21 if rng == "philox" else None, resample=resample)
+    pf = GPMDM_PF(m, T, P, rng=rng, seed=21 if rng == "philox" else None, resample=resample, obs_cutoff=cutoff)
     out = []
     for k in range(FRAMES):
         if draws is None:
@@ -88,7 +88,7 @@ def test_devices_loopback_is_bitwise_one_rank(m2, R, rng, resample):
     _assert_same(ref_out, ref_state, out, pf, f"devices R={R} {rng} {resample}")
 
 
-def _threaded(m, T, P, R, rng, resample, pad, draws=None):
+def _threaded(m, T, P, R, rng, resample, pad, draws=None, cutoff=False, splits=None):
     """R filters of shard=(R, r), each on a thread and a stream of its own, exchanging
     through loopback communicators; returns each rank's read-outs and its filter."""
     from gpmdm_amd import GPMDM_PF
@@ -97,7 +97,9 @@ def _threaded(m, T, P, R, rng, resample, pad, draws=None):
     ranks = []
     for r in range(R):
         torch.manual_seed(5)
-        pf = GPMDM_PF(m, T, P, rng=rng, seed=21, resample=resample, shard=(R, r))
+        pf = GPMDM_PF(m, T, P, rng=rng, seed=21, resample=resample, shard=(R, r), obs_cutoff=cutoff)
+        if splits:
+            pf.set_obs_cutoff(True, split=splits[r % len(splits)])
         pf.set_comm(comms[r], pad_rows=pad)
         ranks.append(pf)
     outs = [[] for _ in range(R)]
@@ -156,6 +158,27 @@ def test_threaded_ranks_loopback_replay_draws(m2, R):
         _assert_same(ref_out, ref_state, outs[r], ranks[r], f"replay rank {r}/{R}")
     del ranks
     comms.destroy()
+
+
+@pytest.mark.parametrize("R", [2, 4])
+def test_threaded_ranks_loopback_obs_cutoff(m2, R):
+    """The opt-in observation cutoff through the library's exchange: R threaded ranks with
+    obs_cutoff=True, their particle tiles scheduled by different policies (whole tiles, the
+    chunk grid, every tile split), bitwise the one-rank cutoff filter (the flush is per value,
+    so a particle's likelihood does not depend on its tile-mates or its rank)."""
+    T = torch.tensor([[0.9, 0.1], [0.1, 0.9]], dtype=torch.float64)
+    P = 10_007
+    m2.enable_obs_cutoff(True)
+    try:
+        ref_out, ref_state = _reference(m2, T, P, "philox", "multinomial", cutoff=True)
+        outs, ranks, comms = _threaded(m2, T, P, R, "philox", "multinomial", False, cutoff=True,
+                                       splits=("auto", "chunks", "all"))
+        for r in range(R):
+            _assert_same(ref_out, ref_state, outs[r], ranks[r], f"cutoff rank {r}/{R}")
+        del ranks
+        comms.destroy()
+    finally:
+        m2.enable_obs_cutoff(False)
 
 
 def test_loopback_validates(m2):
