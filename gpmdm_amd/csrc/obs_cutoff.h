@@ -296,19 +296,17 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
     }
     const int last = cend - 1;
     const int npos = last < n_act ? last + 1 : n_act;          // list positions of this chunk
-    // The K-steps of list positions [kb0, kb0 + 128) in two VGPR windows (lane j of kw0 / kw1:
-    // position kb0 + j / kb0 + 64 + j): in the K loop a K-step is one v_readlane, not an LDS
-    // round trip in front of the B loads and the row staging
-    int kb0 = 0, kw0 = 0, kw1 = 0;
+    // The K-steps of list positions [kb0, kb0 + 64) in a VGPR window (lane j: position kb0 + j):
+    // in the K loop a K-step is one v_readlane, not an LDS round trip in front of the B loads
+    // and the row staging (refilled every 64 - RA positions)
+    int kb0 = 0, kw0 = 0;
     auto kwin = [&](int base) {
       kb0 = base;
-      const int x0 = min(base + lane, n_act - 1), x1 = min(base + 64 + lane, n_act - 1);
+      const int x0 = min(base + lane, n_act - 1);
       kw0 = x0 >= 0 ? (int)klist[x0] : 0;
-      kw1 = x1 >= 0 ? (int)klist[x1] : 0;
     };
-    auto katw = [&](int x) -> int {                          // kb0 <= x < kb0 + 128
-      const int o = x - kb0;
-      return o < 64 ? __builtin_amdgcn_readlane(kw0, o) : __builtin_amdgcn_readlane(kw1, o - 64);
+    auto katw = [&](int x) -> int {                          // kb0 <= x < kb0 + 64
+      return __builtin_amdgcn_readlane(kw0, x - kb0);
     };
     kwin(0);
     // B fragments of list position i, sub-steps 2h, 2h + 1, for every tile (one contiguous
@@ -325,7 +323,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
     auto step = [&](auto t0c, auto t1c, int i, bool retire, double (&bb)[4 * NTW]) {
       constexpr int T0 = decltype(t0c)::value, T1c = decltype(t1c)::value;
       const int buf = i & (ASL - 1);
-      if (i + RA >= kb0 + 128) kwin(i);                      // (uniform; every 124 positions)
+      if (i + RA >= kb0 + 64) kwin(i);                       // (uniform; every 60 positions)
       double v[GV];
       double rr[RPT];
       load_rows(katw(i + RA), rr);
@@ -396,7 +394,7 @@ __global__ __launch_bounds__(64 * NW, 2) void k_obs_cutoff(const CutoffParams pr
       }
     });
     for (; i < npos; ++i) {                                  // other waves' tiles: generate only
-      if (i + RA >= kb0 + 128) kwin(i);
+      if (i + RA >= kb0 + 64) kwin(i);
       double v[GV];
       double rr[RPT];
       load_rows(katw(i + RA), rr);
